@@ -1,0 +1,202 @@
+"""Benchmark: ODE steps/s x batch (replica-steps/s) on random 3-SAT n=10k m=42k (BASELINE.json).
+
+One "step" = one fixed-step Euler step (system.rs:141-154) of every replica of the batch.  Default
+workload: config 2's instance (random 3-SAT n=10 000, m=42 000, generator seed 1), fp32, B=1024 per
+GPU (the north star's roofline point), dt = 0.01, every replica forced to run all K steps
+(ODESAT_STOP_NONE).  Inputs are initialised on the device before the timed region.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
+GPU, each steps its own B replicas (global replica index rank*B + b) with no collective in the data
+path -- weak scaling; barrier + max-over-ranks timing via torch.distributed.
+
+Rank 0 prints ONE JSON line (see DESIGN.md §6 for every field).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--batch", type=int, default=1024, help="replicas per GPU")
+    p.add_argument("--config", default="config2")
+    p.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    p.add_argument("--chunk", type=int, default=0, help="replicas per chunk (0 = automatic)")
+    p.add_argument("--cpu-replicas", type=int, default=16)
+    p.add_argument("--cpu-steps", type=int, default=300)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--traffic", default=None, help="JSON with per-launch HBM bytes from the PMC passes")
+    p.add_argument("--extra-batch", type=int, default=256, help="also time this B (configs[1]); 0 = off")
+    return p.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as td
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        td.init_process_group(backend=backend)
+        dist = td
+    return world, rank, local, dist
+
+
+def barrier_sync(dist, solver, local):
+    """Device sync (the solver's stream carries all of its work) + barrier across ranks.  At N = 1
+    torch is never imported, so the process holds exactly one HIP runtime, the library's."""
+    solver.synchronize()
+    if dist is not None:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(local)
+        dist.barrier()
+
+
+def max_over_ranks(dist, x, local):
+    if dist is None:
+        return x
+    import torch
+    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def time_gpu(solver, steps, warmup, dist, local, profile):
+    from odesat_amd.system import ODESAT_STOP_NONE
+    if warmup:
+        solver.simulate(dt=0.01, max_steps=warmup, stop=ODESAT_STOP_NONE)
+    solver.profile(profile)
+    barrier_sync(dist, solver, local)
+    t0 = time.perf_counter()
+    solver.simulate(dt=0.01, max_steps=steps, stop=ODESAT_STOP_NONE)
+    barrier_sync(dist, solver, local)
+    t1 = time.perf_counter()
+    ms, launches = solver.profile_read() if profile else (None, None)
+    solver.profile(False)
+    return t1 - t0, ms, launches
+
+
+def cpu_baseline(cp, var, neg, n, m, replicas, steps):
+    """Bounded sample of the same workload on the host: the f64 line-by-line oracle (the reference's
+    own precision and algorithm), 1 thread, `replicas` x `steps` fixed steps."""
+    import numpy as np
+
+    from oracle.oracle import Oracle, init_voltages
+    o = Oracle(cp, var, neg, n, "f64")
+    v = init_voltages(42, 0, replicas, n)
+    xs = np.tile(o.init_short_term_memory(), (replicas, 1))
+    xl = np.ones((replicas, m))
+    t0 = time.perf_counter()
+    o.batch_run(v, xs, xl, False, 1e-3, 0.01, steps, 0.001, nthreads=1)
+    dt = time.perf_counter() - t0
+    return {"value": replicas * steps / dt, "unit": "replica-steps/s", "cores": 1, "kind": "port",
+            "sample": f"C f64 oracle (line-by-line restatement of system.rs), 1 thread, {replicas} replicas x "
+                      f"{steps} fixed steps of the same n=10k m=42k instance ({dt:.1f} s)"}
+
+
+def main():
+    args = parse()
+    world, rank, local, dist = dist_setup(args)
+
+    from odesat_amd import cnf
+    from odesat_amd import workloads as wl
+    from odesat_amd.system import Solver
+
+    c = wl.CONFIGS[args.config]
+    n, m = c["n"], c["m"]
+    var, neg = wl.random_ksat(n, m, c["k"], c["seed"])
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    f = cnf.CNFFormula.from_arrays(cp, v_, n_, n)
+    B = args.batch
+
+    def run_batch(batch, profile):
+        from odesat_amd import device_count
+        s = Solver(f, batch, args.dtype, device=local % max(1, device_count()))
+        if args.chunk:
+            s.set_chunk_replicas(args.chunk)
+        s.init_state(42, replica0=rank * batch)
+        wall, ms, launches = time_gpu(s, args.steps, args.warmup, dist, local, profile)
+        bytes_step = s.clause_kernel_bytes()
+        s.close()
+        return wall, ms, launches, bytes_step
+
+    wall, ms, launches, clause_bytes_step = run_batch(B, True)
+    wall_max = max_over_ranks(dist, wall, local)
+    total_replica_steps = B * world * args.steps
+    value = total_replica_steps / wall_max
+    ms_per_step = wall_max * 1e3 / args.steps
+
+    # roofline of the dominant kernel (k_clause): algorithmic bytes per launch / mean launch time
+    nlaunch = int(launches[0])
+    per_launch_s = ms[0] / 1e3 / nlaunch
+    per_launch_bytes = clause_bytes_step * args.steps / nlaunch
+    achieved = per_launch_bytes / per_launch_s / 1e9
+    traffic = None
+    if args.traffic and os.path.exists(args.traffic):
+        with open(args.traffic) as fh:
+            traffic = json.load(fh).get("clause_kernel_hbm_bytes_per_launch")
+    step_bytes = B * (8 * n + 16 * m) * (4 if args.dtype == "f32" else 8)  # algorithmic, per GPU-step
+
+    extra = None
+    if args.extra_batch and args.extra_batch != B:
+        w2, _, _, _ = run_batch(args.extra_batch, False)
+        w2 = max_over_ranks(dist, w2, local)
+        extra = {"batch_per_gpu": args.extra_batch,
+                 "value": args.extra_batch * world * args.steps / w2,
+                 "ms_per_step": w2 * 1e3 / args.steps}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(cp, v_, n_, n, m, args.cpu_replicas, args.cpu_steps)
+
+    if rank == 0:
+        out = {
+            "metric": "ODE steps/s x batch on random 3-SAT n=10k m=42k (replica-steps/s)",
+            "value": value,
+            "unit": "replica-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32" if args.dtype == "f32" else "fp64",
+            "data": "synthetic: seeded random 3-SAT instance + counter-RNG initial voltages (no dataset)",
+            "config": {"workload": f"{args.config}: random 3-SAT n={n} m={m} seed={c['seed']}, fixed-step "
+                                   f"Euler dt=0.01, all replicas stepped (no early exit)",
+                       "global_batch": B * world, "batch_per_gpu": B, "n": n, "m": m,
+                       "parallelism": f"replica-sharded x{world} (no collectives)"},
+            "roofline": {"bound": "hbm", "kernel": "k_clause_u (clause RHS + fused xs/xl update)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": per_launch_bytes,
+                         "mean_launch_us": per_launch_s * 1e6, "launches": nlaunch},
+            "step_kernels_ms": {"clause": ms[0], "variable": ms[1], "status": ms[2]},
+            "step_algorithmic_GBps": step_bytes * args.steps / wall / 1e9,
+            "cpu_baseline": cpu,
+            "extra_batch": extra,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

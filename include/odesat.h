@@ -1,0 +1,163 @@
+/*
+ * odesat.h -- C ABI of libodesat_hip.so, the MI355X-native replacement for odesat's per-step ODE
+ * integrator (reference: AHartNtkn/odesat @ 2024-10-24, Rust).
+ *
+ * The reference has no FFI: its boundary is the Rust library API re-exported by src/lib.rs:1-3
+ * (`pub mod cnf; pub mod stoch; pub mod system;`).  Each entry point below names the Rust function
+ * it replaces (file:line).  INTEGRATION.md shows the `extern "C"` block a maintainer would add to the
+ * Rust crate to bind it.
+ *
+ * Conventions
+ *   - Every `int` function returns ODESAT_OK (0) or a negative ODESAT_E* code; the message is in
+ *     odesat_last_error() (thread-local).  No exception crosses the ABI.  (The reference panics on
+ *     malformed input, cnf.rs:151,160, and aborts, Cargo.toml:24.)
+ *   - Host buffers are caller-owned and copied; device memory is library-owned.
+ *   - One odesat_solver per GPU, driven by one host thread.  Multi-GPU = N solvers on N threads or
+ *     processes (replicas shard with no collective).
+ *   - State arrays at the ABI are replica-major f64: v[B][n], xs[B][m], xl[B][m] -- one Rust
+ *     `State` (system.rs:6-11) per replica.  On the device the library keeps its own layout
+ *     (replica-innermost) in the solver's dtype (f32 or f64).
+ *   - Variables are the normalised 0-based indices of cnf.rs:206-219 (ascending renaming).
+ *   - No CPU fallback: every integrator call needs a gfx950 device and fails loudly otherwise.
+ */
+#ifndef ODESAT_H
+#define ODESAT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ODESAT_OK 0
+#define ODESAT_EINVAL -1   /* bad argument / malformed DIMACS */
+#define ODESAT_ENOMEM -2   /* host or device allocation failed */
+#define ODESAT_EDEVICE -3  /* HIP runtime error or no usable device */
+#define ODESAT_ESTATE -4   /* call not valid in the solver's current state */
+
+#define ODESAT_F32 0
+#define ODESAT_F64 1
+
+/* stop policies for odesat_simulate */
+#define ODESAT_STOP_EACH 0 /* batch (main.rs:278-308): every replica runs until ITS allsat, then freezes */
+#define ODESAT_STOP_ANY 1  /* inter (system.rs:291,308,329,346): all replicas stop at the first step any is allsat */
+#define ODESAT_STOP_NONE 2 /* benchmark: run exactly max_steps on every replica, no sat test acts */
+
+typedef struct odesat_cnf odesat_cnf;       /* host-side parsed formula (cnf.rs:53-57 CNFFormula) */
+typedef struct odesat_solver odesat_solver; /* device-resident formula + B replica states */
+
+const char *odesat_last_error(void);
+const char *odesat_version(void);
+/* number of visible HIP devices (0 on a machine without a GPU) */
+int odesat_device_count(int *count);
+
+/* ------------------------------------------------------------------ loader (cnf.rs) ---------- */
+
+/* cnf.rs:138-172 parse_dimacs_format (+ CNFFormula::new, cnf.rs:60-77).  Lines starting with 'c'
+ * are skipped, "p cnf N ..." sets varnum, every other line is a clause read up to the token "0" (an
+ * empty line is an empty clause).  A token that is not an i32 gives ODESAT_EINVAL where the
+ * reference panics. */
+int odesat_cnf_parse(const char *text, size_t len, odesat_cnf **out);
+/* Build a formula from arrays: clause c owns [clause_ptr[c], clause_ptr[c+1]) of var/neg.
+ * varnum < 0 means "no header": varnum = number of distinct variables (cnf.rs:63-75). */
+int odesat_cnf_from_arrays(int64_t varnum, int64_t nclauses, const int64_t *clause_ptr,
+                           const int64_t *var, const uint8_t *neg, odesat_cnf **out);
+void odesat_cnf_free(odesat_cnf *cnf);
+int64_t odesat_cnf_varnum(const odesat_cnf *cnf);
+int64_t odesat_cnf_nclauses(const odesat_cnf *cnf);
+int64_t odesat_cnf_nliterals(const odesat_cnf *cnf);
+/* copy out the CSR (clause_ptr[m+1], var[L], neg[L]); any pointer may be NULL */
+int odesat_cnf_export(const odesat_cnf *cnf, int64_t *clause_ptr, int64_t *var, uint8_t *neg);
+/* cnf.rs:206-219 normalize_cnf_variables: distinct variables renamed 0..k-1 in ASCENDING order
+ * (declared deviation: the reference iterates a HashSet, a random order per run).  varnum is kept.
+ * old_names[k] (may be NULL, else capacity >= number of distinct variables) receives new -> old. */
+int odesat_cnf_normalize(const odesat_cnf *cnf, odesat_cnf **out, int64_t *old_names,
+                         int64_t *k_out);
+/* cnf.rs:246-264 evaluate_cnf: values[var] for var < nvalues, any other variable reads false.
+ * Returns 1 (satisfied), 0 (not), or a negative error. */
+int odesat_cnf_evaluate(const odesat_cnf *cnf, const uint8_t *values, int64_t nvalues);
+/* system.rs:361-372 init_short_term_memory: xs[c] = +1 if clause c has a negated literal, else -1 */
+int odesat_cnf_init_short_term_memory(const odesat_cnf *cnf, double *xs);
+
+/* ------------------------------------------------------------- integrator (system.rs) -------- */
+
+/* Upload a NORMALISED formula (every variable < varnum) for `batch` replicas on `device`.
+ * dtype = ODESAT_F32 (throughput mode) or ODESAT_F64 (the reference's precision).  The state is
+ * initialised to v = 0, xs = init_short_term_memory, xl = 1; use odesat_set_state or
+ * odesat_init_state before stepping. */
+int odesat_solver_create(int device, const odesat_cnf *normalized, int64_t batch, int dtype,
+                         odesat_solver **out);
+void odesat_solver_destroy(odesat_solver *s);
+int64_t odesat_solver_batch(const odesat_solver *s);
+int64_t odesat_solver_varnum(const odesat_solver *s);
+int64_t odesat_solver_nclauses(const odesat_solver *s);
+/* Device bytes held by the solver. */
+int64_t odesat_solver_device_bytes(const odesat_solver *s);
+
+/* Replace replicas [r0, r0+count) with caller states (replica-major f64; values are rounded to
+ * the solver dtype).  Marks those replicas active, first_sat_step = -1, adaptive dt = 0.01. */
+int odesat_set_state(odesat_solver *s, int64_t r0, int64_t count, const double *v,
+                     const double *xs, const double *xl);
+/* Device-side initial states for every replica b (global index replica0 + b):
+ * v[i] = counter RNG(seed, replica0 + b, i) ~ U[-1,1) (main.rs:171, 285, 353 with a reproducible
+ * generator), xs = init_short_term_memory (system.rs:361), xl = 1 (main.rs:173). */
+int odesat_init_state(odesat_solver *s, uint64_t seed, int64_t replica0);
+/* Copy replicas [r0, r0+count) back (replica-major f64; any pointer may be NULL). */
+int odesat_get_state(odesat_solver *s, int64_t r0, int64_t count, double *v, double *xs,
+                     double *xl);
+/* system.rs:238 / :355: assignment[i] = v[i] > 0 for replica r. */
+int odesat_get_assignment(odesat_solver *s, int64_t r, uint8_t *assignment);
+
+/* system.rs:25-91 compute_derivatives on every replica's current state (no state change).
+ * dv[B][n], dxs[B][m], dxl[B][m] (may be NULL), allsat[B] (may be NULL). */
+int odesat_compute_derivatives(odesat_solver *s, double zeta, double *dv, double *dxs,
+                               double *dxl, uint8_t *allsat);
+/* system.rs:141-154 euler_step_fixed on every replica; allsat[B] = pre-update result. */
+int odesat_euler_step_fixed(odesat_solver *s, double dt, double zeta, uint8_t *allsat);
+/* system.rs:111-139 euler_step on every replica with its own dt: dt[B] in/out (may be NULL: the
+ * solver's per-replica dt is used and kept); allsat[B] as returned by the reference. */
+int odesat_euler_step(odesat_solver *s, double tol, double *dt, double zeta, uint8_t *allsat);
+
+typedef struct {
+    int32_t adaptive;      /* 0: fixed step `dt` (system.rs:190-203); 1: adaptive (:204-234) */
+    int32_t stop;          /* ODESAT_STOP_EACH | ODESAT_STOP_ANY | ODESAT_STOP_NONE */
+    double tol;            /* adaptive tolerance (reference default 1e-3, system.rs:174) */
+    double dt;             /* fixed step size; adaptive starts every replica at 0.01 (:205) */
+    double zeta;           /* learning rate; < 0 = density heuristic (system.rs:164-173) */
+    int64_t max_steps;     /* > 0 (the reference's None = unbounded is refused) */
+    int32_t poll_interval; /* steps between host polls of the stop condition (0 = default 32) */
+    int32_t reserved;
+} odesat_params;
+
+/* system.rs:156-239 (simulate) applied to every replica at once, or :241-359 (simulate_inter)
+ * with stop = ODESAT_STOP_ANY.  Replicas continue from their current state.
+ *   first_sat_step[B] : 0-based step at which the replica was allsat, -1 if never (may be NULL)
+ *   steps_done[B]     : euler steps applied to the replica in this call (may be NULL)
+ *   dt_out[B]         : final adaptive dt per replica (may be NULL)
+ *   steps_run         : steps launched (may be NULL)
+ * Declared deviation: adaptive STOP_ANY uses a per-replica dt; the reference threads ONE dt
+ * serially through the replicas (system.rs:314-326), which cannot run in parallel. */
+int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t *first_sat_step,
+                    int64_t *steps_done, double *dt_out, int64_t *steps_run);
+
+/* Block until all work queued by the solver is done. */
+int odesat_synchronize(odesat_solver *s);
+
+/* --------------------------------------------------------------- measurement ----------------- */
+
+/* When enabled, odesat_simulate brackets every launch with HIP events on the solver's stream.
+ * odesat_profile_read returns, per kernel class (0 = clause kernel, 1 = variable kernel, 2 = status
+ * kernel), the summed device milliseconds and the launch count since the last reset. */
+int odesat_profile_enable(odesat_solver *s, int enable);
+int odesat_profile_read(odesat_solver *s, double *ms /*[3]*/, int64_t *launches /*[3]*/);
+/* Algorithmic bytes per launch of the clause kernel over the whole batch (roofline). */
+int64_t odesat_clause_kernel_bytes(const odesat_solver *s);
+/* Tuning: replicas per chunk (0 = automatic) -- the batch is stepped chunk by chunk so the
+ * contribution buffer of one chunk stays resident in the Infinity Cache. */
+int odesat_set_chunk_replicas(odesat_solver *s, int64_t replicas);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

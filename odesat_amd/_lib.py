@@ -1,0 +1,115 @@
+"""ctypes binding of libodesat_hip.so (include/odesat.h).
+
+The product path: every call goes to the in-tree HIP library; there is no CPU fallback.  If the
+library is missing, import of the integrator fails loudly with the build command to run.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libodesat_hip.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "odesat.h")
+
+ODESAT_OK, ODESAT_EINVAL, ODESAT_ENOMEM, ODESAT_EDEVICE, ODESAT_ESTATE = 0, -1, -2, -3, -4
+ODESAT_F32, ODESAT_F64 = 0, 1
+ODESAT_STOP_EACH, ODESAT_STOP_ANY, ODESAT_STOP_NONE = 0, 1, 2
+
+
+class OdesatError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"odesat error {code}: {msg}")
+        self.code = code
+
+
+class Params(C.Structure):
+    _fields_ = [("adaptive", C.c_int32), ("stop", C.c_int32), ("tol", C.c_double), ("dt", C.c_double),
+                ("zeta", C.c_double), ("max_steps", C.c_int64), ("poll_interval", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+_P = C.c_void_p
+_i64 = C.c_int64
+_dp = C.POINTER(C.c_double)
+_u8p = C.POINTER(C.c_uint8)
+_i64p = C.POINTER(C.c_int64)
+
+# name -> (restype, argtypes); kept in sync with include/odesat.h (tests/test_abi.py checks)
+SIGNATURES = {
+    "odesat_last_error": (C.c_char_p, []),
+    "odesat_version": (C.c_char_p, []),
+    "odesat_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "odesat_cnf_parse": (C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(_P)]),
+    "odesat_cnf_from_arrays": (C.c_int, [_i64, _i64, _i64p, _i64p, _u8p, C.POINTER(_P)]),
+    "odesat_cnf_free": (None, [_P]),
+    "odesat_cnf_varnum": (_i64, [_P]),
+    "odesat_cnf_nclauses": (_i64, [_P]),
+    "odesat_cnf_nliterals": (_i64, [_P]),
+    "odesat_cnf_export": (C.c_int, [_P, _i64p, _i64p, _u8p]),
+    "odesat_cnf_normalize": (C.c_int, [_P, C.POINTER(_P), _i64p, _i64p]),
+    "odesat_cnf_evaluate": (C.c_int, [_P, _u8p, _i64]),
+    "odesat_cnf_init_short_term_memory": (C.c_int, [_P, _dp]),
+    "odesat_solver_create": (C.c_int, [C.c_int, _P, _i64, C.c_int, C.POINTER(_P)]),
+    "odesat_solver_destroy": (None, [_P]),
+    "odesat_solver_batch": (_i64, [_P]),
+    "odesat_solver_varnum": (_i64, [_P]),
+    "odesat_solver_nclauses": (_i64, [_P]),
+    "odesat_solver_device_bytes": (_i64, [_P]),
+    "odesat_set_state": (C.c_int, [_P, _i64, _i64, _dp, _dp, _dp]),
+    "odesat_init_state": (C.c_int, [_P, C.c_uint64, _i64]),
+    "odesat_get_state": (C.c_int, [_P, _i64, _i64, _dp, _dp, _dp]),
+    "odesat_get_assignment": (C.c_int, [_P, _i64, _u8p]),
+    "odesat_compute_derivatives": (C.c_int, [_P, C.c_double, _dp, _dp, _dp, _u8p]),
+    "odesat_euler_step_fixed": (C.c_int, [_P, C.c_double, C.c_double, _u8p]),
+    "odesat_euler_step": (C.c_int, [_P, C.c_double, _dp, C.c_double, _u8p]),
+    "odesat_simulate": (C.c_int, [_P, C.POINTER(Params), _i64p, _i64p, _dp, _i64p]),
+    "odesat_synchronize": (C.c_int, [_P]),
+    "odesat_profile_enable": (C.c_int, [_P, C.c_int]),
+    "odesat_profile_read": (C.c_int, [_P, _dp, _i64p]),
+    "odesat_clause_kernel_bytes": (_i64, [_P]),
+    "odesat_set_chunk_replicas": (C.c_int, [_P, _i64]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load the in-tree libodesat_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OdesatError(ODESAT_EDEVICE, f"{LIB_PATH} not built: run `make -C odesat_amd/csrc` "
+                                              "or `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if isinstance(rc, int) and rc < 0:
+        msg = lib().odesat_last_error()
+        raise OdesatError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def dptr(a):
+    return None if a is None else a.ctypes.data_as(_dp)
+
+
+def u8ptr(a):
+    return None if a is None else a.ctypes.data_as(_u8p)
+
+
+def i64ptr(a):
+    return None if a is None else a.ctypes.data_as(_i64p)
+
+
+def device_count() -> int:
+    c = C.c_int(0)
+    check(lib().odesat_device_count(C.byref(c)))
+    return c.value

@@ -1,0 +1,73 @@
+"""The C ABI boundary (include/odesat.h) -- CPU checks: the library loads, exports every declared
+symbol, the Python binding covers them, and integrator calls fail loudly without a GPU."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from odesat_amd import _lib
+from odesat_amd.cnf import parse_dimacs_format
+
+HEADER = _lib.HEADER
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(odesat_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("odesat_cnf_parse", "odesat_solver_create", "odesat_compute_derivatives",
+                 "odesat_euler_step", "odesat_euler_step_fixed", "odesat_simulate", "odesat_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [n for n in declared_functions() if n not in exported]
+    assert not missing, missing
+
+
+def test_binding_covers_header():
+    assert sorted(_lib.SIGNATURES) == declared_functions()
+
+
+def test_library_loads_and_resolves():
+    L = _lib.lib()
+    for name in declared_functions():
+        assert getattr(L, name) is not None
+    assert b"gfx950" in L.odesat_version()
+
+
+def test_no_torch_types_in_the_abi():
+    text = open(HEADER).read()
+    assert "torch" not in text.lower().replace("no torch", "") and "at::" not in text
+
+
+def test_solver_fails_loudly_without_gpu():
+    if _lib.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    from odesat_amd.cnf import normalize_cnf_variables
+    _, f = normalize_cnf_variables(parse_dimacs_format("p cnf 3 1\n1 2 3 0\n"))
+    h = C.c_void_p()
+    rc = _lib.lib().odesat_solver_create(0, f.handle, 4, 0, C.byref(h))
+    assert rc == _lib.ODESAT_EDEVICE
+    assert b"no HIP device" in _lib.lib().odesat_last_error()
+    from odesat_amd.system import Solver
+    with pytest.raises(_lib.OdesatError):
+        Solver(f, 4)
+
+
+def test_product_does_not_import_the_oracle():
+    root = os.path.dirname(_lib._HERE)
+    for dirpath, _, files in os.walk(os.path.join(root, "odesat_amd")):
+        for fn in files:
+            if fn.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
+                src = open(os.path.join(dirpath, fn)).read()
+                assert "oracle" not in re.sub(r"#.*|//.*", "", src).replace("oracle/", ""), fn

@@ -1,0 +1,338 @@
+"""GPU parity: the HIP integrator (through the C ABI) against the CPU oracle, on the same seeded
+inputs.  Bar: BIT-EXACT states (v, xs, xl), sat steps and assignments, in f64 (the reference's
+precision) and in f32 (vs the oracle's f32 restatement with the same operation order).  At
+BASELINE.json's full size (n=10k, m=42k, B=1024) a subset of replicas is checked bit for bit and the
+rest through size-independent properties.  f32-vs-f64 is compared with a stated tolerance."""
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle, init_voltages
+from odesat_amd import cnf
+from odesat_amd import workloads as wl
+from odesat_amd.system import (ODESAT_STOP_ANY, ODESAT_STOP_EACH, ODESAT_STOP_NONE, Solver, State,
+                               compute_derivatives, euler_step, euler_step_fixed, simulate, simulate_inter)
+from tests.common import FIXTURES, golden, oracle_formula, read
+
+pytestmark = pytest.mark.gpu
+
+T_OF = {"f64": np.float64, "f32": np.float32}
+
+
+def same(a, b):
+    """Bit-equal, except that NaN payloads may differ between the CPU and the GPU."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    if a.shape != b.shape:
+        return False
+    na, nb = np.isnan(a), np.isnan(b)
+    if not np.array_equal(na, nb):
+        return False
+    return np.array_equal(a[~na].view(np.uint64), b[~nb].view(np.uint64))
+
+
+def product_formula(name):
+    _, f = cnf.normalize_cnf_variables(cnf.parse_dimacs_format(read(name)))
+    return f
+
+
+def oracle_for(name, prec):
+    f = oracle_formula(name)
+    return f, Oracle(f.clause_ptr, f.var, f.neg, f.varnum, prec)
+
+
+def init_states(o, B, seed=42, T=np.float64):
+    v = init_voltages(seed, 0, B, o.n).astype(T)
+    xs = np.tile(o.init_short_term_memory(), (B, 1)).astype(T)
+    xl = np.ones((B, o.m), T)
+    return v, xs, xl
+
+
+# --------------------------------------------------------------------------- single RHS / step ---
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("B", [1, 3, 64, 100])
+def test_compute_derivatives_bitexact(name, prec, B):
+    f, o = oracle_for(name, prec)
+    T = T_OF[prec]
+    v, xs, xl = init_states(o, B, T=T)
+    with Solver(product_formula(name), B, prec) as s:
+        s.init_state(42)
+        gv, gxs, gxl = s.get_state()
+        assert same(gv, v) and same(gxs, xs) and same(gxl, xl)  # device init == host oracle init
+        dv, dxs, dxl, allsat = s.compute_derivatives(0.001)
+    for b in range(B):
+        odv, odxs, odxl, osat, _ = o.compute_derivatives(v[b], xs[b], xl[b], T(0.001))
+        assert same(dv[b], odv) and same(dxs[b], odxs) and same(dxl[b], odxl)
+        assert allsat[b] == osat
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_hand_kat_on_gpu(prec):
+    import json
+    import os
+    from tests.common import GOLDEN
+    cases = json.load(open(os.path.join(GOLDEN, "kat_small.json")))["cases"]
+    T = T_OF[prec]
+    f = product_formula("small")
+    for case in cases:
+        y = State(np.array(case["v"]), np.ones(3), np.ones(3))
+        dy, allsat = compute_derivatives(y, f, 0.001, dtype=prec)
+        assert allsat == case["allsat"]
+        if "dv_renamed" in case and prec == "f64":
+            assert dy.v.tolist() == [eval(e) for e in case["dv_renamed"]]  # noqa: S307
+            assert dy.xs.tolist() == [eval(e) for e in case["dxs"]]  # noqa: S307
+            assert dy.xl.tolist() == [eval(e) for e in case["dxl"]]  # noqa: S307
+        if "after_v" in case:
+            sat = euler_step_fixed(y, f, case["dt"], 0.001, dtype=prec)
+            assert sat == case["allsat"]
+            want = [T(eval(e)) for e in case["after_v"]]  # noqa: S307
+            if prec == "f64":
+                assert y.v.tolist() == want
+                assert y.xs.tolist() == [eval(e) for e in case["after_xs"]]  # noqa: S307
+                assert y.xl.tolist() == [eval(e) for e in case["after_xl"]]  # noqa: S307
+
+
+@pytest.mark.parametrize("name", ["small", "easy", "rand200"])
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_single_steps_bitexact(name, prec):
+    f, o = oracle_for(name, prec)
+    T = T_OF[prec]
+    B = 5
+    v, xs, xl = init_states(o, B, T=T)
+    with Solver(product_formula(name), B, prec) as s:
+        s.init_state(42)
+        for k in range(3):  # fixed
+            allsat = s.euler_step_fixed(0.01, 0.001)
+            for b in range(B):
+                assert allsat[b] == o.euler_step_fixed(v[b], xs[b], xl[b], T(0.01), T(0.001))
+        gv, gxs, gxl = s.get_state()
+        assert same(gv, v) and same(gxs, xs) and same(gxl, xl)
+        dts = np.full(B, 0.01)
+        odt = [T(0.01)] * B
+        for k in range(3):  # adaptive, per-replica dt
+            allsat, dts = s.euler_step(1e-3, dts, 0.001)
+            for b in range(B):
+                sat, odt[b] = o.euler_step(v[b], xs[b], xl[b], T(1e-3), odt[b], T(0.001))
+                assert allsat[b] == sat
+                assert T(dts[b]) == T(odt[b])
+        gv, gxs, gxl = s.get_state()
+        assert same(gv, v) and same(gxs, xs) and same(gxl, xl)
+
+
+def test_reference_shaped_functions():
+    f = product_formula("easy")
+    _, o = oracle_for("easy", "f64")
+    v, xs, xl = init_states(o, 1)
+    y = State(v[0].copy(), xs[0].copy(), xl[0].copy())
+    sat, h = euler_step(y, f, 1e-3, 0.01, 0.001)
+    osat, oh = o.euler_step(v[0], xs[0], xl[0], 1e-3, 0.01, 0.001)
+    assert sat == osat and h == oh and same(y.v, v[0]) and same(y.xl, xl[0])
+
+
+# ---------------------------------------------------------------------- whole trajectories ---
+@pytest.mark.parametrize("name", FIXTURES)
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("mode", ["fixed", "adaptive"])
+def test_batch_trajectories_match_golden(name, prec, mode):
+    """odesat_simulate(STOP_EACH) == the reference's sequential restart loop (main.rs:278-308):
+    every replica runs to its own allsat (frozen after) or to the step limit, bit for bit."""
+    g = golden(name)
+    B, steps = int(g["B"]), int(g["steps"])
+    with Solver(product_formula(name), B, prec) as s:
+        s.init_state(int(g["seed"]))
+        r = s.simulate(adaptive=mode == "adaptive", dt=0.01, tol=1e-3, max_steps=steps, stop=ODESAT_STOP_EACH,
+                       poll_interval=7)
+        v, xs, xl = s.get_state()
+    key = f"{prec}_{mode}_"
+    assert np.array_equal(r["steps_done"], g[key + "steps"])
+    assert np.array_equal(r["first_sat_step"] >= 0, g[key + "sat"])
+    assert np.array_equal(r["first_sat_step"][g[key + "sat"]], g[key + "steps"][g[key + "sat"]] - 1)
+    assert same(v, g[key + "v"]) and same(xs, g[key + "xs"]) and same(xl, g[key + "xl"])
+    if mode == "adaptive":
+        assert np.array_equal(r["dt"].astype(T_OF[prec]), g[key + "dt"].astype(T_OF[prec]))
+
+
+def test_easy_solves_and_evaluates():
+    """End to end on the reference's SAT fixture: the GPU assignment satisfies the ORIGINAL formula."""
+    text = read("easy")
+    f = cnf.parse_dimacs_format(text)
+    mapping, nf = cnf.normalize_cnf_variables(f)
+    for prec in ("f64", "f32"):
+        with Solver(nf, 8, prec) as s:
+            s.init_state(7)
+            r = s.simulate(dt=0.1, max_steps=5000, stop=ODESAT_STOP_EACH)
+            winners = np.flatnonzero(r["first_sat_step"] >= 0)
+            assert len(winners) > 0
+            a = s.get_assignment(int(winners[0]))
+        vals = cnf.map_values_by_indices(mapping, a)
+        assert cnf.evaluate_cnf(vals, f)
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_inter_fixed_matches_oracle(prec):
+    """STOP_ANY == simulate_inter (fixed step): same stop step, winner and EVERY replica's state."""
+    f, o = oracle_for("easy", prec)
+    T = T_OF[prec]
+    B = 6
+    v, xs, xl = init_states(o, B, T=T)
+    t, win, assign, _ = o.simulate_inter(v, xs, xl, dt=T(0.01), steps=4000)
+    with Solver(product_formula("easy"), B, prec) as s:
+        s.init_state(42)
+        r = s.simulate(dt=0.01, max_steps=4000, stop=ODESAT_STOP_ANY, poll_interval=16)
+        gv, gxs, gxl = s.get_state()
+    sat = np.flatnonzero(r["first_sat_step"] >= 0)
+    assert len(sat) and int(sat[0]) == win and r["first_sat_step"][win] == t - 1
+    assert np.all(r["steps_done"] == t)
+    assert same(gv, v) and same(gxs, xs) and same(gxl, xl)
+
+
+def test_inter_adaptive_per_replica_dt_matches_oracle():
+    """Declared deviation: adaptive STOP_ANY uses per-replica dt (oracle shared_dt=False)."""
+    f, o = oracle_for("easy", "f64")
+    B = 4
+    v, xs, xl = init_states(o, B)
+    t, win, _, dts = o.simulate_inter(v, xs, xl, tol=1e-3, steps=3000, shared_dt=False)
+    with Solver(product_formula("easy"), B, "f64") as s:
+        s.init_state(42)
+        r = s.simulate(adaptive=True, tol=1e-3, max_steps=3000, stop=ODESAT_STOP_ANY)
+        gv, gxs, gxl = s.get_state()
+    assert int(np.flatnonzero(r["first_sat_step"] >= 0)[0]) == win
+    assert same(gv, v) and same(gxs, xs) and same(gxl, xl) and same(r["dt"], dts)
+
+
+def test_simulate_inter_function():
+    f = product_formula("easy")
+    _, o = oracle_for("easy", "f64")
+    v, xs, xl = init_states(o, 3)
+    states = [State(v[b].copy(), xs[b].copy(), xl[b].copy()) for b in range(3)]
+    a = simulate_inter(states, f, step_size=0.01, steps=4000)
+    t, win, assign, _ = o.simulate_inter(v, xs, xl, dt=0.01, steps=4000)
+    assert np.array_equal(a, assign.astype(bool))
+    y = State(v[0].copy(), xs[0].copy(), xl[0].copy())
+    a1 = simulate(y, f, step_size=0.01, steps=50)
+    assert a1.dtype == bool and a1.shape == (f.varnum,)
+
+
+# ---------------------------------------------------------------------- edge cases ---------
+EDGE = {
+    "empty_clause": "p cnf 3 3\n1 -2 0\n\n2 3 0\n",
+    "unit_clauses_inf": "p cnf 3 4\n1 0\n-1 0\n2 -3 0\n3 0\n",
+    "duplicate_var_in_clause": "p cnf 3 2\n1 1 -2 0\n-1 2 2 3 0\n",
+    "unused_variables": "p cnf 8 2\n1 -2 0\n2 3 0\n",
+    "wide_clauses": "p cnf 7 3\n1 2 3 4 5 6 7 0\n-1 -2 -3 -4 -5 0\n6 -7 0\n",
+    "all_positive": "p cnf 3 2\n1 2 3 0\n1 -2 3 0\n",
+}
+
+
+@pytest.mark.parametrize("name", sorted(EDGE))
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("B", [2, 70])
+def test_edge_formulas(name, prec, B):
+    text = EDGE[name]
+    _, nf = cnf.normalize_cnf_variables(cnf.parse_dimacs_format(text))
+    cp, var, neg = nf.arrays()
+    o = Oracle(cp, var, neg, nf.varnum, prec)
+    T = T_OF[prec]
+    v, xs, xl = init_states(o, B, seed=3, T=T)
+    for b in range(B):
+        o.simulate(v[b], xs[b], xl[b], dt=T(0.05), steps=40, zeta=T(0.01))
+    with Solver(nf, B, prec) as s:
+        s.init_state(3)
+        s.simulate(dt=0.05, zeta=0.01, max_steps=40, stop=ODESAT_STOP_EACH)
+        gv, gxs, gxl = s.get_state()
+    assert same(gv, v) and same(gxs, xs) and same(gxl, xl)
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_out_of_range_initial_state_rigidity_term(prec):
+    """v outside [-1, 1] makes the rigidity term fire (R != 0) on the first RHS; kept bit-exact."""
+    _, nf = cnf.normalize_cnf_variables(cnf.parse_dimacs_format("p cnf 3 2\n1 2 0\n-2 3 0\n"))
+    cp, var, neg = nf.arrays()
+    o = Oracle(cp, var, neg, 3, prec)
+    T = T_OF[prec]
+    v = np.array([[2.0, 1.5, -3.0]], T)
+    xs = np.array([[0.5, 0.25]], T)
+    xl = np.array([[1.0, 3.0]], T)
+    odv, odxs, odxl, _, rf = o.compute_derivatives(v[0], xs[0], xl[0], T(0.1))
+    assert rf > 0
+    with Solver(nf, 1, prec) as s:
+        s.set_state(v, xs, xl)
+        dv, dxs, dxl, _ = s.compute_derivatives(0.1)
+    assert same(dv[0], odv) and same(dxs[0], odxs) and same(dxl[0], odxl)
+
+
+def test_set_state_partial_range_and_readback():
+    f = product_formula("rand200")
+    rng = np.random.default_rng(1)
+    with Solver(f, 130, "f64") as s:
+        s.init_state(5)
+        v0, xs0, xl0 = s.get_state()
+        nv = rng.uniform(-1, 1, (7, f.varnum))
+        s.set_state(nv, xs0[60:67], xl0[60:67], r0=60)
+        v1, _, _ = s.get_state()
+    assert same(v1[60:67], nv) and same(v1[:60], v0[:60]) and same(v1[67:], v0[67:])
+
+
+def test_chunking_does_not_change_results():
+    f = product_formula("rand200")
+    out = []
+    for chunk in (0, 64, 128):
+        with Solver(f, 256, "f32") as s:
+            s.set_chunk_replicas(chunk)
+            s.init_state(11)
+            s.simulate(dt=0.02, max_steps=30, stop=ODESAT_STOP_NONE)
+            out.append(s.get_state())
+    for o_ in out[1:]:
+        for a, b in zip(out[0], o_):
+            assert same(a, b)
+
+
+# ------------------------------------------------------------------------ f32 vs f64 ---------
+def test_f32_tracks_f64_on_short_horizon():
+    """Tolerance (stated): after 20 fixed steps of dt=0.01 from identical f32-representable
+    initial states, |v32 - v64| <= 1e-4 and |xl32 - xl64| <= 1e-4 * xl64 elementwise."""
+    f = product_formula("rand200")
+    res = {}
+    for prec in ("f32", "f64"):
+        with Solver(f, 16, prec) as s:
+            s.init_state(2)
+            v, xs, xl = s.get_state()
+            s.set_state(v.astype(np.float32).astype(np.float64), xs, xl)
+            s.simulate(dt=0.01, max_steps=20, stop=ODESAT_STOP_NONE)
+            res[prec] = s.get_state()
+    v32, xs32, xl32 = res["f32"]
+    v64, xs64, xl64 = res["f64"]
+    assert np.max(np.abs(v32 - v64)) <= 1e-4
+    assert np.max(np.abs(xs32 - xs64)) <= 1e-4
+    assert np.all(np.abs(xl32 - xl64) <= 1e-4 * xl64)
+
+
+# ---------------------------------------------------------------- full size (BASELINE config 2) ---
+def test_config2_full_size_subset_bitexact_and_properties():
+    """n=10k, m=42k, B=1024 f32 for 12 steps: replicas {0, 517, 1023} bit-exact vs the oracle's f32
+    restatement; every replica: v in [-1,1], xs in [eps, 1-eps], xl in [1, 1e4 m], finite."""
+    c = wl.CONFIGS["config2"]
+    var, neg = wl.random_ksat(c["n"], c["m"], 3, c["seed"])
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
+    o = Oracle(cp, v_, n_, c["n"], "f32")
+    B, K = 1024, 12
+    with Solver(f, B, "f32") as s:
+        s.init_state(42)
+        r = s.simulate(dt=0.01, max_steps=K, stop=ODESAT_STOP_NONE)
+        assert r["steps_run"] == K and np.all(r["steps_done"] == K)
+        pick = [0, 517, 1023]
+        states = {b: s.get_state(b, 1) for b in pick}
+        v, xs, xl = s.get_state()
+    assert np.isfinite(v).all() and np.isfinite(xs).all() and np.isfinite(xl).all()
+    assert v.min() >= -1 and v.max() <= 1
+    eps = np.float32(0.001)
+    assert xs.min() >= eps and xs.max() <= np.float32(1) - eps
+    assert xl.min() >= 1 and xl.max() <= np.float32(1e4) * np.float32(c["m"])
+    for b in pick:
+        ov = init_voltages(42, b, 1, c["n"])[0].astype(np.float32)
+        oxs = o.init_short_term_memory()
+        oxl = np.ones(c["m"], np.float32)
+        o.simulate(ov, oxs, oxl, dt=np.float32(0.01), steps=K, zeta=np.float32(0.001))
+        gv, gxs, gxl = states[b]
+        assert same(gv[0], ov) and same(gxs[0], oxs) and same(gxl[0], oxl)
