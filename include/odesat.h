@@ -156,6 +156,12 @@ int64_t odesat_clause_kernel_bytes(const odesat_solver *s);
 /* Tuning: replicas per chunk (0 = automatic) -- the batch is stepped chunk by chunk so the
  * contribution buffer of one chunk stays resident in the Infinity Cache. */
 int odesat_set_chunk_replicas(odesat_solver *s, int64_t replicas);
+/* Schedule of odesat_simulate over chunks (results are identical; STOP_ANY is always step-major):
+ * AUTO = chunk-major when the batch spans several chunks. */
+#define ODESAT_SCHED_AUTO 0
+#define ODESAT_SCHED_STEP_MAJOR 1  /* every step: all chunks, then the next step */
+#define ODESAT_SCHED_CHUNK_MAJOR 2 /* every chunk: all steps, then the next chunk */
+int odesat_set_schedule(odesat_solver *s, int schedule);
 
 #ifdef __cplusplus
 }

@@ -410,13 +410,13 @@ struct StatusArgs {
     int64_t *sat_step;
     int64_t *steps_done;
     int32_t *stop;
-    int32_t B, step, stop_mode, adaptive;
+    int32_t r0, r1, step, stop_mode, adaptive;
     double tol;
 };
 
 template <typename T> __global__ void k_status(StatusArgs s) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= s.B) return;
+    const int r = s.r0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= s.r1) return;
     if (*s.stop < s.step) return;  // this step did not run
     auto *err = (typename Bits<T>::U *)s.err;
     T *dtr = (T *)s.dtr;
@@ -507,6 +507,7 @@ struct odesat_solver {
     int W = 64, G = 1;
     int chunk_groups = 1;
     int uniform_k = 0;  // every clause has this many literals (0 = mixed widths)
+    int schedule = ODESAT_SCHED_AUTO;
     bool force_generic = false;
     size_t tsize = 4;
     hipStream_t stream = nullptr;
@@ -663,15 +664,15 @@ int launch_kernel(odesat_solver *s, KArgs<T> a, bool clause) {
 
 // One RHS(+update) of `mode` for every chunk: k_clause then k_variable per chunk.
 template <typename T, int W, int MODE>
-int step_chunks(odesat_solver *s, int step, T dt, T zeta) {
+int step_chunks(odesat_solver *s, int step, T dt, T zeta, int gA, int gB) {
     KArgs<T> a = make_args<T>(s);
     a.step = step;
     a.dt = dt;
     a.zeta = zeta;
     int rc;
-    for (int g0 = 0; g0 < s->G; g0 += s->chunk_groups) {
+    for (int g0 = gA; g0 < gB; g0 += s->chunk_groups) {
         a.g0 = g0;
-        a.ng = std::min(s->chunk_groups, s->G - g0);
+        a.ng = std::min(s->chunk_groups, gB - g0);
         if ((rc = launch_kernel<T, W, MODE>(s, a, true))) return rc;
         if ((rc = launch_kernel<T, W, MODE>(s, a, false))) return rc;
     }
@@ -679,7 +680,7 @@ int step_chunks(odesat_solver *s, int step, T dt, T zeta) {
 }
 
 template <typename T>
-int launch_status(odesat_solver *s, int step, int stop_mode, bool adaptive, double tol) {
+int launch_status(odesat_solver *s, int step, int stop_mode, bool adaptive, double tol, int64_t r0, int64_t r1) {
     StatusArgs sa{};
     sa.act = s->act;
     sa.unsat = s->unsat;
@@ -688,7 +689,10 @@ int launch_status(odesat_solver *s, int step, int stop_mode, bool adaptive, doub
     sa.sat_step = s->sat_step;
     sa.steps_done = s->steps_done;
     sa.stop = s->stop;
-    sa.B = (int32_t)s->B;
+    r1 = std::min<int64_t>(r1, s->B);
+    if (r1 <= r0) return ODESAT_OK;
+    sa.r0 = (int32_t)r0;
+    sa.r1 = (int32_t)r1;
     sa.step = step;
     sa.stop_mode = stop_mode;
     sa.adaptive = adaptive ? 1 : 0;
@@ -700,7 +704,7 @@ int launch_status(odesat_solver *s, int step, int stop_mode, bool adaptive, doub
         HIP_TRY(hipEventRecord(e0, s->stream));
     }
     const int threads = 256;
-    const int blocks = (int)((s->B + threads - 1) / threads);
+    const int blocks = (int)((r1 - r0 + threads - 1) / threads);
     hipLaunchKernelGGL((k_status<T>), dim3(blocks), dim3(threads), 0, s->stream, sa);
     HIP_TRY(hipGetLastError());
     if (s->profile) {
@@ -711,42 +715,49 @@ int launch_status(odesat_solver *s, int step, int stop_mode, bool adaptive, doub
 }
 
 // One full euler step (fixed or adaptive) for every replica, enqueued on the stream.
+// One full euler step (fixed or adaptive) for the replica groups [gA, gB), enqueued on the stream.
 template <typename T, int W>
-int enqueue_step(odesat_solver *s, int step, bool adaptive, T dt, T zeta, double tol, int stop_mode) {
+int enqueue_step(odesat_solver *s, int step, bool adaptive, T dt, T zeta, double tol, int stop_mode, int gA,
+                 int gB) {
     int rc;
     if (!adaptive) {
-        if ((rc = step_chunks<T, W, M_FIXED>(s, step, dt, zeta))) return rc;
+        if ((rc = step_chunks<T, W, M_FIXED>(s, step, dt, zeta, gA, gB))) return rc;
     } else {
-        if ((rc = step_chunks<T, W, M_ADA>(s, step, dt, zeta))) return rc;
-        if ((rc = step_chunks<T, W, M_ADB>(s, step, dt, zeta))) return rc;
+        // all chunks' first half before any second half would need one contribution buffer per chunk;
+        // the half steps of one chunk run back to back instead
+        for (int g0 = gA; g0 < gB; g0 += s->chunk_groups) {
+            const int g1 = std::min(gB, g0 + s->chunk_groups);
+            if ((rc = step_chunks<T, W, M_ADA>(s, step, dt, zeta, g0, g1))) return rc;
+            if ((rc = step_chunks<T, W, M_ADB>(s, step, dt, zeta, g0, g1))) return rc;
+        }
     }
-    return launch_status<T>(s, step, stop_mode, adaptive, tol);
+    return launch_status<T>(s, step, stop_mode, adaptive, tol, (int64_t)gA * s->W, (int64_t)gB * s->W);
 }
 
 template <typename T>
 int dispatch_step(odesat_solver *s, int step, bool adaptive, double dt, double zeta, double tol,
-                  int stop_mode) {
+                  int stop_mode, int gA, int gB) {
     switch (s->W) {
-        case 1: return enqueue_step<T, 1>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode);
-        case 2: return enqueue_step<T, 2>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode);
-        case 4: return enqueue_step<T, 4>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode);
-        case 8: return enqueue_step<T, 8>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode);
-        case 16: return enqueue_step<T, 16>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode);
-        case 32: return enqueue_step<T, 32>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode);
-        default: return enqueue_step<T, 64>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode);
+        case 1: return enqueue_step<T, 1>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
+        case 2: return enqueue_step<T, 2>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
+        case 4: return enqueue_step<T, 4>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
+        case 8: return enqueue_step<T, 8>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
+        case 16: return enqueue_step<T, 16>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
+        case 32: return enqueue_step<T, 32>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
+        default: return enqueue_step<T, 64>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
     }
 }
 
 template <typename T>
 int dispatch_deriv(odesat_solver *s, double zeta) {
     switch (s->W) {
-        case 1: return step_chunks<T, 1, M_DERIV>(s, 0, (T)0, (T)zeta);
-        case 2: return step_chunks<T, 2, M_DERIV>(s, 0, (T)0, (T)zeta);
-        case 4: return step_chunks<T, 4, M_DERIV>(s, 0, (T)0, (T)zeta);
-        case 8: return step_chunks<T, 8, M_DERIV>(s, 0, (T)0, (T)zeta);
-        case 16: return step_chunks<T, 16, M_DERIV>(s, 0, (T)0, (T)zeta);
-        case 32: return step_chunks<T, 32, M_DERIV>(s, 0, (T)0, (T)zeta);
-        default: return step_chunks<T, 64, M_DERIV>(s, 0, (T)0, (T)zeta);
+        case 1: return step_chunks<T, 1, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
+        case 2: return step_chunks<T, 2, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
+        case 4: return step_chunks<T, 4, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
+        case 8: return step_chunks<T, 8, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
+        case 16: return step_chunks<T, 16, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
+        case 32: return step_chunks<T, 32, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
+        default: return step_chunks<T, 64, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
     }
 }
 
@@ -1033,6 +1044,14 @@ extern "C" int odesat_set_chunk_replicas(odesat_solver *s, int64_t replicas) {
     return ODESAT_OK;
 }
 
+extern "C" int odesat_set_schedule(odesat_solver *s, int schedule) {
+    int rc;
+    if ((rc = check_solver(s))) return rc;
+    if (schedule < ODESAT_SCHED_AUTO || schedule > ODESAT_SCHED_CHUNK_MAJOR) return fail(ODESAT_EINVAL, "bad schedule");
+    s->schedule = schedule;
+    return ODESAT_OK;
+}
+
 extern "C" int odesat_set_state(odesat_solver *s, int64_t r0, int64_t count, const double *v, const double *xs,
                                 const double *xl) {
     int rc;
@@ -1135,8 +1154,8 @@ static int single_step(odesat_solver *s, bool adaptive, double tol, double dt, d
     HIP_TRY(hipMemcpy(sat_save.data(), s->sat_step, s->Bp * 8, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(done_save.data(), s->steps_done, s->Bp * 8, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(s->sat_step, minus.data(), s->Bp * 8, hipMemcpyHostToDevice));
-    rc = s->dtype == ODESAT_F64 ? dispatch_step<double>(s, 0, adaptive, dt, zeta, tol, ODESAT_STOP_NONE)
-                                : dispatch_step<float>(s, 0, adaptive, dt, zeta, tol, ODESAT_STOP_NONE);
+    rc = s->dtype == ODESAT_F64 ? dispatch_step<double>(s, 0, adaptive, dt, zeta, tol, ODESAT_STOP_NONE, 0, s->G)
+                                : dispatch_step<float>(s, 0, adaptive, dt, zeta, tol, ODESAT_STOP_NONE, 0, s->G);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
     std::vector<int64_t> sat(s->Bp);
@@ -1208,28 +1227,43 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
         (void)hipHostFree(h_stop);
         return fail(ODESAT_ENOMEM, "hipHostMalloc failed");
     }
-    int64_t t = 0;
+    // Schedule: replicas are independent, so with STOP_EACH / STOP_NONE the batch may be stepped
+    // chunk by chunk (all steps of one chunk, then the next): one chunk's state + contribution buffer
+    // stays resident in the Infinity Cache across steps.  STOP_ANY needs lock-step (step-major).
+    const bool chunk_major = p->stop != ODESAT_STOP_ANY &&
+                             (s->schedule == ODESAT_SCHED_CHUNK_MAJOR ||
+                              (s->schedule == ODESAT_SCHED_AUTO && s->G > s->chunk_groups));
+    const int span = chunk_major ? s->chunk_groups : s->G;
+    int64_t t_run = 0;
     rc = ODESAT_OK;
-    for (; t < p->max_steps; ++t) {
-        rc = s->dtype == ODESAT_F64 ? dispatch_step<double>(s, (int)t, adaptive, p->dt, zeta, tol, p->stop)
-                                    : dispatch_step<float>(s, (int)t, adaptive, p->dt, zeta, tol, p->stop);
-        if (rc) break;
-        if (p->stop != ODESAT_STOP_NONE && (t + 1) % poll == 0 && t + 1 < p->max_steps) {
-            // poll the stop condition (results are exact regardless: later launches are no-ops)
-            if (hipMemcpyAsync(h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
-                hipMemcpyAsync(h_act, s->act, s->Bp, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
-                hipStreamSynchronize(s->stream) != hipSuccess) {
-                rc = fail(ODESAT_EDEVICE, "poll failed");
-                break;
-            }
-            if (p->stop == ODESAT_STOP_ANY && *h_stop != INT_MAX) { ++t; break; }
-            if (p->stop == ODESAT_STOP_EACH) {
-                bool any = false;
-                for (int64_t r = 0; r < s->B && !any; ++r) any = h_act[r] != 0;
-                if (!any) { ++t; break; }
+    for (int gA = 0; gA < s->G && rc == ODESAT_OK; gA += span) {
+        const int gB = std::min(s->G, gA + span);
+        const int64_t r0 = (int64_t)gA * s->W, r1 = std::min<int64_t>((int64_t)gB * s->W, s->B);
+        int64_t t = 0;
+        for (; t < p->max_steps; ++t) {
+            rc = s->dtype == ODESAT_F64
+                     ? dispatch_step<double>(s, (int)t, adaptive, p->dt, zeta, tol, p->stop, gA, gB)
+                     : dispatch_step<float>(s, (int)t, adaptive, p->dt, zeta, tol, p->stop, gA, gB);
+            if (rc) break;
+            if (p->stop != ODESAT_STOP_NONE && (t + 1) % poll == 0 && t + 1 < p->max_steps) {
+                // poll the stop condition (results are exact regardless: later launches are no-ops)
+                if (hipMemcpyAsync(h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
+                    hipMemcpyAsync(h_act + r0, s->act + r0, r1 - r0, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
+                    hipStreamSynchronize(s->stream) != hipSuccess) {
+                    rc = fail(ODESAT_EDEVICE, "poll failed");
+                    break;
+                }
+                if (p->stop == ODESAT_STOP_ANY && *h_stop != INT_MAX) { ++t; break; }
+                if (p->stop == ODESAT_STOP_EACH) {
+                    bool any = false;
+                    for (int64_t r = r0; r < r1 && !any; ++r) any = h_act[r] != 0;
+                    if (!any) { ++t; break; }
+                }
             }
         }
+        t_run = std::max(t_run, t);
     }
+    const int64_t t = t_run;
     (void)hipHostFree(h_stop);
     (void)hipHostFree(h_act);
     if (rc) return rc;

@@ -146,6 +146,10 @@ class Solver:
     def set_chunk_replicas(self, replicas: int):
         check(lib().odesat_set_chunk_replicas(self._h, int(replicas)))
 
+    def set_schedule(self, schedule: int):
+        """_lib.ODESAT_SCHED_AUTO / _STEP_MAJOR / _CHUNK_MAJOR (results are identical)."""
+        check(lib().odesat_set_schedule(self._h, int(schedule)))
+
     def profile(self, enable: bool):
         check(lib().odesat_profile_enable(self._h, 1 if enable else 0))
 

@@ -336,3 +336,25 @@ def test_config2_full_size_subset_bitexact_and_properties():
         o.simulate(ov, oxs, oxl, dt=np.float32(0.01), steps=K, zeta=np.float32(0.001))
         gv, gxs, gxl = states[b]
         assert same(gv[0], ov) and same(gxs[0], oxs) and same(gxl[0], oxl)
+
+
+def test_schedules_identical():
+    """Step-major and chunk-major schedules give bit-identical states (replicas are independent)."""
+    from odesat_amd import _lib
+    f = product_formula("rand200")
+    out = []
+    for sched, chunk in ((_lib.ODESAT_SCHED_STEP_MAJOR, 64), (_lib.ODESAT_SCHED_CHUNK_MAJOR, 64),
+                         (_lib.ODESAT_SCHED_CHUNK_MAJOR, 128), (_lib.ODESAT_SCHED_AUTO, 0)):
+        for adaptive in (False, True):
+            with Solver(f, 200, "f32") as s:
+                s.set_chunk_replicas(chunk)
+                s.set_schedule(sched)
+                s.init_state(13)
+                r = s.simulate(adaptive=adaptive, dt=0.05, max_steps=60, stop=ODESAT_STOP_EACH, poll_interval=5)
+                out.append((adaptive, r["first_sat_step"], r["steps_done"], s.get_state()))
+    base = {False: out[0], True: out[1]}
+    for adaptive, sat, done, st in out:
+        b = base[adaptive]
+        assert np.array_equal(sat, b[1]) and np.array_equal(done, b[2])
+        for x, y in zip(st, b[3]):
+            assert same(x, y)
