@@ -1,11 +1,15 @@
 // odesat_hip.hip -- MI355X (gfx950) integrator for the Bearden-Pei-Di Ventra memcomputing ODE:
 // the replacement of /root/reference/src/system.rs:25-359 behind the C ABI of include/odesat.h.
 //
-// Device layout: every per-item array is replica-innermost in groups of W replicas,
-//   X[g][item][W], replica r = g*W + lane, W = 64 for batches >= 64 (one wave = the 64 replicas of
-//   one clause / variable: literal indices are wave-uniform scalar loads and every state access is
-//   one coalesced 256-B row), W = next pow2 >= B for small batches (a wave spans 64/W items).
-// One Euler step = two HBM-streaming kernels per replica chunk + one status kernel:
+// Device layout.  Every per-item array (item = variable or clause) is
+// replica-innermost in groups of W replicas:  X[g][item][W],  replica r = g*W + j.
+// A wave covers one "row": LW lanes per item, VEC contiguous replicas per lane, W = LW*VEC.
+//   * batches >= 256 (f32) / >= 128 (f64):  LW = 64, VEC = 16 B / sizeof(T): one wave = the
+//     W replicas of ONE clause / variable, every state access is a 1 KiB dwordx4 wave-load, literal
+//     indices are wave-uniform scalar loads;
+//   * 128 <= B < 256 (f32): LW = 64, VEC = 2; 64 <= B < 128: LW = 64, VEC = 1;
+//   * B < 64: LW = next pow2 >= B, VEC = 1: a wave spans 64/LW items.
+// One Euler step = two kernels per replica chunk + one status kernel:
 //   k_clause   (system.rs:35-90)   per clause: gather the literal voltages, strict-< min/second-min,
 //              C, G, R, the per-literal dv contribution, dxs/dxl, the fused update_state of xs/xl
 //              (system.rs:94-95) and the per-replica "some clause unsat" flag.  The contribution of
@@ -16,8 +20,7 @@
 //              bit-identical to the CPU oracle -- then the clamped v update.  No atomics.
 //   k_status   (system.rs:149-153, 122-136, 190-235, 291) per replica: sat bookkeeping, stop
 //              policy, adaptive dt.
-// Kernels are compiled with FP contraction OFF: every + and * rounds exactly as written in
-// system.rs, in the solver's dtype.
+// FP contraction is OFF: every + and * rounds exactly as written in system.rs, in the solver dtype.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -29,6 +32,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/odesat.h"
@@ -70,6 +74,28 @@ __device__ __forceinline__ double frombits(unsigned long long x) {
 }
 template <typename T> __device__ __forceinline__ T inf_v() { return (T)__builtin_huge_val(); }
 
+// VEC contiguous elements, loaded / stored as one 4-, 8- or 16-byte access per lane
+template <typename T, int N> struct alignas(sizeof(T) * N) Vec {
+    T e[N];
+};
+template <typename T, int N> __device__ __forceinline__ Vec<T, N> ldv(const T *p) {
+    return *reinterpret_cast<const Vec<T, N> *>(p);
+}
+template <typename T, int N> __device__ __forceinline__ void stv(T *p, const Vec<T, N> &x) {
+    *reinterpret_cast<Vec<T, N> *>(p) = x;
+}
+// store only the active elements (a partially frozen lane must not overwrite frozen replicas)
+template <typename T, int N>
+__device__ __forceinline__ void stv_masked(T *p, const Vec<T, N> &x, const bool (&on)[N], bool all_on) {
+    if (all_on) {
+        stv<T, N>(p, x);
+    } else {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (on[k]) p[k] = x.e[k];
+    }
+}
+
 // splitmix64 counter RNG -- same function as oracle/odesat_oracle.c (oc_hash3).
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -86,6 +112,11 @@ __host__ __device__ __forceinline__ double init_voltage(uint64_t seed, uint64_t 
 
 enum Mode : int { M_DERIV = 0, M_FIXED = 1, M_ADA = 2, M_ADB = 3 };
 
+// The topology arrays are never written by a kernel: reading them through the constant address
+// space lets wave-uniform indices become scalar (s_load) loads on the scalar cache.
+typedef const __attribute__((address_space(4))) int32_t cint32;
+__device__ __forceinline__ int32_t ldc(const int32_t *p, size_t i) { return ((cint32 *)p)[i]; }
+
 template <typename T> struct KArgs {
     const int32_t *__restrict__ cptr;  // [m+1]
     const int32_t *__restrict__ lits;  // [L] var<<1 | neg, file order
@@ -101,306 +132,390 @@ template <typename T> struct KArgs {
     const int32_t *stop;               // first stop step (INT_MAX = none)
     int32_t n, m, L;
     int32_t g0, ng;                    // group range of this chunk
-    int32_t rows;                      // rows (of 64/W items) per wave
+    int32_t rows;                      // rows (of 64/LW items) per wave
     int32_t tiles;                     // waves per group
     int32_t step;
     T dt, zeta, xl_max;
 };
 
 constexpr int WAVES_PER_BLOCK = 4;
-constexpr int KREG = 4;  // literal values kept in registers (3-SAT + the 4-literal fixture clause)
+
+// Per-wave geometry shared by the kernels.
+template <int LW, int VEC> struct Geo {
+    static constexpr int W = LW * VEC;  // replicas per group
+    static constexpr int IPR = 64 / LW; // items per wave row
+    int gl, g, tile, isub, lin;
+    size_t off;  // element offset of this lane's first replica inside an item row
+    int r0;      // this lane's first replica
+    __device__ __forceinline__ bool init(int tiles, int g0, int ng) {
+        const int lane = threadIdx.x & 63;
+        const int wave = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+        gl = wave / tiles;
+        tile = wave - gl * tiles;
+        if (gl >= ng) return false;
+        g = g0 + gl;
+        lin = lane % LW;
+        isub = lane / LW;
+        off = (size_t)lin * VEC;
+        r0 = g * W + lin * VEC;
+        return true;
+    }
+};
 
 // :84-85 memory derivatives, then (by mode) the fused update_state of xs / xl (:94-95), the
-// adaptive half / full candidates (:124-130) or the second half step and its max_error (:132).
-template <typename T, int MODE>
-__device__ __forceinline__ void clause_update(const KArgs<T> &a, size_t ci, T C, T xs_m, T xl_m, T h,
-                                              T half, T &e) {
+// adaptive half / full candidates (:124-130) or the second half step and its max_error (:132),
+// for the VEC replicas of one lane.
+template <typename T, int VEC, int MODE>
+__device__ __forceinline__ void clause_update(const KArgs<T> &a, size_t ci, const T (&C)[VEC],
+                                              const Vec<T, VEC> &xs_m, const Vec<T, VEC> &xl_m,
+                                              const T (&h)[VEC], const bool (&on)[VEC], bool all_on,
+                                              T (&e)[VEC]) {
     const T one = (T)1.0, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
-    const T dxs = (T)20.0 * (xs_m + eps) * (C - (T)0.25);  // :84
-    const T dxl = (T)5.0 * (C - (T)0.05);                  // :85
+    Vec<T, VEC> o1, o2, o3, o4;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        const T dxs = (T)20.0 * (xs_m.e[k] + eps) * (C[k] - (T)0.25);  // :84
+        const T dxl = (T)5.0 * (C[k] - (T)0.05);                       // :85
+        const T half = (T)0.5 * h[k];
+        if (MODE == M_DERIV) {
+            o1.e[k] = dxs;
+            o2.e[k] = dxl;
+        } else if (MODE == M_FIXED) {
+            o1.e[k] = dmin(dmax(xs_m.e[k] + h[k] * dxs, eps), xs_hi);
+            o2.e[k] = dmin(dmax(xl_m.e[k] + h[k] * dxl, one), a.xl_max);
+        } else if (MODE == M_ADA) {
+            o1.e[k] = dmin(dmax(xs_m.e[k] + h[k] * dxs, eps), xs_hi);     // full-step clone
+            o2.e[k] = dmin(dmax(xl_m.e[k] + h[k] * dxl, one), a.xl_max);
+            o3.e[k] = dmin(dmax(xs_m.e[k] + half * dxs, eps), xs_hi);     // first half step
+            o4.e[k] = dmin(dmax(xl_m.e[k] + half * dxl, one), a.xl_max);
+        } else {
+            o1.e[k] = dmin(dmax(xs_m.e[k] + half * dxs, eps), xs_hi);     // second half step
+            o2.e[k] = dmin(dmax(xl_m.e[k] + half * dxl, one), a.xl_max);
+        }
+    }
     if (MODE == M_DERIV) {
-        a.xsh[ci] = dxs;
-        a.xlh[ci] = dxl;
+        stv<T, VEC>(a.xsh + ci, o1);
+        stv<T, VEC>(a.xlh + ci, o2);
     } else if (MODE == M_FIXED) {
-        a.xs[ci] = dmin(dmax(xs_m + h * dxs, eps), xs_hi);
-        a.xl[ci] = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
+        stv_masked<T, VEC>(a.xs + ci, o1, on, all_on);
+        stv_masked<T, VEC>(a.xl + ci, o2, on, all_on);
     } else if (MODE == M_ADA) {
-        a.xsf[ci] = dmin(dmax(xs_m + h * dxs, eps), xs_hi);
-        a.xlf[ci] = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
-        a.xsh[ci] = dmin(dmax(xs_m + half * dxs, eps), xs_hi);
-        a.xlh[ci] = dmin(dmax(xl_m + half * dxl, one), a.xl_max);
+        stv<T, VEC>(a.xsf + ci, o1);
+        stv<T, VEC>(a.xlf + ci, o2);
+        stv<T, VEC>(a.xsh + ci, o3);
+        stv<T, VEC>(a.xlh + ci, o4);
     } else {
-        const T xsn = dmin(dmax(xs_m + half * dxs, eps), xs_hi);
-        const T xln = dmin(dmax(xl_m + half * dxl, one), a.xl_max);
-        a.xs[ci] = xsn;
-        a.xl[ci] = xln;
-        e = dmax(e, dmax(dabs(a.xsf[ci] - xsn), dabs(a.xlf[ci] - xln)));
+        const Vec<T, VEC> fs = ldv<T, VEC>(a.xsf + ci), fl = ldv<T, VEC>(a.xlf + ci);
+        stv_masked<T, VEC>(a.xs + ci, o1, on, all_on);
+        stv_masked<T, VEC>(a.xl + ci, o2, on, all_on);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k)  // :101-108 max_error terms
+            e[k] = dmax(e[k], dmax(dabs(fs.e[k] - o1.e[k]), dabs(fl.e[k] - o2.e[k])));
     }
 }
 
-// ------------------------------------------------------------------------------------------------
-// k_clause: system.rs:35-90 (+ :94-95 for the fixed step)
-// ------------------------------------------------------------------------------------------------
-template <typename T, int W, int MODE>
-__global__ __launch_bounds__(256) void k_clause(KArgs<T> a) {
-    constexpr int IPR = 64 / W;  // items per wave row
-    const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
-    const int gl = wave / a.tiles;
-    const int tile = wave - gl * a.tiles;
-    if (gl >= a.ng) return;
-    if (*a.stop < a.step) return;  // ODESAT_STOP_ANY already triggered
-    const int g = a.g0 + gl;
-    const int rin = lane % W;
-    const int isub = lane / W;
-    const int r = g * W + rin;
-    bool on = a.act[r] != 0;
-    if (MODE == M_ADB) on = on && a.unsat[r] != 0;  // allsat at the first RHS: no update (:122)
-    if (!__any(on)) return;
-
-    const T *__restrict__ V = (MODE == M_ADB) ? a.vh : a.v;
-    const T *XS = (MODE == M_ADB) ? a.xsh : a.xs;
-    const T *XL = (MODE == M_ADB) ? a.xlh : a.xl;
-    const T h = (MODE == M_ADA || MODE == M_ADB) ? a.dtr[r] : a.dt;
-    const T half = (T)0.5 * h;
-    const T one = (T)1.0, halfc = (T)0.5;
-    const size_t vbase = (size_t)g * a.n * W + rin;
-    const size_t cbase = (size_t)g * a.m * W + rin;
-    const size_t wbase = (size_t)gl * a.L * W + rin;
-    bool uns = false;
-    T e = (T)0.0;
-
-    for (int row = 0; row < a.rows; ++row) {
-        int c = (tile * a.rows + row) * IPR + isub;
-        if (W == 64) c = __builtin_amdgcn_readfirstlane(c);
-        if (c >= a.m) break;
-        const int s0 = a.cptr[c], s1 = a.cptr[c + 1];
-        // :43-57 strict-< min / second-min in literal (file) order
-        T mn = inf_v<T>(), sec = inf_v<T>();
-        T val[KREG], vv[KREG];
+// The per-replica prologue shared by both clause kernels and the variable kernel.
+template <typename T, int VEC, int MODE, bool CLAUSE>
+__device__ __forceinline__ bool lane_state(const KArgs<T> &a, int r0, bool (&on)[VEC], bool &all_on,
+                                           T (&h)[VEC]) {
+    bool any = false;
+    all_on = true;
 #pragma unroll
-        for (int j = 0; j < KREG; ++j) {
-            val[j] = (T)0.0;
-            vv[j] = (T)0.0;
-            if (s0 + j < s1) {
-                const int lit = a.lits[s0 + j];
-                const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
-                vv[j] = V[vbase + (size_t)(lit >> 1) * W];
-                val[j] = one - q * vv[j];
-                if (val[j] < mn) {
-                    sec = mn;
-                    mn = val[j];
-                } else if (val[j] < sec) {
-                    sec = val[j];
-                }
-            }
-        }
-        for (int s = s0 + KREG; s < s1; ++s) {  // wide clauses: values re-gathered below
-            const int lit = a.lits[s];
-            const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
-            const T value = one - q * V[vbase + (size_t)(lit >> 1) * W];
-            if (value < mn) {
-                sec = mn;
-                mn = value;
-            } else if (value < sec) {
-                sec = value;
-            }
-        }
-        const T C = halfc * mn;                       // :60
-        const size_t ci = cbase + (size_t)c * W;
-        const T xs_m = XS[ci], xl_m = XL[ci];
-        const T t = xl_m * xs_m;                      // :80 first product
-        const T tr = (one + a.zeta * xl_m) * (one - xs_m);
-        if (on) {
-#pragma unroll
-            for (int j = 0; j < KREG; ++j) {
-                if (s0 + j < s1) {
-                    const int lit = a.lits[s0 + j];
-                    const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
-                    const T g_ = halfc * q * (val[j] != mn ? mn : sec);                  // :64-70
-                    const T r_ = (C == one - q * vv[j]) ? halfc * (q - vv[j]) : (T)0.0;  // :73-77
-                    a.w[wbase + (size_t)a.wpos[s0 + j] * W] = t * g_ + tr * r_;          // :80
-                }
-            }
-            for (int s = s0 + KREG; s < s1; ++s) {
-                const int lit = a.lits[s];
-                const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
-                const T vi = V[vbase + (size_t)(lit >> 1) * W];
-                const T value = one - q * vi;
-                const T g_ = halfc * q * (value != mn ? mn : sec);
-                const T r_ = (C == one - q * vi) ? halfc * (q - vi) : (T)0.0;
-                a.w[wbase + (size_t)a.wpos[s] * W] = t * g_ + tr * r_;
-            }
-            clause_update<T, MODE>(a, ci, C, xs_m, xl_m, h, half, e);
-            if (MODE != M_ADB) uns = uns || !(C < (T)0.25);  // :88
-        }
+    for (int k = 0; k < VEC; ++k) {
+        bool o = a.act[r0 + k] != 0;
+        // adaptive: a replica allsat at the first RHS takes no step (system.rs:122)
+        if (MODE == M_ADB || (!CLAUSE && MODE == M_ADA)) o = o && a.unsat[r0 + k] != 0;
+        on[k] = o;
+        any = any || o;
+        all_on = all_on && o;
+        h[k] = (MODE == M_ADA || MODE == M_ADB) ? a.dtr[r0 + k] : a.dt;
     }
-    if (MODE != M_ADB) {
-        if (on && uns) a.unsat[r] = 1u;
-    } else {
-        if (on) atomicMax(&a.err[r], tobits(e));
-    }
+    return __any(any);
 }
 
-// k_clause_u: the same computation for formulas whose clauses all have K literals (random k-SAT).
-// RB clauses per batch: their K*RB literal indices (scalar loads for W = 64), K*RB voltage rows and
-// 2*RB memory rows are all issued before the first use, so a wave keeps ~3 KiB of loads in flight
-// instead of one dependent 256-B gather at a time.  Out-of-range clauses of the last batch load
-// clause m-1 and store nothing.
-template <typename T, int W, int MODE, int K>
+// ------------------------------------------------------------------------------------------------
+// k_clause_u: system.rs:35-90 (+ :94-95) for formulas whose clauses all have K literals (random
+// k-SAT).  RB clauses per batch: their K*RB literal indices (scalar loads for LW = 64), K*RB voltage
+// rows and 2*RB memory rows are all issued before the first use.  Out-of-range clauses of the last
+// batch load clause m-1 and store nothing.
+// ------------------------------------------------------------------------------------------------
+template <typename T, int LW, int VEC, int MODE, int K>
 __global__ __launch_bounds__(256) void k_clause_u(KArgs<T> a) {
-    constexpr int IPR = 64 / W;
-    constexpr int RB = 4;
-    const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
-    const int gl = wave / a.tiles;
-    const int tile = wave - gl * a.tiles;
-    if (gl >= a.ng) return;
-    if (*a.stop < a.step) return;
-    const int g = a.g0 + gl;
-    const int rin = lane % W;
-    const int isub = lane / W;
-    const int r = g * W + rin;
-    bool on = a.act[r] != 0;
-    if (MODE == M_ADB) on = on && a.unsat[r] != 0;
-    if (!__any(on)) return;
+    using G_ = Geo<LW, VEC>;
+    constexpr int W = G_::W, IPR = G_::IPR;
+    constexpr int RB = VEC >= 4 ? 2 : 4;
+    G_ geo;
+    if (!geo.init(a.tiles, a.g0, a.ng)) return;
+    if (*a.stop < a.step) return;  // ODESAT_STOP_ANY already triggered
+    bool on[VEC], all_on;
+    T h[VEC];
+    if (!lane_state<T, VEC, MODE, true>(a, geo.r0, on, all_on, h)) return;
 
     const T *__restrict__ V = (MODE == M_ADB) ? a.vh : a.v;
     const T *XS = (MODE == M_ADB) ? a.xsh : a.xs;
     const T *XL = (MODE == M_ADB) ? a.xlh : a.xl;
-    const T h = (MODE == M_ADA || MODE == M_ADB) ? a.dtr[r] : a.dt;
-    const T half = (T)0.5 * h;
     const T one = (T)1.0, halfc = (T)0.5;
-    const size_t vbase = (size_t)g * a.n * W + rin;
-    const size_t cbase = (size_t)g * a.m * W + rin;
-    const size_t wbase = (size_t)gl * a.L * W + rin;
-    bool uns = false;
-    T e = (T)0.0;
+    const size_t vbase = (size_t)geo.g * a.n * W + geo.off;
+    const size_t cbase = (size_t)geo.g * a.m * W + geo.off;
+    const size_t wbase = (size_t)geo.gl * a.L * W + geo.off;
+    bool uns[VEC];
+    T e[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        uns[k] = false;
+        e[k] = (T)0.0;
+    }
 
     for (int row0 = 0; row0 < a.rows; row0 += RB) {
         int cc[RB];
         bool ok[RB];
 #pragma unroll
         for (int b = 0; b < RB; ++b) {
-            int c = (tile * a.rows + row0 + b) * IPR + isub;
+            int c = (geo.tile * a.rows + row0 + b) * IPR + geo.isub;
             ok[b] = (row0 + b < a.rows) && (c < a.m);
             c = ok[b] ? c : a.m - 1;
-            if (W == 64) c = __builtin_amdgcn_readfirstlane(c);
+            if (LW == 64) c = __builtin_amdgcn_readfirstlane(c);
             cc[b] = c;
         }
-        int lit[RB][K];
+        int lit[RB][K], pos[RB][K];
 #pragma unroll
         for (int b = 0; b < RB; ++b)
 #pragma unroll
-            for (int j = 0; j < K; ++j) lit[b][j] = a.lits[cc[b] * K + j];
-        T vv[RB][K];
+            for (int j = 0; j < K; ++j) {
+                lit[b][j] = ldc(a.lits, (size_t)cc[b] * K + j);
+                pos[b][j] = ldc(a.wpos, (size_t)cc[b] * K + j);
+            }
+        Vec<T, VEC> vv[RB][K], xs_m[RB], xl_m[RB];
 #pragma unroll
         for (int b = 0; b < RB; ++b)
 #pragma unroll
-            for (int j = 0; j < K; ++j) vv[b][j] = V[vbase + (size_t)(lit[b][j] >> 1) * W];
-        T xs_m[RB], xl_m[RB];
+            for (int j = 0; j < K; ++j) vv[b][j] = ldv<T, VEC>(V + vbase + (size_t)(lit[b][j] >> 1) * W);
 #pragma unroll
         for (int b = 0; b < RB; ++b) {
-            xs_m[b] = XS[cbase + (size_t)cc[b] * W];
-            xl_m[b] = XL[cbase + (size_t)cc[b] * W];
+            xs_m[b] = ldv<T, VEC>(XS + cbase + (size_t)cc[b] * W);
+            xl_m[b] = ldv<T, VEC>(XL + cbase + (size_t)cc[b] * W);
         }
 #pragma unroll
         for (int b = 0; b < RB; ++b) {
             if (!ok[b]) continue;
-            T val[K];
-            T mn = inf_v<T>(), sec = inf_v<T>();
+            T C[VEC], mn[VEC], sec[VEC], t[VEC], tr[VEC];
 #pragma unroll
-            for (int j = 0; j < K; ++j) {  // :43-57, branch-free strict-< min / second-min
-                const T q = (lit[b][j] & 1) ? (T)-1.0 : (T)1.0;
-                val[j] = one - q * vv[b][j];
-                const bool lt = val[j] < mn;
-                sec = lt ? mn : (val[j] < sec ? val[j] : sec);
-                mn = lt ? val[j] : mn;
-            }
-            const T C = halfc * mn;  // :60
-            const T t = xl_m[b] * xs_m[b];
-            const T tr = (one + a.zeta * xl_m[b]) * (one - xs_m[b]);
-            if (on) {
+            for (int k = 0; k < VEC; ++k) {
+                mn[k] = inf_v<T>();
+                sec[k] = inf_v<T>();
 #pragma unroll
-                for (int j = 0; j < K; ++j) {
+                for (int j = 0; j < K; ++j) {  // :43-57 strict-< min / second-min, literal order
                     const T q = (lit[b][j] & 1) ? (T)-1.0 : (T)1.0;
-                    const T g_ = halfc * q * (val[j] != mn ? mn : sec);                        // :64-70
-                    const T r_ = (C == one - q * vv[b][j]) ? halfc * (q - vv[b][j]) : (T)0.0;  // :73-77
-                    a.w[wbase + (size_t)a.wpos[cc[b] * K + j] * W] = t * g_ + tr * r_;          // :80
+                    const T val = one - q * vv[b][j].e[k];
+                    const bool lt = val < mn[k];
+                    sec[k] = lt ? mn[k] : (val < sec[k] ? val : sec[k]);
+                    mn[k] = lt ? val : mn[k];
                 }
-                clause_update<T, MODE>(a, cbase + (size_t)cc[b] * W, C, xs_m[b], xl_m[b], h, half, e);
-                if (MODE != M_ADB) uns = uns || !(C < (T)0.25);  // :88
+                C[k] = halfc * mn[k];                                       // :60
+                t[k] = xl_m[b].e[k] * xs_m[b].e[k];                         // :80 xl_m * xs_m
+                tr[k] = (one + a.zeta * xl_m[b].e[k]) * (one - xs_m[b].e[k]);
+                if (MODE != M_ADB) uns[k] = uns[k] || (on[k] && !(C[k] < (T)0.25));  // :88
             }
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const T q = (lit[b][j] & 1) ? (T)-1.0 : (T)1.0;
+                Vec<T, VEC> out;
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const T vi = vv[b][j].e[k];
+                    const T val = one - q * vi;
+                    const T g_ = halfc * q * (val != mn[k] ? mn[k] : sec[k]);        // :64-70
+                    const T r_ = (C[k] == one - q * vi) ? halfc * (q - vi) : (T)0.0;  // :73-77
+                    out.e[k] = t[k] * g_ + tr[k] * r_;                                // :80
+                }
+                stv<T, VEC>(a.w + wbase + (size_t)pos[b][j] * W, out);
+            }
+            clause_update<T, VEC, MODE>(a, cbase + (size_t)cc[b] * W, C, xs_m[b], xl_m[b], h, on, all_on, e);
         }
     }
-    if (MODE != M_ADB) {
-        if (on && uns) a.unsat[r] = 1u;
-    } else {
-        if (on) atomicMax(&a.err[r], tobits(e));
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        if (MODE != M_ADB) {
+            if (uns[k]) a.unsat[geo.r0 + k] = 1u;
+        } else if (on[k]) {
+            atomicMax(&a.err[geo.r0 + k], tobits(e[k]));
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_clause: the same for mixed clause widths (literal values re-gathered for the second pass)
+// ------------------------------------------------------------------------------------------------
+template <typename T, int LW, int VEC, int MODE>
+__global__ __launch_bounds__(256) void k_clause(KArgs<T> a) {
+    using G_ = Geo<LW, VEC>;
+    constexpr int W = G_::W, IPR = G_::IPR;
+    G_ geo;
+    if (!geo.init(a.tiles, a.g0, a.ng)) return;
+    if (*a.stop < a.step) return;
+    bool on[VEC], all_on;
+    T h[VEC];
+    if (!lane_state<T, VEC, MODE, true>(a, geo.r0, on, all_on, h)) return;
+
+    const T *__restrict__ V = (MODE == M_ADB) ? a.vh : a.v;
+    const T *XS = (MODE == M_ADB) ? a.xsh : a.xs;
+    const T *XL = (MODE == M_ADB) ? a.xlh : a.xl;
+    const T one = (T)1.0, halfc = (T)0.5;
+    const size_t vbase = (size_t)geo.g * a.n * W + geo.off;
+    const size_t cbase = (size_t)geo.g * a.m * W + geo.off;
+    const size_t wbase = (size_t)geo.gl * a.L * W + geo.off;
+    bool uns[VEC];
+    T e[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        uns[k] = false;
+        e[k] = (T)0.0;
+    }
+    for (int row = 0; row < a.rows; ++row) {
+        int c = (geo.tile * a.rows + row) * IPR + geo.isub;
+        if (LW == 64) c = __builtin_amdgcn_readfirstlane(c);
+        if (c >= a.m) break;
+        const int s0 = ldc(a.cptr, c), s1 = ldc(a.cptr, c + 1);
+        const size_t ci = cbase + (size_t)c * W;
+        const Vec<T, VEC> xs_m = ldv<T, VEC>(XS + ci), xl_m = ldv<T, VEC>(XL + ci);
+        T mn[VEC], sec[VEC], C[VEC], t[VEC], tr[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            mn[k] = inf_v<T>();
+            sec[k] = inf_v<T>();
+        }
+        for (int s = s0; s < s1; ++s) {  // :43-57
+            const int lit = ldc(a.lits, s);
+            const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
+            const Vec<T, VEC> vv = ldv<T, VEC>(V + vbase + (size_t)(lit >> 1) * W);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const T val = one - q * vv.e[k];
+                const bool lt = val < mn[k];
+                sec[k] = lt ? mn[k] : (val < sec[k] ? val : sec[k]);
+                mn[k] = lt ? val : mn[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            C[k] = halfc * mn[k];
+            t[k] = xl_m.e[k] * xs_m.e[k];
+            tr[k] = (one + a.zeta * xl_m.e[k]) * (one - xs_m.e[k]);
+            if (MODE != M_ADB) uns[k] = uns[k] || (on[k] && !(C[k] < (T)0.25));
+        }
+        for (int s = s0; s < s1; ++s) {  // :62-81
+            const int lit = ldc(a.lits, s);
+            const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
+            const Vec<T, VEC> vv = ldv<T, VEC>(V + vbase + (size_t)(lit >> 1) * W);
+            Vec<T, VEC> out;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const T vi = vv.e[k];
+                const T val = one - q * vi;
+                const T g_ = halfc * q * (val != mn[k] ? mn[k] : sec[k]);
+                const T r_ = (C[k] == one - q * vi) ? halfc * (q - vi) : (T)0.0;
+                out.e[k] = t[k] * g_ + tr[k] * r_;
+            }
+            stv<T, VEC>(a.w + wbase + (size_t)ldc(a.wpos, s) * W, out);
+        }
+        clause_update<T, VEC, MODE>(a, ci, C, xs_m, xl_m, h, on, all_on, e);
+    }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        if (MODE != M_ADB) {
+            if (uns[k]) a.unsat[geo.r0 + k] = 1u;
+        } else if (on[k]) {
+            atomicMax(&a.err[geo.r0 + k], tobits(e[k]));
+        }
     }
 }
 
 // ------------------------------------------------------------------------------------------------
 // k_variable: system.rs:33,80 (dv in the reference's accumulation order) + :96
 // ------------------------------------------------------------------------------------------------
-template <typename T, int W, int MODE>
+template <typename T, int LW, int VEC, int MODE>
 __global__ __launch_bounds__(256) void k_variable(KArgs<T> a) {
-    constexpr int IPR = 64 / W;
-    const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
-    const int gl = wave / a.tiles;
-    const int tile = wave - gl * a.tiles;
-    if (gl >= a.ng) return;
+    using G_ = Geo<LW, VEC>;
+    constexpr int W = G_::W, IPR = G_::IPR;
+    G_ geo;
+    if (!geo.init(a.tiles, a.g0, a.ng)) return;
     if (*a.stop < a.step) return;
-    const int g = a.g0 + gl;
-    const int rin = lane % W;
-    const int isub = lane / W;
-    const int r = g * W + rin;
-    bool on = a.act[r] != 0;
-    if (MODE == M_ADA || MODE == M_ADB) on = on && a.unsat[r] != 0;
-    if (!__any(on)) return;
-    const T h = (MODE == M_ADA || MODE == M_ADB) ? a.dtr[r] : a.dt;
-    const T half = (T)0.5 * h;
-    const size_t vbase = (size_t)g * a.n * W + rin;
-    const T *__restrict__ wsrc = a.w + (size_t)gl * a.L * W + rin;
-    T e = (T)0.0;
+    bool on[VEC], all_on;
+    T h[VEC];
+    if (!lane_state<T, VEC, MODE, false>(a, geo.r0, on, all_on, h)) return;
+    const size_t vbase = (size_t)geo.g * a.n * W + geo.off;
+    const T *__restrict__ wsrc = a.w + (size_t)geo.gl * a.L * W + geo.off;
+    T e[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) e[k] = (T)0.0;
     for (int row = 0; row < a.rows; ++row) {
-        int i = (tile * a.rows + row) * IPR + isub;
-        if (W == 64) i = __builtin_amdgcn_readfirstlane(i);
+        int i = (geo.tile * a.rows + row) * IPR + geo.isub;
+        if (LW == 64) i = __builtin_amdgcn_readfirstlane(i);
         if (i >= a.n) break;
-        const int p0 = a.vptr[i], p1 = a.vptr[i + 1];
-        T dv = (T)0.0;  // :33
-        int p = p0;
-        for (; p + 4 <= p1; p += 4) {  // independent loads, sequential adds (order kept)
-            const T w0 = wsrc[(size_t)p * W], w1 = wsrc[(size_t)(p + 1) * W];
-            const T w2 = wsrc[(size_t)(p + 2) * W], w3 = wsrc[(size_t)(p + 3) * W];
-            dv += w0;
-            dv += w1;
-            dv += w2;
-            dv += w3;
-        }
-        for (; p < p1; ++p) dv += wsrc[(size_t)p * W];
-        if (!on) continue;
+        const int p0 = ldc(a.vptr, i), p1 = ldc(a.vptr, i + 1);
         const size_t vi = vbase + (size_t)i * W;
+        const Vec<T, VEC> v0 = ldv<T, VEC>(((MODE == M_ADB) ? a.vh : a.v) + vi);  // issued early
+        T dv[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) dv[k] = (T)0.0;  // :33
+        int p = p0;
+        for (; p + 4 <= p1; p += 4) {  // four rows in flight, sequential adds (order kept)
+            const Vec<T, VEC> w0 = ldv<T, VEC>(wsrc + (size_t)p * W);
+            const Vec<T, VEC> w1 = ldv<T, VEC>(wsrc + (size_t)(p + 1) * W);
+            const Vec<T, VEC> w2 = ldv<T, VEC>(wsrc + (size_t)(p + 2) * W);
+            const Vec<T, VEC> w3 = ldv<T, VEC>(wsrc + (size_t)(p + 3) * W);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                dv[k] += w0.e[k];
+                dv[k] += w1.e[k];
+                dv[k] += w2.e[k];
+                dv[k] += w3.e[k];
+            }
+        }
+        for (; p < p1; ++p) {
+            const Vec<T, VEC> w0 = ldv<T, VEC>(wsrc + (size_t)p * W);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) dv[k] += w0.e[k];
+        }
+        Vec<T, VEC> o1, o2;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            if (MODE == M_DERIV) {
+                o1.e[k] = dv[k];
+            } else if (MODE == M_FIXED) {
+                o1.e[k] = dmin(dmax(v0.e[k] + h[k] * dv[k], (T)-1.0), (T)1.0);
+            } else if (MODE == M_ADA) {
+                const T half = (T)0.5 * h[k];
+                o1.e[k] = dmin(dmax(v0.e[k] + h[k] * dv[k], (T)-1.0), (T)1.0);   // full-step clone
+                o2.e[k] = dmin(dmax(v0.e[k] + half * dv[k], (T)-1.0), (T)1.0);  // first half step
+            } else {
+                const T half = (T)0.5 * h[k];
+                o1.e[k] = dmin(dmax(v0.e[k] + half * dv[k], (T)-1.0), (T)1.0);  // second half step
+            }
+        }
         if (MODE == M_DERIV) {
-            a.vh[vi] = dv;
+            stv<T, VEC>(a.vh + vi, o1);
         } else if (MODE == M_FIXED) {
-            a.v[vi] = dmin(dmax(a.v[vi] + h * dv, (T)-1.0), (T)1.0);
+            stv_masked<T, VEC>(a.v + vi, o1, on, all_on);
         } else if (MODE == M_ADA) {
-            const T v0 = a.v[vi];
-            a.vf[vi] = dmin(dmax(v0 + h * dv, (T)-1.0), (T)1.0);
-            a.vh[vi] = dmin(dmax(v0 + half * dv, (T)-1.0), (T)1.0);
+            stv<T, VEC>(a.vf + vi, o1);
+            stv<T, VEC>(a.vh + vi, o2);
         } else {
-            const T vn = dmin(dmax(a.vh[vi] + half * dv, (T)-1.0), (T)1.0);
-            a.v[vi] = vn;
-            e = dmax(e, dabs(a.vf[vi] - vn));
+            const Vec<T, VEC> f = ldv<T, VEC>(a.vf + vi);
+            stv_masked<T, VEC>(a.v + vi, o1, on, all_on);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) e[k] = dmax(e[k], dabs(f.e[k] - o1.e[k]));
         }
     }
-    if (MODE == M_ADB && on) atomicMax(&a.err[r], tobits(e));
+    if (MODE == M_ADB) {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k)
+            if (on[k]) atomicMax(&a.err[geo.r0 + k], tobits(e[k]));
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_status: per-replica bookkeeping after all chunks of one step
+// k_status: per-replica bookkeeping after all kernels of one step of a replica range
 // ------------------------------------------------------------------------------------------------
 struct StatusArgs {
     uint8_t *act;
@@ -438,11 +553,11 @@ template <typename T> __global__ void k_status(StatusArgs s) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// init / layout kernels
+// init / layout kernels (not on the hot path: group width W is a runtime argument)
 // ------------------------------------------------------------------------------------------------
-template <typename T, int W>
-__global__ void k_init(T *v, T *xs, T *xl, const int32_t *cptr, const int32_t *lits, int n, int m,
-                       int G, int B, uint64_t seed, int64_t replica0) {
+template <typename T>
+__global__ void k_init(T *v, T *xs, T *xl, const int32_t *cptr, const int32_t *lits, int n, int m, int G,
+                       int W, int B, uint64_t seed, int64_t replica0) {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t nv = (size_t)G * n * W, nc = (size_t)G * m * W;
     if (tid < nv) {
@@ -464,8 +579,8 @@ __global__ void k_init(T *v, T *xs, T *xl, const int32_t *cptr, const int32_t *l
 }
 
 // compact [count][items] f64 <-> layout [G][items][W] in dtype T
-template <typename T, int W>
-__global__ void k_scatter(T *dst, const double *src, int items, int64_t r0, int64_t count) {
+template <typename T>
+__global__ void k_scatter(T *dst, const double *src, int items, int W, int64_t r0, int64_t count) {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= (size_t)count * items) return;
     const int64_t b = (int64_t)(tid / items);
@@ -474,8 +589,8 @@ __global__ void k_scatter(T *dst, const double *src, int items, int64_t r0, int6
     dst[((size_t)(r / W) * items + i) * W + (r % W)] = (T)src[tid];
 }
 
-template <typename T, int W>
-__global__ void k_gather(double *dst, const T *src, int items, int64_t r0, int64_t count) {
+template <typename T>
+__global__ void k_gather(double *dst, const T *src, int items, int W, int64_t r0, int64_t count) {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= (size_t)count * items) return;
     const int64_t b = (int64_t)(tid / items);
@@ -504,11 +619,10 @@ __global__ void k_reset_replicas(uint8_t *act, uint32_t *unsat, int64_t *sat_ste
 struct odesat_solver {
     int device = 0, dtype = ODESAT_F32;
     int64_t n = 0, m = 0, L = 0, B = 0, Bp = 0;
-    int W = 64, G = 1;
+    int LW = 64, VEC = 1, W = 64, G = 1;
     int chunk_groups = 1;
     int uniform_k = 0;  // every clause has this many literals (0 = mixed widths)
     int schedule = ODESAT_SCHED_AUTO;
-    bool force_generic = false;
     size_t tsize = 4;
     hipStream_t stream = nullptr;
     int32_t *cptr = nullptr, *lits = nullptr, *wpos = nullptr, *vptr = nullptr;
@@ -530,6 +644,26 @@ struct odesat_solver {
 };
 
 namespace {
+
+template <int V> using IC = std::integral_constant<int, V>;
+
+// Call f(IC<LW>, IC<VEC>) with the solver's compile-time layout.
+template <typename T, typename F> int with_layout(const odesat_solver *s, F &&f) {
+    if (s->VEC == 4) {
+        if constexpr (sizeof(T) == 4) return f(IC<64>{}, IC<4>{});
+        else return fail(ODESAT_EINVAL, "VEC=4 is f32-only");
+    }
+    if (s->VEC == 2) return f(IC<64>{}, IC<2>{});
+    switch (s->LW) {
+        case 1: return f(IC<1>{}, IC<1>{});
+        case 2: return f(IC<2>{}, IC<1>{});
+        case 4: return f(IC<4>{}, IC<1>{});
+        case 8: return f(IC<8>{}, IC<1>{});
+        case 16: return f(IC<16>{}, IC<1>{});
+        case 32: return f(IC<32>{}, IC<1>{});
+        default: return f(IC<64>{}, IC<1>{});
+    }
+}
 
 int dmalloc(odesat_solver *s, void **p, size_t bytes) {
     if (bytes == 0) bytes = 16;
@@ -594,10 +728,10 @@ int drain_profile(odesat_solver *s) {
 }
 
 // rows per wave: enough waves to fill 256 CUs many times over, rows >= 1
-int pick_rows(int64_t items_per_group, int ng, int W) {
-    const int64_t ipr = 64 / W;
+int pick_rows(int64_t items_per_group, int ng, int LW) {
+    const int64_t ipr = 64 / LW;
     const int64_t row_total = (items_per_group + ipr - 1) / ipr * ng;
-    int64_t rows = row_total / 16384;
+    const int64_t rows = row_total / 16384;
     return (int)std::max<int64_t>(1, std::min<int64_t>(rows, 16));
 }
 
@@ -629,41 +763,51 @@ template <typename T> KArgs<T> make_args(odesat_solver *s) {
     return a;
 }
 
-template <typename T, int W, int MODE>
+struct Timed {  // brackets one launch with profiling events
+    odesat_solver *s;
+    int cls;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    Timed(odesat_solver *s_, int c) : s(s_), cls(c) {
+        if (s->profile) {
+            e0 = take_event(s);
+            e1 = take_event(s);
+            (void)hipEventRecord(e0, s->stream);
+        }
+    }
+    ~Timed() {
+        if (s->profile) {
+            (void)hipEventRecord(e1, s->stream);
+            s->pending.push_back({cls, e0, e1});
+        }
+    }
+};
+
+template <typename T, int LW, int VEC, int MODE>
 int launch_kernel(odesat_solver *s, KArgs<T> a, bool clause) {
     const int64_t items = clause ? s->m : s->n;
-    a.rows = pick_rows(items, a.ng, W);
-    const int64_t ipr = 64 / W;
+    a.rows = pick_rows(items, a.ng, LW);
+    const int64_t ipr = 64 / LW;
     a.tiles = (int)((items + ipr * a.rows - 1) / (ipr * a.rows));
     if (a.tiles == 0) return ODESAT_OK;
     const int64_t waves = (int64_t)a.tiles * a.ng;
     const int64_t blocks = (waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (blocks > INT_MAX) return fail(ODESAT_EINVAL, "grid too large");
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (s->profile) {
-        e0 = take_event(s);
-        e1 = take_event(s);
-        HIP_TRY(hipEventRecord(e0, s->stream));
+    const dim3 grid((unsigned)blocks), block(64 * WAVES_PER_BLOCK);
+    {
+        Timed tm(s, clause ? 0 : 1);
+        if (clause && s->uniform_k == 3)
+            hipLaunchKernelGGL((k_clause_u<T, LW, VEC, MODE, 3>), grid, block, 0, s->stream, a);
+        else if (clause)
+            hipLaunchKernelGGL((k_clause<T, LW, VEC, MODE>), grid, block, 0, s->stream, a);
+        else
+            hipLaunchKernelGGL((k_variable<T, LW, VEC, MODE>), grid, block, 0, s->stream, a);
     }
-    if (clause && s->uniform_k == 3)
-        hipLaunchKernelGGL((k_clause_u<T, W, MODE, 3>), dim3((unsigned)blocks), dim3(64 * WAVES_PER_BLOCK),
-                           0, s->stream, a);
-    else if (clause)
-        hipLaunchKernelGGL((k_clause<T, W, MODE>), dim3((unsigned)blocks), dim3(64 * WAVES_PER_BLOCK), 0,
-                           s->stream, a);
-    else
-        hipLaunchKernelGGL((k_variable<T, W, MODE>), dim3((unsigned)blocks), dim3(64 * WAVES_PER_BLOCK),
-                           0, s->stream, a);
     HIP_TRY(hipGetLastError());
-    if (s->profile) {
-        HIP_TRY(hipEventRecord(e1, s->stream));
-        s->pending.push_back({clause ? 0 : 1, e0, e1});
-    }
     return ODESAT_OK;
 }
 
-// One RHS(+update) of `mode` for every chunk: k_clause then k_variable per chunk.
-template <typename T, int W, int MODE>
+// One RHS(+update) of `MODE` for the groups [gA, gB): k_clause then k_variable per chunk.
+template <typename T, int LW, int VEC, int MODE>
 int step_chunks(odesat_solver *s, int step, T dt, T zeta, int gA, int gB) {
     KArgs<T> a = make_args<T>(s);
     a.step = step;
@@ -673,14 +817,16 @@ int step_chunks(odesat_solver *s, int step, T dt, T zeta, int gA, int gB) {
     for (int g0 = gA; g0 < gB; g0 += s->chunk_groups) {
         a.g0 = g0;
         a.ng = std::min(s->chunk_groups, gB - g0);
-        if ((rc = launch_kernel<T, W, MODE>(s, a, true))) return rc;
-        if ((rc = launch_kernel<T, W, MODE>(s, a, false))) return rc;
+        if ((rc = launch_kernel<T, LW, VEC, MODE>(s, a, true))) return rc;
+        if ((rc = launch_kernel<T, LW, VEC, MODE>(s, a, false))) return rc;
     }
     return ODESAT_OK;
 }
 
 template <typename T>
 int launch_status(odesat_solver *s, int step, int stop_mode, bool adaptive, double tol, int64_t r0, int64_t r1) {
+    r1 = std::min<int64_t>(r1, s->B);
+    if (r1 <= r0) return ODESAT_OK;
     StatusArgs sa{};
     sa.act = s->act;
     sa.unsat = s->unsat;
@@ -689,113 +835,76 @@ int launch_status(odesat_solver *s, int step, int stop_mode, bool adaptive, doub
     sa.sat_step = s->sat_step;
     sa.steps_done = s->steps_done;
     sa.stop = s->stop;
-    r1 = std::min<int64_t>(r1, s->B);
-    if (r1 <= r0) return ODESAT_OK;
     sa.r0 = (int32_t)r0;
     sa.r1 = (int32_t)r1;
     sa.step = step;
     sa.stop_mode = stop_mode;
     sa.adaptive = adaptive ? 1 : 0;
     sa.tol = tol;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (s->profile) {
-        e0 = take_event(s);
-        e1 = take_event(s);
-        HIP_TRY(hipEventRecord(e0, s->stream));
-    }
     const int threads = 256;
     const int blocks = (int)((r1 - r0 + threads - 1) / threads);
-    hipLaunchKernelGGL((k_status<T>), dim3(blocks), dim3(threads), 0, s->stream, sa);
-    HIP_TRY(hipGetLastError());
-    if (s->profile) {
-        HIP_TRY(hipEventRecord(e1, s->stream));
-        s->pending.push_back({2, e0, e1});
+    {
+        Timed tm(s, 2);
+        hipLaunchKernelGGL((k_status<T>), dim3(blocks), dim3(threads), 0, s->stream, sa);
     }
+    HIP_TRY(hipGetLastError());
     return ODESAT_OK;
 }
 
-// One full euler step (fixed or adaptive) for every replica, enqueued on the stream.
 // One full euler step (fixed or adaptive) for the replica groups [gA, gB), enqueued on the stream.
-template <typename T, int W>
-int enqueue_step(odesat_solver *s, int step, bool adaptive, T dt, T zeta, double tol, int stop_mode, int gA,
-                 int gB) {
-    int rc;
-    if (!adaptive) {
-        if ((rc = step_chunks<T, W, M_FIXED>(s, step, dt, zeta, gA, gB))) return rc;
-    } else {
-        // all chunks' first half before any second half would need one contribution buffer per chunk;
-        // the half steps of one chunk run back to back instead
+template <typename T>
+int enqueue_step(odesat_solver *s, int step, bool adaptive, double dt, double zeta, double tol, int stop_mode,
+                 int gA, int gB) {
+    int rc = with_layout<T>(s, [&](auto lw, auto vec) -> int {
+        constexpr int LW = decltype(lw)::value, VEC = decltype(vec)::value;
+        int r;
+        if (!adaptive) return step_chunks<T, LW, VEC, M_FIXED>(s, step, (T)dt, (T)zeta, gA, gB);
+        // the two half steps of one chunk run back to back (one contribution buffer per chunk)
         for (int g0 = gA; g0 < gB; g0 += s->chunk_groups) {
             const int g1 = std::min(gB, g0 + s->chunk_groups);
-            if ((rc = step_chunks<T, W, M_ADA>(s, step, dt, zeta, g0, g1))) return rc;
-            if ((rc = step_chunks<T, W, M_ADB>(s, step, dt, zeta, g0, g1))) return rc;
+            if ((r = step_chunks<T, LW, VEC, M_ADA>(s, step, (T)dt, (T)zeta, g0, g1))) return r;
+            if ((r = step_chunks<T, LW, VEC, M_ADB>(s, step, (T)dt, (T)zeta, g0, g1))) return r;
         }
-    }
+        return ODESAT_OK;
+    });
+    if (rc) return rc;
     return launch_status<T>(s, step, stop_mode, adaptive, tol, (int64_t)gA * s->W, (int64_t)gB * s->W);
 }
 
-template <typename T>
-int dispatch_step(odesat_solver *s, int step, bool adaptive, double dt, double zeta, double tol,
-                  int stop_mode, int gA, int gB) {
-    switch (s->W) {
-        case 1: return enqueue_step<T, 1>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
-        case 2: return enqueue_step<T, 2>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
-        case 4: return enqueue_step<T, 4>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
-        case 8: return enqueue_step<T, 8>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
-        case 16: return enqueue_step<T, 16>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
-        case 32: return enqueue_step<T, 32>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
-        default: return enqueue_step<T, 64>(s, step, adaptive, (T)dt, (T)zeta, tol, stop_mode, gA, gB);
-    }
+int dispatch_step(odesat_solver *s, int step, bool adaptive, double dt, double zeta, double tol, int stop_mode,
+                  int gA, int gB) {
+    return s->dtype == ODESAT_F64 ? enqueue_step<double>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB)
+                                  : enqueue_step<float>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB);
+}
+
+template <typename T> int deriv_t(odesat_solver *s, double zeta) {
+    return with_layout<T>(s, [&](auto lw, auto vec) -> int {
+        constexpr int LW = decltype(lw)::value, VEC = decltype(vec)::value;
+        return step_chunks<T, LW, VEC, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
+    });
 }
 
 template <typename T>
-int dispatch_deriv(odesat_solver *s, double zeta) {
-    switch (s->W) {
-        case 1: return step_chunks<T, 1, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
-        case 2: return step_chunks<T, 2, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
-        case 4: return step_chunks<T, 4, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
-        case 8: return step_chunks<T, 8, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
-        case 16: return step_chunks<T, 16, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
-        case 32: return step_chunks<T, 32, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
-        default: return step_chunks<T, 64, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
-    }
-}
-
-template <typename T, int W>
-int launch_layout(odesat_solver *s, void *dev, const double *dsrc, double *ddst, int64_t items,
-                  int64_t r0, int64_t count, bool scatter) {
+int layout_t(odesat_solver *s, void *dev, const double *dsrc, double *ddst, int64_t items, int64_t r0,
+             int64_t count, bool scatter) {
     const size_t total = (size_t)count * items;
     if (!total) return ODESAT_OK;
     const int threads = 256;
     const size_t blocks = (total + threads - 1) / threads;
     if (scatter)
-        hipLaunchKernelGGL((k_scatter<T, W>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, (T *)dev,
-                           dsrc, (int)items, r0, count);
+        hipLaunchKernelGGL((k_scatter<T>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, (T *)dev, dsrc,
+                           (int)items, s->W, r0, count);
     else
-        hipLaunchKernelGGL((k_gather<T, W>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, ddst,
-                           (const T *)dev, (int)items, r0, count);
+        hipLaunchKernelGGL((k_gather<T>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, ddst,
+                           (const T *)dev, (int)items, s->W, r0, count);
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
 }
 
-template <typename T>
-int layout_dispatch(odesat_solver *s, void *dev, const double *dsrc, double *ddst, int64_t items, int64_t r0,
-                    int64_t count, bool scatter) {
-    switch (s->W) {
-        case 1: return launch_layout<T, 1>(s, dev, dsrc, ddst, items, r0, count, scatter);
-        case 2: return launch_layout<T, 2>(s, dev, dsrc, ddst, items, r0, count, scatter);
-        case 4: return launch_layout<T, 4>(s, dev, dsrc, ddst, items, r0, count, scatter);
-        case 8: return launch_layout<T, 8>(s, dev, dsrc, ddst, items, r0, count, scatter);
-        case 16: return launch_layout<T, 16>(s, dev, dsrc, ddst, items, r0, count, scatter);
-        case 32: return launch_layout<T, 32>(s, dev, dsrc, ddst, items, r0, count, scatter);
-        default: return launch_layout<T, 64>(s, dev, dsrc, ddst, items, r0, count, scatter);
-    }
-}
-
 int layout(odesat_solver *s, void *dev, const double *dsrc, double *ddst, int64_t items, int64_t r0,
            int64_t count, bool scatter) {
-    return s->dtype == ODESAT_F64 ? layout_dispatch<double>(s, dev, dsrc, ddst, items, r0, count, scatter)
-                                  : layout_dispatch<float>(s, dev, dsrc, ddst, items, r0, count, scatter);
+    return s->dtype == ODESAT_F64 ? layout_t<double>(s, dev, dsrc, ddst, items, r0, count, scatter)
+                                  : layout_t<float>(s, dev, dsrc, ddst, items, r0, count, scatter);
 }
 
 // host f64 [count][items] <-> device layout, through a device staging buffer
@@ -851,30 +960,19 @@ int check_solver(odesat_solver *s) {
     return ODESAT_OK;
 }
 
-template <typename T, int W>
-int init_dispatch_w(odesat_solver *s, uint64_t seed, int64_t replica0) {
+template <typename T> int init_t(odesat_solver *s, uint64_t seed, int64_t replica0) {
     const size_t total = std::max(state_elems(s, s->n), state_elems(s, s->m));
     if (!total) return ODESAT_OK;
     const int threads = 256;
     const size_t blocks = (total + threads - 1) / threads;
-    hipLaunchKernelGGL((k_init<T, W>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, (T *)s->v,
-                       (T *)s->xs, (T *)s->xl, s->cptr, s->lits, (int)s->n, (int)s->m, s->G, (int)s->B,
-                       seed, replica0);
+    hipLaunchKernelGGL((k_init<T>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, (T *)s->v, (T *)s->xs,
+                       (T *)s->xl, s->cptr, s->lits, (int)s->n, (int)s->m, s->G, s->W, (int)s->B, seed, replica0);
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
 }
 
-template <typename T>
 int init_dispatch(odesat_solver *s, uint64_t seed, int64_t replica0) {
-    switch (s->W) {
-        case 1: return init_dispatch_w<T, 1>(s, seed, replica0);
-        case 2: return init_dispatch_w<T, 2>(s, seed, replica0);
-        case 4: return init_dispatch_w<T, 4>(s, seed, replica0);
-        case 8: return init_dispatch_w<T, 8>(s, seed, replica0);
-        case 16: return init_dispatch_w<T, 16>(s, seed, replica0);
-        case 32: return init_dispatch_w<T, 32>(s, seed, replica0);
-        default: return init_dispatch_w<T, 64>(s, seed, replica0);
-    }
+    return s->dtype == ODESAT_F64 ? init_t<double>(s, seed, replica0) : init_t<float>(s, seed, replica0);
 }
 
 double default_zeta(const odesat_solver *s) {  // system.rs:164-173
@@ -883,16 +981,50 @@ double default_zeta(const odesat_solver *s) {  // system.rs:164-173
 }
 
 void pick_chunk(odesat_solver *s, int64_t replicas) {
-    const int64_t per_group = s->L * s->W * (int64_t)s->tsize;
+    // one chunk = state + contribution buffer of chunk_groups groups
+    const int64_t per_group = (s->n + 2 * s->m + s->L) * s->W * (int64_t)s->tsize;
     int64_t groups;
     if (replicas > 0) {
         groups = std::max<int64_t>(1, replicas / s->W);
     } else {
-        // keep one chunk's contribution buffer well inside the 256 MiB Infinity Cache
-        const int64_t budget = 64ll << 20;
+        // keep one chunk's working set well inside the 256 MiB Infinity Cache
+        const int64_t budget = 120ll << 20;
         groups = std::max<int64_t>(1, budget / std::max<int64_t>(per_group, 1));
     }
     s->chunk_groups = (int)std::min<int64_t>(groups, s->G);
+}
+
+std::vector<int64_t> host_i64(int64_t n, int64_t v) { return std::vector<int64_t>((size_t)n, v); }
+
+int put_dt(odesat_solver *s, const double *vals, double fill) {
+    if (s->dtype == ODESAT_F64) {
+        std::vector<double> h(s->Bp, fill);
+        if (vals) for (int64_t r = 0; r < s->B; ++r) h[r] = vals[r];
+        HIP_TRY(hipMemcpy(s->dtr, h.data(), s->Bp * 8, hipMemcpyHostToDevice));
+    } else {
+        std::vector<float> h(s->Bp, (float)fill);
+        if (vals) for (int64_t r = 0; r < s->B; ++r) h[r] = (float)vals[r];
+        HIP_TRY(hipMemcpy(s->dtr, h.data(), s->Bp * 4, hipMemcpyHostToDevice));
+    }
+    return ODESAT_OK;
+}
+
+int get_dt(odesat_solver *s, double *out) {
+    if (s->dtype == ODESAT_F64) {
+        HIP_TRY(hipMemcpy(out, s->dtr, s->B * 8, hipMemcpyDeviceToHost));
+    } else {
+        std::vector<float> h(s->B);
+        HIP_TRY(hipMemcpy(h.data(), s->dtr, s->B * 4, hipMemcpyDeviceToHost));
+        for (int64_t r = 0; r < s->B; ++r) out[r] = h[r];
+    }
+    return ODESAT_OK;
+}
+
+int set_all_active(odesat_solver *s) {
+    std::vector<uint8_t> on(s->Bp, 0);
+    for (int64_t r = 0; r < s->B; ++r) on[r] = 1;
+    HIP_TRY(hipMemcpy(s->act, on.data(), s->Bp, hipMemcpyHostToDevice));
+    return ODESAT_OK;
 }
 
 }  // namespace
@@ -900,7 +1032,7 @@ void pick_chunk(odesat_solver *s, int64_t replicas) {
 // ================================================================================================
 // C ABI
 // ================================================================================================
-extern "C" const char *odesat_version(void) { return "odesat_amd 0.1 (gfx950)"; }
+extern "C" const char *odesat_version(void) { return "odesat_amd 0.2 (gfx950)"; }
 
 extern "C" int odesat_device_count(int *count) {
     if (!count) return fail(ODESAT_EINVAL, "null count");
@@ -936,7 +1068,8 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     if (dtype != ODESAT_F32 && dtype != ODESAT_F64) return fail(ODESAT_EINVAL, "dtype must be ODESAT_F32 or ODESAT_F64");
     const int64_t n = f->varnum, m = f->nclauses(), L = f->nliterals();
     if (n <= 0) return fail(ODESAT_EINVAL, "varnum must be > 0");
-    if (n >= (1ll << 30) || m >= INT_MAX || L >= INT_MAX) return fail(ODESAT_EINVAL, "formula too large");
+    if (n >= (1ll << 30) || m >= INT_MAX / 4 || L >= INT_MAX || batch >= INT_MAX / 2)
+        return fail(ODESAT_EINVAL, "formula or batch too large");
     for (int64_t s = 0; s < L; ++s)
         if (f->var[s] < 0 || f->var[s] >= n)
             return fail(ODESAT_EINVAL, "variable " + std::to_string(f->var[s]) + " out of range [0, " +
@@ -961,11 +1094,23 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     s->m = m;
     s->L = L;
     s->B = batch;
-    int W = 1;
-    while (W < batch && W < 64) W <<= 1;
-    s->W = W;
-    s->Bp = (batch + W - 1) / W * W;
-    s->G = (int)(s->Bp / W);
+    // layout: 16-byte lanes once a batch fills 64 lanes of 16 B
+    const int vmax = 16 / (int)s->tsize;
+    if (batch >= 64 * vmax) {
+        s->LW = 64;
+        s->VEC = vmax;
+    } else if (batch >= 128 && vmax >= 2) {
+        s->LW = 64;
+        s->VEC = 2;
+    } else {
+        int lw = 1;
+        while (lw < batch && lw < 64) lw <<= 1;
+        s->LW = lw;
+        s->VEC = 1;
+    }
+    s->W = s->LW * s->VEC;
+    s->Bp = (batch + s->W - 1) / s->W * s->W;
+    s->G = (int)(s->Bp / s->W);
     pick_chunk(s, 0);
     s->uniform_k = m > 0 ? (int)(f->clause_ptr[1] - f->clause_ptr[0]) : 0;
     for (int64_t c = 0; c < m && s->uniform_k; ++c)
@@ -1011,12 +1156,10 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     if ((rc = dmalloc(s, (void **)&s->sat_step, s->Bp * 8))) return bail(rc);
     if ((rc = dmalloc(s, (void **)&s->steps_done, s->Bp * 8))) return bail(rc);
     if ((rc = dmalloc(s, (void **)&s->stop, 16))) return bail(rc);
-    if (hipMemsetAsync(s->err, 0, s->Bp * 8, s->stream) != hipSuccess ||
-        hipMemsetAsync(s->v, 0, state_elems(s, n) * s->tsize, s->stream) != hipSuccess)
+    if (hipMemsetAsync(s->err, 0, s->Bp * 8, s->stream) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "memset failed"));
-    // default state: v = 0, xs = init_short_term_memory, xl = 1 (k_init with v forced to 0 after)
-    rc = dtype == ODESAT_F64 ? init_dispatch<double>(s, 0, 0) : init_dispatch<float>(s, 0, 0);
-    if (rc) return bail(rc);
+    // default state: v = 0, xs = init_short_term_memory, xl = 1
+    if ((rc = init_dispatch(s, 0, 0))) return bail(rc);
     if (hipMemsetAsync(s->v, 0, state_elems(s, n) * s->tsize, s->stream) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "memset failed"));
     if ((rc = reset_replicas(s, 0, s->Bp))) return bail(rc);
@@ -1068,8 +1211,7 @@ extern "C" int odesat_set_state(odesat_solver *s, int64_t r0, int64_t count, con
 extern "C" int odesat_init_state(odesat_solver *s, uint64_t seed, int64_t replica0) {
     int rc;
     if ((rc = check_solver(s))) return rc;
-    rc = s->dtype == ODESAT_F64 ? init_dispatch<double>(s, seed, replica0) : init_dispatch<float>(s, seed, replica0);
-    if (rc) return rc;
+    if ((rc = init_dispatch(s, seed, replica0))) return rc;
     if ((rc = reset_replicas(s, 0, s->Bp))) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ODESAT_OK;
@@ -1104,13 +1246,9 @@ extern "C" int odesat_compute_derivatives(odesat_solver *s, double zeta, double 
     // every real replica evaluates (act = 1) without touching the stored sat bookkeeping
     std::vector<uint8_t> act_save(s->Bp);
     HIP_TRY(hipMemcpy(act_save.data(), s->act, s->Bp, hipMemcpyDeviceToHost));
-    {
-        std::vector<uint8_t> on(s->Bp, 0);
-        for (int64_t r = 0; r < s->B; ++r) on[r] = 1;
-        HIP_TRY(hipMemcpy(s->act, on.data(), s->Bp, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemset(s->unsat, 0, s->Bp * 4));
-    }
-    rc = s->dtype == ODESAT_F64 ? dispatch_deriv<double>(s, zeta) : dispatch_deriv<float>(s, zeta);
+    if ((rc = set_all_active(s))) return rc;
+    HIP_TRY(hipMemset(s->unsat, 0, s->Bp * 4));
+    rc = s->dtype == ODESAT_F64 ? deriv_t<double>(s, zeta) : deriv_t<float>(s, zeta);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
     if ((rc = download_items(s, s->vh, dv, s->n, 0, s->B))) return rc;
@@ -1126,7 +1264,7 @@ extern "C" int odesat_compute_derivatives(odesat_solver *s, double zeta, double 
     return drain_profile(s);
 }
 
-// single steps share odesat_simulate's machinery with max_steps = 1 and STOP_NONE bookkeeping
+// one step of every replica, with STOP_NONE bookkeeping that is restored afterwards
 static int single_step(odesat_solver *s, bool adaptive, double tol, double dt, double zeta, double *dt_io,
                        uint8_t *allsat) {
     int rc;
@@ -1135,44 +1273,21 @@ static int single_step(odesat_solver *s, bool adaptive, double tol, double dt, d
     if ((rc = ensure_w(s))) return rc;
     if (adaptive && (rc = ensure_scratch(s))) return rc;
     if ((rc = set_stop(s, INT_MAX))) return rc;
-    std::vector<uint8_t> act_save(s->Bp), on(s->Bp, 0);
+    std::vector<uint8_t> act_save(s->Bp);
     HIP_TRY(hipMemcpy(act_save.data(), s->act, s->Bp, hipMemcpyDeviceToHost));
-    for (int64_t r = 0; r < s->B; ++r) on[r] = 1;
-    HIP_TRY(hipMemcpy(s->act, on.data(), s->Bp, hipMemcpyHostToDevice));
-    if (adaptive && dt_io) {
-        if (s->dtype == ODESAT_F64) {
-            std::vector<double> h(s->Bp, 0.01);
-            for (int64_t r = 0; r < s->B; ++r) h[r] = dt_io[r];
-            HIP_TRY(hipMemcpy(s->dtr, h.data(), s->Bp * 8, hipMemcpyHostToDevice));
-        } else {
-            std::vector<float> h(s->Bp, 0.01f);
-            for (int64_t r = 0; r < s->B; ++r) h[r] = (float)dt_io[r];
-            HIP_TRY(hipMemcpy(s->dtr, h.data(), s->Bp * 4, hipMemcpyHostToDevice));
-        }
-    }
-    std::vector<int64_t> sat_save(s->Bp), done_save(s->Bp), minus(s->Bp, -1);
+    if ((rc = set_all_active(s))) return rc;
+    if (adaptive && dt_io && (rc = put_dt(s, dt_io, 0.01))) return rc;
+    std::vector<int64_t> sat_save(s->Bp), done_save(s->Bp), minus = host_i64(s->Bp, -1);
     HIP_TRY(hipMemcpy(sat_save.data(), s->sat_step, s->Bp * 8, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(done_save.data(), s->steps_done, s->Bp * 8, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(s->sat_step, minus.data(), s->Bp * 8, hipMemcpyHostToDevice));
-    rc = s->dtype == ODESAT_F64 ? dispatch_step<double>(s, 0, adaptive, dt, zeta, tol, ODESAT_STOP_NONE, 0, s->G)
-                                : dispatch_step<float>(s, 0, adaptive, dt, zeta, tol, ODESAT_STOP_NONE, 0, s->G);
-    if (rc) return rc;
+    if ((rc = dispatch_step(s, 0, adaptive, dt, zeta, tol, ODESAT_STOP_NONE, 0, s->G))) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
     std::vector<int64_t> sat(s->Bp);
     HIP_TRY(hipMemcpy(sat.data(), s->sat_step, s->Bp * 8, hipMemcpyDeviceToHost));
     if (allsat)
         for (int64_t r = 0; r < s->B; ++r) allsat[r] = sat[r] == 0;
-    if (adaptive && dt_io) {
-        if (s->dtype == ODESAT_F64) {
-            std::vector<double> h(s->Bp);
-            HIP_TRY(hipMemcpy(h.data(), s->dtr, s->Bp * 8, hipMemcpyDeviceToHost));
-            for (int64_t r = 0; r < s->B; ++r) dt_io[r] = h[r];
-        } else {
-            std::vector<float> h(s->Bp);
-            HIP_TRY(hipMemcpy(h.data(), s->dtr, s->Bp * 4, hipMemcpyDeviceToHost));
-            for (int64_t r = 0; r < s->B; ++r) dt_io[r] = h[r];
-        }
-    }
+    if (adaptive && dt_io && (rc = get_dt(s, dt_io))) return rc;
     HIP_TRY(hipMemcpy(s->act, act_save.data(), s->Bp, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(s->sat_step, sat_save.data(), s->Bp * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(s->steps_done, done_save.data(), s->Bp * 8, hipMemcpyHostToDevice));
@@ -1203,21 +1318,11 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
     if (adaptive && (rc = ensure_scratch(s))) return rc;
     if ((rc = set_stop(s, INT_MAX))) return rc;
     {   // per-call bookkeeping: sat step / steps done restart; adaptive dt restarts at 0.01 (:205)
-        std::vector<int64_t> minus(s->Bp, -1), zero(s->Bp, 0);
+        std::vector<int64_t> minus = host_i64(s->Bp, -1), zero = host_i64(s->Bp, 0);
         HIP_TRY(hipMemcpy(s->sat_step, minus.data(), s->Bp * 8, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(s->steps_done, zero.data(), s->Bp * 8, hipMemcpyHostToDevice));
-        std::vector<uint8_t> on(s->Bp, 0);
-        for (int64_t r = 0; r < s->B; ++r) on[r] = 1;
-        HIP_TRY(hipMemcpy(s->act, on.data(), s->Bp, hipMemcpyHostToDevice));
-        if (adaptive) {
-            if (s->dtype == ODESAT_F64) {
-                std::vector<double> h(s->Bp, 0.01);
-                HIP_TRY(hipMemcpy(s->dtr, h.data(), s->Bp * 8, hipMemcpyHostToDevice));
-            } else {
-                std::vector<float> h(s->Bp, 0.01f);
-                HIP_TRY(hipMemcpy(s->dtr, h.data(), s->Bp * 4, hipMemcpyHostToDevice));
-            }
-        }
+        if ((rc = set_all_active(s))) return rc;
+        if (adaptive && (rc = put_dt(s, nullptr, 0.01))) return rc;
     }
     const int poll = p->poll_interval > 0 ? p->poll_interval : 32;
     int32_t *h_stop = nullptr;
@@ -1241,10 +1346,7 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
         const int64_t r0 = (int64_t)gA * s->W, r1 = std::min<int64_t>((int64_t)gB * s->W, s->B);
         int64_t t = 0;
         for (; t < p->max_steps; ++t) {
-            rc = s->dtype == ODESAT_F64
-                     ? dispatch_step<double>(s, (int)t, adaptive, p->dt, zeta, tol, p->stop, gA, gB)
-                     : dispatch_step<float>(s, (int)t, adaptive, p->dt, zeta, tol, p->stop, gA, gB);
-            if (rc) break;
+            if ((rc = dispatch_step(s, (int)t, adaptive, p->dt, zeta, tol, p->stop, gA, gB))) break;
             if (p->stop != ODESAT_STOP_NONE && (t + 1) % poll == 0 && t + 1 < p->max_steps) {
                 // poll the stop condition (results are exact regardless: later launches are no-ops)
                 if (hipMemcpyAsync(h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
@@ -1263,23 +1365,18 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
         }
         t_run = std::max(t_run, t);
     }
-    const int64_t t = t_run;
     (void)hipHostFree(h_stop);
     (void)hipHostFree(h_act);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
-    if (steps_run) *steps_run = t;
+    if (steps_run) *steps_run = t_run;
     if (first_sat_step) HIP_TRY(hipMemcpy(first_sat_step, s->sat_step, s->B * 8, hipMemcpyDeviceToHost));
     if (steps_done) HIP_TRY(hipMemcpy(steps_done, s->steps_done, s->B * 8, hipMemcpyDeviceToHost));
     if (dt_out) {
         if (!adaptive) {
             for (int64_t r = 0; r < s->B; ++r) dt_out[r] = p->dt;
-        } else if (s->dtype == ODESAT_F64) {
-            HIP_TRY(hipMemcpy(dt_out, s->dtr, s->B * 8, hipMemcpyDeviceToHost));
-        } else {
-            std::vector<float> h(s->B);
-            HIP_TRY(hipMemcpy(h.data(), s->dtr, s->B * 4, hipMemcpyDeviceToHost));
-            for (int64_t r = 0; r < s->B; ++r) dt_out[r] = h[r];
+        } else if ((rc = get_dt(s, dt_out))) {
+            return rc;
         }
     }
     return s->profile ? ODESAT_OK : drain_profile(s);
@@ -1316,7 +1413,7 @@ extern "C" int odesat_profile_read(odesat_solver *s, double *ms, int64_t *launch
 }
 
 extern "C" int64_t odesat_clause_kernel_bytes(const odesat_solver *s) {
-    // per launch over the whole batch: v gathered once (4n), xs/xl read + written (16m), in dtype
+    // per step over the whole batch: v gathered once (4n), xs/xl read + written (16m), in dtype
     if (!s) return -1;
     return (int64_t)s->B * (s->n + 4 * s->m) * (int64_t)s->tsize;
 }
