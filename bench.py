@@ -151,7 +151,8 @@ def main():
     if args.traffic and os.path.exists(args.traffic):
         with open(args.traffic) as fh:
             traffic = json.load(fh).get("clause_kernel_hbm_bytes_per_launch")
-    step_bytes = B * (8 * n + 16 * m) * (4 if args.dtype == "f32" else 8)  # algorithmic, per GPU-step
+    tsize = 4 if args.dtype == "f32" else 8
+    step_bytes = B * (2 * n + 4 * m) * tsize  # algorithmic per GPU-step: v, xs, xl read + written once
 
     extra = None
     if args.extra_batch and args.extra_batch != B:

@@ -151,7 +151,8 @@ int odesat_synchronize(odesat_solver *s);
  * kernel), the summed device milliseconds and the launch count since the last reset. */
 int odesat_profile_enable(odesat_solver *s, int enable);
 int odesat_profile_read(odesat_solver *s, double *ms /*[3]*/, int64_t *launches /*[3]*/);
-/* Algorithmic bytes per launch of the clause kernel over the whole batch (roofline). */
+/* Algorithmic bytes per step of the dominant kernel over the whole batch (roofline):
+ * FUSED k_step (2n + 4m) * dtype bytes per replica, TWOPASS k_clause (n + 4m) * dtype bytes. */
 int64_t odesat_clause_kernel_bytes(const odesat_solver *s);
 /* Tuning: replicas per chunk (0 = automatic) -- the batch is stepped chunk by chunk so the
  * contribution buffer of one chunk stays resident in the Infinity Cache. */
@@ -162,6 +163,12 @@ int odesat_set_chunk_replicas(odesat_solver *s, int64_t replicas);
 #define ODESAT_SCHED_STEP_MAJOR 1  /* every step: all chunks, then the next step */
 #define ODESAT_SCHED_CHUNK_MAJOR 2 /* every chunk: all steps, then the next chunk */
 int odesat_set_schedule(odesat_solver *s, int schedule);
+/* Per-step algorithm (results are bit-identical):
+ * FUSED   = one variable-major kernel per RHS, clauses recomputed from L2-resident voltages;
+ * TWOPASS = clause kernel writing per-literal contributions + variable kernel summing them. */
+#define ODESAT_ALG_FUSED 0
+#define ODESAT_ALG_TWOPASS 1
+int odesat_set_algorithm(odesat_solver *s, int alg);
 
 #ifdef __cplusplus
 }

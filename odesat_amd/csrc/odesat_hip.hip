@@ -1,26 +1,5 @@
-// odesat_hip.hip -- MI355X (gfx950) integrator for the Bearden-Pei-Di Ventra memcomputing ODE:
-// the replacement of /root/reference/src/system.rs:25-359 behind the C ABI of include/odesat.h.
-//
-// Device layout.  Every per-item array (item = variable or clause) is
-// replica-innermost in groups of W replicas:  X[g][item][W],  replica r = g*W + j.
-// A wave covers one "row": LW lanes per item, VEC contiguous replicas per lane, W = LW*VEC.
-//   * batches >= 256 (f32) / >= 128 (f64):  LW = 64, VEC = 16 B / sizeof(T): one wave = the
-//     W replicas of ONE clause / variable, every state access is a 1 KiB dwordx4 wave-load, literal
-//     indices are wave-uniform scalar loads;
-//   * 128 <= B < 256 (f32): LW = 64, VEC = 2; 64 <= B < 128: LW = 64, VEC = 1;
-//   * B < 64: LW = next pow2 >= B, VEC = 1: a wave spans 64/LW items.
-// One Euler step = two kernels per replica chunk + one status kernel:
-//   k_clause   (system.rs:35-90)   per clause: gather the literal voltages, strict-< min/second-min,
-//              C, G, R, the per-literal dv contribution, dxs/dxl, the fused update_state of xs/xl
-//              (system.rs:94-95) and the per-replica "some clause unsat" flag.  The contribution of
-//              slot s is stored at w[g][wpos[s]][W]: slots are laid out variable-major (each
-//              variable's slots sorted by clause, then literal position).
-//   k_variable (system.rs:80,96)   per variable: dv = 0 + w[..] summed over its slots in that
-//              order -- exactly the reference's sequential scatter order, so f32 and f64 results are
-//              bit-identical to the CPU oracle -- then the clamped v update.  No atomics.
-//   k_status   (system.rs:149-153, 122-136, 190-235, 291) per replica: sat bookkeeping, stop
-//              policy, adaptive dt.
-// FP contraction is OFF: every + and * rounds exactly as written in system.rs, in the solver dtype.
+// odesat_hip.hip -- host side and C ABI of libodesat_hip.so: the MI355X replacement of
+// /root/reference/src/system.rs:25-359 (include/odesat.h).  Device code: kernels.hpp.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -29,6 +8,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -37,8 +17,10 @@
 
 #include "../../include/odesat.h"
 #include "cnf.hpp"
+#include "kernels.hpp"
 
 using odesat::fail;
+using namespace odk;
 
 #define HIP_TRY(expr)                                                                         \
     do {                                                                                      \
@@ -47,575 +29,6 @@ using odesat::fail;
             return fail(ODESAT_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));   \
     } while (0)
 
-namespace {
-
-// ------------------------------------------------------------------------------------------------
-// device helpers
-// ------------------------------------------------------------------------------------------------
-template <typename T> struct Bits;
-template <> struct Bits<float> { using U = uint32_t; };
-template <> struct Bits<double> { using U = unsigned long long; };
-
-__device__ __forceinline__ float dmax(float a, float b) { return fmaxf(a, b); }
-__device__ __forceinline__ double dmax(double a, double b) { return fmax(a, b); }
-__device__ __forceinline__ float dmin(float a, float b) { return fminf(a, b); }
-__device__ __forceinline__ double dmin(double a, double b) { return fmin(a, b); }
-__device__ __forceinline__ float dabs(float a) { return fabsf(a); }
-__device__ __forceinline__ double dabs(double a) { return fabs(a); }
-__device__ __forceinline__ float dsqrt(float a) { return sqrtf(a); }
-__device__ __forceinline__ double dsqrt(double a) { return sqrt(a); }
-__device__ __forceinline__ uint32_t tobits(float x) { return __float_as_uint(x); }
-__device__ __forceinline__ unsigned long long tobits(double x) {
-    return (unsigned long long)__double_as_longlong(x);
-}
-__device__ __forceinline__ float frombits(uint32_t x) { return __uint_as_float(x); }
-__device__ __forceinline__ double frombits(unsigned long long x) {
-    return __longlong_as_double((long long)x);
-}
-template <typename T> __device__ __forceinline__ T inf_v() { return (T)__builtin_huge_val(); }
-
-// VEC contiguous elements, loaded / stored as one 4-, 8- or 16-byte access per lane
-template <typename T, int N> struct alignas(sizeof(T) * N) Vec {
-    T e[N];
-};
-template <typename T, int N> __device__ __forceinline__ Vec<T, N> ldv(const T *p) {
-    return *reinterpret_cast<const Vec<T, N> *>(p);
-}
-template <typename T, int N> __device__ __forceinline__ void stv(T *p, const Vec<T, N> &x) {
-    *reinterpret_cast<Vec<T, N> *>(p) = x;
-}
-// store only the active elements (a partially frozen lane must not overwrite frozen replicas)
-template <typename T, int N>
-__device__ __forceinline__ void stv_masked(T *p, const Vec<T, N> &x, const bool (&on)[N], bool all_on) {
-    if (all_on) {
-        stv<T, N>(p, x);
-    } else {
-#pragma unroll
-        for (int k = 0; k < N; ++k)
-            if (on[k]) p[k] = x.e[k];
-    }
-}
-
-// splitmix64 counter RNG -- same function as oracle/odesat_oracle.c (oc_hash3).
-__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-    return z ^ (z >> 31);
-}
-__host__ __device__ __forceinline__ double init_voltage(uint64_t seed, uint64_t replica, uint64_t var) {
-    uint64_t h = mix64(seed + 0x9E3779B97F4A7C15ULL);
-    h = mix64(h ^ (replica * 0xD1B54A32D192ED03ULL + 0x632BE59BD9B4E019ULL));
-    h = mix64(h ^ (var * 0x8CB92BA72F3D8DD7ULL + 0x9E3779B97F4A7C15ULL));
-    const double u = (double)(h >> 11) * (1.0 / 9007199254740992.0);
-    return u * 2.0 - 1.0;
-}
-
-enum Mode : int { M_DERIV = 0, M_FIXED = 1, M_ADA = 2, M_ADB = 3 };
-
-// The topology arrays are never written by a kernel: reading them through the constant address
-// space lets wave-uniform indices become scalar (s_load) loads on the scalar cache.
-typedef const __attribute__((address_space(4))) int32_t cint32;
-__device__ __forceinline__ int32_t ldc(const int32_t *p, size_t i) { return ((cint32 *)p)[i]; }
-
-template <typename T> struct KArgs {
-    const int32_t *__restrict__ cptr;  // [m+1]
-    const int32_t *__restrict__ lits;  // [L] var<<1 | neg, file order
-    const int32_t *__restrict__ wpos;  // [L] slot -> variable-major position
-    const int32_t *__restrict__ vptr;  // [n+1] variable -> first variable-major position
-    T *v, *xs, *xl;                    // state        [G][n|m][W]
-    T *w;                              // contributions [chunk groups][L][W]
-    T *vh, *vf, *xsh, *xlh, *xsf, *xlf;  // half / full candidates (adaptive), derivatives (DERIV)
-    T *dtr;                            // [Bp] per-replica adaptive dt
-    typename Bits<T>::U *err;          // [Bp] max_error bits (non-negative floats order as ints)
-    uint32_t *unsat;                   // [Bp] 1 = some clause had C >= gamma this step
-    uint8_t *act;                      // [Bp] replica still stepping
-    const int32_t *stop;               // first stop step (INT_MAX = none)
-    int32_t n, m, L;
-    int32_t g0, ng;                    // group range of this chunk
-    int32_t rows;                      // rows (of 64/LW items) per wave
-    int32_t tiles;                     // waves per group
-    int32_t step;
-    T dt, zeta, xl_max;
-};
-
-constexpr int WAVES_PER_BLOCK = 4;
-
-// Per-wave geometry shared by the kernels.
-template <int LW, int VEC> struct Geo {
-    static constexpr int W = LW * VEC;  // replicas per group
-    static constexpr int IPR = 64 / LW; // items per wave row
-    int gl, g, tile, isub, lin;
-    size_t off;  // element offset of this lane's first replica inside an item row
-    int r0;      // this lane's first replica
-    __device__ __forceinline__ bool init(int tiles, int g0, int ng) {
-        const int lane = threadIdx.x & 63;
-        const int wave = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
-        gl = wave / tiles;
-        tile = wave - gl * tiles;
-        if (gl >= ng) return false;
-        g = g0 + gl;
-        lin = lane % LW;
-        isub = lane / LW;
-        off = (size_t)lin * VEC;
-        r0 = g * W + lin * VEC;
-        return true;
-    }
-};
-
-// :84-85 memory derivatives, then (by mode) the fused update_state of xs / xl (:94-95), the
-// adaptive half / full candidates (:124-130) or the second half step and its max_error (:132),
-// for the VEC replicas of one lane.
-template <typename T, int VEC, int MODE>
-__device__ __forceinline__ void clause_update(const KArgs<T> &a, size_t ci, const T (&C)[VEC],
-                                              const Vec<T, VEC> &xs_m, const Vec<T, VEC> &xl_m,
-                                              const T (&h)[VEC], const bool (&on)[VEC], bool all_on,
-                                              T (&e)[VEC]) {
-    const T one = (T)1.0, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
-    Vec<T, VEC> o1, o2, o3, o4;
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-        const T dxs = (T)20.0 * (xs_m.e[k] + eps) * (C[k] - (T)0.25);  // :84
-        const T dxl = (T)5.0 * (C[k] - (T)0.05);                       // :85
-        const T half = (T)0.5 * h[k];
-        if (MODE == M_DERIV) {
-            o1.e[k] = dxs;
-            o2.e[k] = dxl;
-        } else if (MODE == M_FIXED) {
-            o1.e[k] = dmin(dmax(xs_m.e[k] + h[k] * dxs, eps), xs_hi);
-            o2.e[k] = dmin(dmax(xl_m.e[k] + h[k] * dxl, one), a.xl_max);
-        } else if (MODE == M_ADA) {
-            o1.e[k] = dmin(dmax(xs_m.e[k] + h[k] * dxs, eps), xs_hi);     // full-step clone
-            o2.e[k] = dmin(dmax(xl_m.e[k] + h[k] * dxl, one), a.xl_max);
-            o3.e[k] = dmin(dmax(xs_m.e[k] + half * dxs, eps), xs_hi);     // first half step
-            o4.e[k] = dmin(dmax(xl_m.e[k] + half * dxl, one), a.xl_max);
-        } else {
-            o1.e[k] = dmin(dmax(xs_m.e[k] + half * dxs, eps), xs_hi);     // second half step
-            o2.e[k] = dmin(dmax(xl_m.e[k] + half * dxl, one), a.xl_max);
-        }
-    }
-    if (MODE == M_DERIV) {
-        stv<T, VEC>(a.xsh + ci, o1);
-        stv<T, VEC>(a.xlh + ci, o2);
-    } else if (MODE == M_FIXED) {
-        stv_masked<T, VEC>(a.xs + ci, o1, on, all_on);
-        stv_masked<T, VEC>(a.xl + ci, o2, on, all_on);
-    } else if (MODE == M_ADA) {
-        stv<T, VEC>(a.xsf + ci, o1);
-        stv<T, VEC>(a.xlf + ci, o2);
-        stv<T, VEC>(a.xsh + ci, o3);
-        stv<T, VEC>(a.xlh + ci, o4);
-    } else {
-        const Vec<T, VEC> fs = ldv<T, VEC>(a.xsf + ci), fl = ldv<T, VEC>(a.xlf + ci);
-        stv_masked<T, VEC>(a.xs + ci, o1, on, all_on);
-        stv_masked<T, VEC>(a.xl + ci, o2, on, all_on);
-#pragma unroll
-        for (int k = 0; k < VEC; ++k)  // :101-108 max_error terms
-            e[k] = dmax(e[k], dmax(dabs(fs.e[k] - o1.e[k]), dabs(fl.e[k] - o2.e[k])));
-    }
-}
-
-// The per-replica prologue shared by both clause kernels and the variable kernel.
-template <typename T, int VEC, int MODE, bool CLAUSE>
-__device__ __forceinline__ bool lane_state(const KArgs<T> &a, int r0, bool (&on)[VEC], bool &all_on,
-                                           T (&h)[VEC]) {
-    bool any = false;
-    all_on = true;
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-        bool o = a.act[r0 + k] != 0;
-        // adaptive: a replica allsat at the first RHS takes no step (system.rs:122)
-        if (MODE == M_ADB || (!CLAUSE && MODE == M_ADA)) o = o && a.unsat[r0 + k] != 0;
-        on[k] = o;
-        any = any || o;
-        all_on = all_on && o;
-        h[k] = (MODE == M_ADA || MODE == M_ADB) ? a.dtr[r0 + k] : a.dt;
-    }
-    return __any(any);
-}
-
-// ------------------------------------------------------------------------------------------------
-// k_clause_u: system.rs:35-90 (+ :94-95) for formulas whose clauses all have K literals (random
-// k-SAT).  RB clauses per batch: their K*RB literal indices (scalar loads for LW = 64), K*RB voltage
-// rows and 2*RB memory rows are all issued before the first use.  Out-of-range clauses of the last
-// batch load clause m-1 and store nothing.
-// ------------------------------------------------------------------------------------------------
-template <typename T, int LW, int VEC, int MODE, int K>
-__global__ __launch_bounds__(256) void k_clause_u(KArgs<T> a) {
-    using G_ = Geo<LW, VEC>;
-    constexpr int W = G_::W, IPR = G_::IPR;
-    constexpr int RB = VEC >= 4 ? 2 : 4;
-    G_ geo;
-    if (!geo.init(a.tiles, a.g0, a.ng)) return;
-    if (*a.stop < a.step) return;  // ODESAT_STOP_ANY already triggered
-    bool on[VEC], all_on;
-    T h[VEC];
-    if (!lane_state<T, VEC, MODE, true>(a, geo.r0, on, all_on, h)) return;
-
-    const T *__restrict__ V = (MODE == M_ADB) ? a.vh : a.v;
-    const T *XS = (MODE == M_ADB) ? a.xsh : a.xs;
-    const T *XL = (MODE == M_ADB) ? a.xlh : a.xl;
-    const T one = (T)1.0, halfc = (T)0.5;
-    const size_t vbase = (size_t)geo.g * a.n * W + geo.off;
-    const size_t cbase = (size_t)geo.g * a.m * W + geo.off;
-    const size_t wbase = (size_t)geo.gl * a.L * W + geo.off;
-    bool uns[VEC];
-    T e[VEC];
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-        uns[k] = false;
-        e[k] = (T)0.0;
-    }
-
-    for (int row0 = 0; row0 < a.rows; row0 += RB) {
-        int cc[RB];
-        bool ok[RB];
-#pragma unroll
-        for (int b = 0; b < RB; ++b) {
-            int c = (geo.tile * a.rows + row0 + b) * IPR + geo.isub;
-            ok[b] = (row0 + b < a.rows) && (c < a.m);
-            c = ok[b] ? c : a.m - 1;
-            if (LW == 64) c = __builtin_amdgcn_readfirstlane(c);
-            cc[b] = c;
-        }
-        int lit[RB][K], pos[RB][K];
-#pragma unroll
-        for (int b = 0; b < RB; ++b)
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                lit[b][j] = ldc(a.lits, (size_t)cc[b] * K + j);
-                pos[b][j] = ldc(a.wpos, (size_t)cc[b] * K + j);
-            }
-        Vec<T, VEC> vv[RB][K], xs_m[RB], xl_m[RB];
-#pragma unroll
-        for (int b = 0; b < RB; ++b)
-#pragma unroll
-            for (int j = 0; j < K; ++j) vv[b][j] = ldv<T, VEC>(V + vbase + (size_t)(lit[b][j] >> 1) * W);
-#pragma unroll
-        for (int b = 0; b < RB; ++b) {
-            xs_m[b] = ldv<T, VEC>(XS + cbase + (size_t)cc[b] * W);
-            xl_m[b] = ldv<T, VEC>(XL + cbase + (size_t)cc[b] * W);
-        }
-#pragma unroll
-        for (int b = 0; b < RB; ++b) {
-            if (!ok[b]) continue;
-            T C[VEC], mn[VEC], sec[VEC], t[VEC], tr[VEC];
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                mn[k] = inf_v<T>();
-                sec[k] = inf_v<T>();
-#pragma unroll
-                for (int j = 0; j < K; ++j) {  // :43-57 strict-< min / second-min, literal order
-                    const T q = (lit[b][j] & 1) ? (T)-1.0 : (T)1.0;
-                    const T val = one - q * vv[b][j].e[k];
-                    const bool lt = val < mn[k];
-                    sec[k] = lt ? mn[k] : (val < sec[k] ? val : sec[k]);
-                    mn[k] = lt ? val : mn[k];
-                }
-                C[k] = halfc * mn[k];                                       // :60
-                t[k] = xl_m[b].e[k] * xs_m[b].e[k];                         // :80 xl_m * xs_m
-                tr[k] = (one + a.zeta * xl_m[b].e[k]) * (one - xs_m[b].e[k]);
-                if (MODE != M_ADB) uns[k] = uns[k] || (on[k] && !(C[k] < (T)0.25));  // :88
-            }
-#pragma unroll
-            for (int j = 0; j < K; ++j) {
-                const T q = (lit[b][j] & 1) ? (T)-1.0 : (T)1.0;
-                Vec<T, VEC> out;
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) {
-                    const T vi = vv[b][j].e[k];
-                    const T val = one - q * vi;
-                    const T g_ = halfc * q * (val != mn[k] ? mn[k] : sec[k]);        // :64-70
-                    const T r_ = (C[k] == one - q * vi) ? halfc * (q - vi) : (T)0.0;  // :73-77
-                    out.e[k] = t[k] * g_ + tr[k] * r_;                                // :80
-                }
-                stv<T, VEC>(a.w + wbase + (size_t)pos[b][j] * W, out);
-            }
-            clause_update<T, VEC, MODE>(a, cbase + (size_t)cc[b] * W, C, xs_m[b], xl_m[b], h, on, all_on, e);
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-        if (MODE != M_ADB) {
-            if (uns[k]) a.unsat[geo.r0 + k] = 1u;
-        } else if (on[k]) {
-            atomicMax(&a.err[geo.r0 + k], tobits(e[k]));
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// k_clause: the same for mixed clause widths (literal values re-gathered for the second pass)
-// ------------------------------------------------------------------------------------------------
-template <typename T, int LW, int VEC, int MODE>
-__global__ __launch_bounds__(256) void k_clause(KArgs<T> a) {
-    using G_ = Geo<LW, VEC>;
-    constexpr int W = G_::W, IPR = G_::IPR;
-    G_ geo;
-    if (!geo.init(a.tiles, a.g0, a.ng)) return;
-    if (*a.stop < a.step) return;
-    bool on[VEC], all_on;
-    T h[VEC];
-    if (!lane_state<T, VEC, MODE, true>(a, geo.r0, on, all_on, h)) return;
-
-    const T *__restrict__ V = (MODE == M_ADB) ? a.vh : a.v;
-    const T *XS = (MODE == M_ADB) ? a.xsh : a.xs;
-    const T *XL = (MODE == M_ADB) ? a.xlh : a.xl;
-    const T one = (T)1.0, halfc = (T)0.5;
-    const size_t vbase = (size_t)geo.g * a.n * W + geo.off;
-    const size_t cbase = (size_t)geo.g * a.m * W + geo.off;
-    const size_t wbase = (size_t)geo.gl * a.L * W + geo.off;
-    bool uns[VEC];
-    T e[VEC];
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-        uns[k] = false;
-        e[k] = (T)0.0;
-    }
-    for (int row = 0; row < a.rows; ++row) {
-        int c = (geo.tile * a.rows + row) * IPR + geo.isub;
-        if (LW == 64) c = __builtin_amdgcn_readfirstlane(c);
-        if (c >= a.m) break;
-        const int s0 = ldc(a.cptr, c), s1 = ldc(a.cptr, c + 1);
-        const size_t ci = cbase + (size_t)c * W;
-        const Vec<T, VEC> xs_m = ldv<T, VEC>(XS + ci), xl_m = ldv<T, VEC>(XL + ci);
-        T mn[VEC], sec[VEC], C[VEC], t[VEC], tr[VEC];
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            mn[k] = inf_v<T>();
-            sec[k] = inf_v<T>();
-        }
-        for (int s = s0; s < s1; ++s) {  // :43-57
-            const int lit = ldc(a.lits, s);
-            const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
-            const Vec<T, VEC> vv = ldv<T, VEC>(V + vbase + (size_t)(lit >> 1) * W);
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                const T val = one - q * vv.e[k];
-                const bool lt = val < mn[k];
-                sec[k] = lt ? mn[k] : (val < sec[k] ? val : sec[k]);
-                mn[k] = lt ? val : mn[k];
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            C[k] = halfc * mn[k];
-            t[k] = xl_m.e[k] * xs_m.e[k];
-            tr[k] = (one + a.zeta * xl_m.e[k]) * (one - xs_m.e[k]);
-            if (MODE != M_ADB) uns[k] = uns[k] || (on[k] && !(C[k] < (T)0.25));
-        }
-        for (int s = s0; s < s1; ++s) {  // :62-81
-            const int lit = ldc(a.lits, s);
-            const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
-            const Vec<T, VEC> vv = ldv<T, VEC>(V + vbase + (size_t)(lit >> 1) * W);
-            Vec<T, VEC> out;
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                const T vi = vv.e[k];
-                const T val = one - q * vi;
-                const T g_ = halfc * q * (val != mn[k] ? mn[k] : sec[k]);
-                const T r_ = (C[k] == one - q * vi) ? halfc * (q - vi) : (T)0.0;
-                out.e[k] = t[k] * g_ + tr[k] * r_;
-            }
-            stv<T, VEC>(a.w + wbase + (size_t)ldc(a.wpos, s) * W, out);
-        }
-        clause_update<T, VEC, MODE>(a, ci, C, xs_m, xl_m, h, on, all_on, e);
-    }
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-        if (MODE != M_ADB) {
-            if (uns[k]) a.unsat[geo.r0 + k] = 1u;
-        } else if (on[k]) {
-            atomicMax(&a.err[geo.r0 + k], tobits(e[k]));
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// k_variable: system.rs:33,80 (dv in the reference's accumulation order) + :96
-// ------------------------------------------------------------------------------------------------
-template <typename T, int LW, int VEC, int MODE>
-__global__ __launch_bounds__(256) void k_variable(KArgs<T> a) {
-    using G_ = Geo<LW, VEC>;
-    constexpr int W = G_::W, IPR = G_::IPR;
-    G_ geo;
-    if (!geo.init(a.tiles, a.g0, a.ng)) return;
-    if (*a.stop < a.step) return;
-    bool on[VEC], all_on;
-    T h[VEC];
-    if (!lane_state<T, VEC, MODE, false>(a, geo.r0, on, all_on, h)) return;
-    const size_t vbase = (size_t)geo.g * a.n * W + geo.off;
-    const T *__restrict__ wsrc = a.w + (size_t)geo.gl * a.L * W + geo.off;
-    T e[VEC];
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) e[k] = (T)0.0;
-    for (int row = 0; row < a.rows; ++row) {
-        int i = (geo.tile * a.rows + row) * IPR + geo.isub;
-        if (LW == 64) i = __builtin_amdgcn_readfirstlane(i);
-        if (i >= a.n) break;
-        const int p0 = ldc(a.vptr, i), p1 = ldc(a.vptr, i + 1);
-        const size_t vi = vbase + (size_t)i * W;
-        const Vec<T, VEC> v0 = ldv<T, VEC>(((MODE == M_ADB) ? a.vh : a.v) + vi);  // issued early
-        T dv[VEC];
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) dv[k] = (T)0.0;  // :33
-        int p = p0;
-        for (; p + 4 <= p1; p += 4) {  // four rows in flight, sequential adds (order kept)
-            const Vec<T, VEC> w0 = ldv<T, VEC>(wsrc + (size_t)p * W);
-            const Vec<T, VEC> w1 = ldv<T, VEC>(wsrc + (size_t)(p + 1) * W);
-            const Vec<T, VEC> w2 = ldv<T, VEC>(wsrc + (size_t)(p + 2) * W);
-            const Vec<T, VEC> w3 = ldv<T, VEC>(wsrc + (size_t)(p + 3) * W);
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                dv[k] += w0.e[k];
-                dv[k] += w1.e[k];
-                dv[k] += w2.e[k];
-                dv[k] += w3.e[k];
-            }
-        }
-        for (; p < p1; ++p) {
-            const Vec<T, VEC> w0 = ldv<T, VEC>(wsrc + (size_t)p * W);
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) dv[k] += w0.e[k];
-        }
-        Vec<T, VEC> o1, o2;
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            if (MODE == M_DERIV) {
-                o1.e[k] = dv[k];
-            } else if (MODE == M_FIXED) {
-                o1.e[k] = dmin(dmax(v0.e[k] + h[k] * dv[k], (T)-1.0), (T)1.0);
-            } else if (MODE == M_ADA) {
-                const T half = (T)0.5 * h[k];
-                o1.e[k] = dmin(dmax(v0.e[k] + h[k] * dv[k], (T)-1.0), (T)1.0);   // full-step clone
-                o2.e[k] = dmin(dmax(v0.e[k] + half * dv[k], (T)-1.0), (T)1.0);  // first half step
-            } else {
-                const T half = (T)0.5 * h[k];
-                o1.e[k] = dmin(dmax(v0.e[k] + half * dv[k], (T)-1.0), (T)1.0);  // second half step
-            }
-        }
-        if (MODE == M_DERIV) {
-            stv<T, VEC>(a.vh + vi, o1);
-        } else if (MODE == M_FIXED) {
-            stv_masked<T, VEC>(a.v + vi, o1, on, all_on);
-        } else if (MODE == M_ADA) {
-            stv<T, VEC>(a.vf + vi, o1);
-            stv<T, VEC>(a.vh + vi, o2);
-        } else {
-            const Vec<T, VEC> f = ldv<T, VEC>(a.vf + vi);
-            stv_masked<T, VEC>(a.v + vi, o1, on, all_on);
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) e[k] = dmax(e[k], dabs(f.e[k] - o1.e[k]));
-        }
-    }
-    if (MODE == M_ADB) {
-#pragma unroll
-        for (int k = 0; k < VEC; ++k)
-            if (on[k]) atomicMax(&a.err[geo.r0 + k], tobits(e[k]));
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// k_status: per-replica bookkeeping after all kernels of one step of a replica range
-// ------------------------------------------------------------------------------------------------
-struct StatusArgs {
-    uint8_t *act;
-    uint32_t *unsat;
-    void *err;
-    void *dtr;
-    int64_t *sat_step;
-    int64_t *steps_done;
-    int32_t *stop;
-    int32_t r0, r1, step, stop_mode, adaptive;
-    double tol;
-};
-
-template <typename T> __global__ void k_status(StatusArgs s) {
-    const int r = s.r0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= s.r1) return;
-    if (*s.stop < s.step) return;  // this step did not run
-    auto *err = (typename Bits<T>::U *)s.err;
-    T *dtr = (T *)s.dtr;
-    if (s.act[r]) {
-        const bool allsat = s.unsat[r] == 0u;
-        s.steps_done[r] += 1;
-        if (allsat) {
-            if (s.sat_step[r] < 0) s.sat_step[r] = s.step;
-            if (s.stop_mode == ODESAT_STOP_EACH) s.act[r] = 0;             // simulate() breaks (:193)
-            if (s.stop_mode == ODESAT_STOP_ANY) atomicMin(s.stop, s.step);  // simulate_inter (:291)
-        } else if (s.adaptive) {  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
-            const T error = frombits(err[r]);
-            const T h = dtr[r];
-            dtr[r] = dmax(dmin(h * dsqrt((T)s.tol / error), (T)1e3), (T)0.0078125);
-        }
-    }
-    s.unsat[r] = 0u;
-    if (s.adaptive) err[r] = 0;
-}
-
-// ------------------------------------------------------------------------------------------------
-// init / layout kernels (not on the hot path: group width W is a runtime argument)
-// ------------------------------------------------------------------------------------------------
-template <typename T>
-__global__ void k_init(T *v, T *xs, T *xl, const int32_t *cptr, const int32_t *lits, int n, int m, int G,
-                       int W, int B, uint64_t seed, int64_t replica0) {
-    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t nv = (size_t)G * n * W, nc = (size_t)G * m * W;
-    if (tid < nv) {
-        const int lane = (int)(tid % W);
-        const size_t gi = tid / W;
-        const int i = (int)(gi % n);
-        const int g = (int)(gi / n);
-        const int r = g * W + lane;
-        v[tid] = r < B ? (T)init_voltage(seed, (uint64_t)(replica0 + r), (uint64_t)i) : (T)0.0;
-    }
-    if (tid < nc) {
-        const size_t gi = tid / W;
-        const int c = (int)(gi % m);
-        bool anyneg = false;  // system.rs:361-372
-        for (int s = cptr[c]; s < cptr[c + 1]; ++s) anyneg |= (lits[s] & 1) != 0;
-        xs[tid] = anyneg ? (T)1.0 : (T)-1.0;
-        xl[tid] = (T)1.0;
-    }
-}
-
-// compact [count][items] f64 <-> layout [G][items][W] in dtype T
-template <typename T>
-__global__ void k_scatter(T *dst, const double *src, int items, int W, int64_t r0, int64_t count) {
-    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid >= (size_t)count * items) return;
-    const int64_t b = (int64_t)(tid / items);
-    const int i = (int)(tid % items);
-    const int64_t r = r0 + b;
-    dst[((size_t)(r / W) * items + i) * W + (r % W)] = (T)src[tid];
-}
-
-template <typename T>
-__global__ void k_gather(double *dst, const T *src, int items, int W, int64_t r0, int64_t count) {
-    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (tid >= (size_t)count * items) return;
-    const int64_t b = (int64_t)(tid / items);
-    const int i = (int)(tid % items);
-    const int64_t r = r0 + b;
-    dst[tid] = (double)src[((size_t)(r / W) * items + i) * W + (r % W)];
-}
-
-__global__ void k_reset_replicas(uint8_t *act, uint32_t *unsat, int64_t *sat_step, int64_t *steps_done,
-                                 void *dtr, int dtype, int64_t r0, int64_t count, int64_t B, int64_t Bp) {
-    const int64_t r = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= r0 + count || r >= Bp) return;
-    act[r] = r < B ? 1 : 0;
-    unsat[r] = 0;
-    sat_step[r] = -1;
-    steps_done[r] = 0;
-    if (dtype == ODESAT_F64) ((double *)dtr)[r] = 0.01;
-    else ((float *)dtr)[r] = 0.01f;
-}
-
-}  // namespace
-
-// ================================================================================================
-// host side
-// ================================================================================================
 struct odesat_solver {
     int device = 0, dtype = ODESAT_F32;
     int64_t n = 0, m = 0, L = 0, B = 0, Bp = 0;
@@ -623,11 +36,19 @@ struct odesat_solver {
     int chunk_groups = 1;
     int uniform_k = 0;  // every clause has this many literals (0 = mixed widths)
     int schedule = ODESAT_SCHED_AUTO;
+    int alg = ODESAT_ALG_FUSED;
+    int rb = 4;  // 3-SAT incidences per batch in k_step (ODESAT_RB: 4 or 8)
     size_t tsize = 4;
     hipStream_t stream = nullptr;
-    int32_t *cptr = nullptr, *lits = nullptr, *wpos = nullptr, *vptr = nullptr;
-    void *v = nullptr, *xs = nullptr, *xl = nullptr, *w = nullptr;
-    void *vh = nullptr, *vf = nullptr, *xsh = nullptr, *xlh = nullptr, *xsf = nullptr, *xlf = nullptr;
+    int32_t *cptr = nullptr, *lits = nullptr, *wpos = nullptr, *vptr = nullptr, *pc = nullptr, *ps = nullptr;
+    int32_t *empty = nullptr;  // clauses without literals (FUSED handles them separately)
+    Inc *inc = nullptr;        // 3-SAT incidence records, variable-major
+    int n_empty = 0;
+    void *v[2] = {nullptr, nullptr};   // voltages [G][n][W]
+    void *c[2] = {nullptr, nullptr};   // clause memories [G][m][W][2] (xs, xl)
+    uint8_t *par = nullptr;  // [G]
+    void *w = nullptr;
+    void *vh = nullptr, *vf = nullptr, *ch = nullptr, *cf = nullptr;
     void *dtr = nullptr, *err = nullptr;
     uint32_t *unsat = nullptr;
     uint8_t *act = nullptr;
@@ -689,15 +110,13 @@ int ensure_scratch(odesat_solver *s) {
     int rc;
     if ((rc = dmalloc(s, &s->vh, state_elems(s, s->n) * s->tsize))) return rc;
     if ((rc = dmalloc(s, &s->vf, state_elems(s, s->n) * s->tsize))) return rc;
-    if ((rc = dmalloc(s, &s->xsh, state_elems(s, s->m) * s->tsize))) return rc;
-    if ((rc = dmalloc(s, &s->xlh, state_elems(s, s->m) * s->tsize))) return rc;
-    if ((rc = dmalloc(s, &s->xsf, state_elems(s, s->m) * s->tsize))) return rc;
-    if ((rc = dmalloc(s, &s->xlf, state_elems(s, s->m) * s->tsize))) return rc;
+    if ((rc = dmalloc(s, &s->ch, 2 * state_elems(s, s->m) * s->tsize))) return rc;
+    if ((rc = dmalloc(s, &s->cf, 2 * state_elems(s, s->m) * s->tsize))) return rc;
     return ODESAT_OK;
 }
 
 int ensure_w(odesat_solver *s) {
-    if (s->w) return ODESAT_OK;
+    if (s->alg != ODESAT_ALG_TWOPASS || s->w) return ODESAT_OK;
     return dmalloc(s, &s->w, (size_t)s->chunk_groups * s->L * s->W * s->tsize);
 }
 
@@ -741,16 +160,19 @@ template <typename T> KArgs<T> make_args(odesat_solver *s) {
     a.lits = s->lits;
     a.wpos = s->wpos;
     a.vptr = s->vptr;
-    a.v = (T *)s->v;
-    a.xs = (T *)s->xs;
-    a.xl = (T *)s->xl;
+    a.pc = s->pc;
+    a.ps = s->ps;
+    a.inc = s->inc;
+    a.v0 = (T *)s->v[0];
+    a.v1 = (T *)s->v[1];
+    a.c0 = (T *)s->c[0];
+    a.c1 = (T *)s->c[1];
+    a.par = s->par;
     a.w = (T *)s->w;
     a.vh = (T *)s->vh;
     a.vf = (T *)s->vf;
-    a.xsh = (T *)s->xsh;
-    a.xlh = (T *)s->xlh;
-    a.xsf = (T *)s->xsf;
-    a.xlf = (T *)s->xlf;
+    a.ch = (T *)s->ch;
+    a.cf = (T *)s->cf;
     a.dtr = (T *)s->dtr;
     a.err = (typename Bits<T>::U *)s->err;
     a.unsat = s->unsat;
@@ -782,43 +204,84 @@ struct Timed {  // brackets one launch with profiling events
     }
 };
 
-template <typename T, int LW, int VEC, int MODE>
-int launch_kernel(odesat_solver *s, KArgs<T> a, bool clause) {
-    const int64_t items = clause ? s->m : s->n;
+enum Kern { K_STEP = 0, K_CLAUSE = 1, K_VARIABLE = 2 };
+
+// Grid geometry: rows per wave, waves per group, block placement (XCD-aware when the group count
+// and the 8 XCDs divide one another).
+template <typename T> unsigned geometry(const odesat_solver *s, KArgs<T> &a, int64_t items, int LW) {
     a.rows = pick_rows(items, a.ng, LW);
     const int64_t ipr = 64 / LW;
     a.tiles = (int)((items + ipr * a.rows - 1) / (ipr * a.rows));
-    if (a.tiles == 0) return ODESAT_OK;
-    const int64_t waves = (int64_t)a.tiles * a.ng;
-    const int64_t blocks = (waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-    if (blocks > INT_MAX) return fail(ODESAT_EINVAL, "grid too large");
-    const dim3 grid((unsigned)blocks), block(64 * WAVES_PER_BLOCK);
+    a.bpg = (a.tiles + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    int64_t blocks;
+    if (a.ng >= 8 && a.ng % 8 == 0) {
+        a.xmode = 1;
+        blocks = (int64_t)a.ng * a.bpg;
+    } else if (a.ng < 8 && 8 % a.ng == 0 && a.bpg >= 8 / a.ng) {
+        a.xmode = 2;
+        const int sh = 8 / a.ng;
+        blocks = 8ll * ((a.bpg + sh - 1) / sh);
+    } else {
+        a.xmode = 0;
+        blocks = (int64_t)a.ng * a.bpg;
+    }
+    (void)s;
+    return a.tiles == 0 ? 0u : (unsigned)std::min<int64_t>(blocks, INT_MAX);
+}
+
+template <typename T, int LW, int VEC, int MODE>
+int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which) {
+    const int64_t items = which == K_CLAUSE ? s->m : s->n;
+    const unsigned blocks = geometry<T>(s, a, items, LW);
+    if (blocks == 0) return ODESAT_OK;
+    const dim3 grid(blocks), block(64 * WAVES_PER_BLOCK);
     {
-        Timed tm(s, clause ? 0 : 1);
-        if (clause && s->uniform_k == 3)
-            hipLaunchKernelGGL((k_clause_u<T, LW, VEC, MODE, 3>), grid, block, 0, s->stream, a);
-        else if (clause)
-            hipLaunchKernelGGL((k_clause<T, LW, VEC, MODE>), grid, block, 0, s->stream, a);
-        else
+        Timed tm(s, which == K_VARIABLE ? 1 : 0);
+        if (which == K_STEP) {
+            if (s->uniform_k == 3 && s->rb == 8)
+                hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 3, 8>), grid, block, 0, s->stream, a);
+            else if (s->uniform_k == 3)
+                hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 3, 4>), grid, block, 0, s->stream, a);
+            else
+                hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 0>), grid, block, 0, s->stream, a);
+        } else if (which == K_CLAUSE) {
+            if (s->uniform_k == 3)
+                hipLaunchKernelGGL((k_clause_u<T, LW, VEC, MODE, 3>), grid, block, 0, s->stream, a);
+            else
+                hipLaunchKernelGGL((k_clause<T, LW, VEC, MODE>), grid, block, 0, s->stream, a);
+        } else {
             hipLaunchKernelGGL((k_variable<T, LW, VEC, MODE>), grid, block, 0, s->stream, a);
+        }
     }
     HIP_TRY(hipGetLastError());
+    if (which == K_STEP && s->n_empty > 0) {  // clauses with no literal (no owning variable)
+        const int64_t threads = (int64_t)a.ng * s->n_empty * LW;
+        const int64_t nb = (threads + 255) / 256;
+        hipLaunchKernelGGL((k_empty_clauses<T, LW, VEC, MODE>), dim3((unsigned)nb), dim3(256), 0, s->stream, a,
+                           (const int32_t *)s->empty, s->n_empty);
+        HIP_TRY(hipGetLastError());
+    }
     return ODESAT_OK;
 }
 
-// One RHS(+update) of `MODE` for the groups [gA, gB): k_clause then k_variable per chunk.
+// One RHS(+update) of `MODE` for the groups [gA, gB).
 template <typename T, int LW, int VEC, int MODE>
-int step_chunks(odesat_solver *s, int step, T dt, T zeta, int gA, int gB) {
+int step_groups(odesat_solver *s, int step, T dt, T zeta, int gA, int gB) {
     KArgs<T> a = make_args<T>(s);
     a.step = step;
     a.dt = dt;
     a.zeta = zeta;
     int rc;
-    for (int g0 = gA; g0 < gB; g0 += s->chunk_groups) {
+    if (s->alg == ODESAT_ALG_FUSED) {
+        a.g0 = gA;
+        a.ng = gB - gA;
+        return launch_kernel<T, LW, VEC, MODE>(s, a, K_STEP);
+    }
+    for (int g0 = gA; g0 < gB; g0 += s->chunk_groups) {  // TWOPASS: one contribution buffer per chunk
         a.g0 = g0;
         a.ng = std::min(s->chunk_groups, gB - g0);
-        if ((rc = launch_kernel<T, LW, VEC, MODE>(s, a, true))) return rc;
-        if ((rc = launch_kernel<T, LW, VEC, MODE>(s, a, false))) return rc;
+        if ((rc = launch_kernel<T, LW, VEC, MODE>(s, a, K_CLAUSE))) return rc;
+        if ((rc = launch_kernel<T, LW, VEC, MODE>(s, a, K_VARIABLE))) return rc;
     }
     return ODESAT_OK;
 }
@@ -835,8 +298,10 @@ int launch_status(odesat_solver *s, int step, int stop_mode, bool adaptive, doub
     sa.sat_step = s->sat_step;
     sa.steps_done = s->steps_done;
     sa.stop = s->stop;
+    sa.par = s->par;
     sa.r0 = (int32_t)r0;
     sa.r1 = (int32_t)r1;
+    sa.W = s->W;
     sa.step = step;
     sa.stop_mode = stop_mode;
     sa.adaptive = adaptive ? 1 : 0;
@@ -858,12 +323,12 @@ int enqueue_step(odesat_solver *s, int step, bool adaptive, double dt, double ze
     int rc = with_layout<T>(s, [&](auto lw, auto vec) -> int {
         constexpr int LW = decltype(lw)::value, VEC = decltype(vec)::value;
         int r;
-        if (!adaptive) return step_chunks<T, LW, VEC, M_FIXED>(s, step, (T)dt, (T)zeta, gA, gB);
-        // the two half steps of one chunk run back to back (one contribution buffer per chunk)
-        for (int g0 = gA; g0 < gB; g0 += s->chunk_groups) {
-            const int g1 = std::min(gB, g0 + s->chunk_groups);
-            if ((r = step_chunks<T, LW, VEC, M_ADA>(s, step, (T)dt, (T)zeta, g0, g1))) return r;
-            if ((r = step_chunks<T, LW, VEC, M_ADB>(s, step, (T)dt, (T)zeta, g0, g1))) return r;
+        if (!adaptive) return step_groups<T, LW, VEC, M_FIXED>(s, step, (T)dt, (T)zeta, gA, gB);
+        const int span = s->alg == ODESAT_ALG_TWOPASS ? s->chunk_groups : gB - gA;
+        for (int g0 = gA; g0 < gB; g0 += span) {  // both half steps of one contribution-buffer chunk
+            const int g1 = std::min(gB, g0 + span);
+            if ((r = step_groups<T, LW, VEC, M_ADA>(s, step, (T)dt, (T)zeta, g0, g1))) return r;
+            if ((r = step_groups<T, LW, VEC, M_ADB>(s, step, (T)dt, (T)zeta, g0, g1))) return r;
         }
         return ODESAT_OK;
     });
@@ -880,41 +345,46 @@ int dispatch_step(odesat_solver *s, int step, bool adaptive, double dt, double z
 template <typename T> int deriv_t(odesat_solver *s, double zeta) {
     return with_layout<T>(s, [&](auto lw, auto vec) -> int {
         constexpr int LW = decltype(lw)::value, VEC = decltype(vec)::value;
-        return step_chunks<T, LW, VEC, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
+        return step_groups<T, LW, VEC, M_DERIV>(s, 0, (T)0, (T)zeta, 0, s->G);
     });
 }
 
+// compact host-side f64 [count][items] <-> device layout of a buffer pair (par-selected) or a
+// single buffer (pair[1] == nullptr)
 template <typename T>
-int layout_t(odesat_solver *s, void *dev, const double *dsrc, double *ddst, int64_t items, int64_t r0,
-             int64_t count, bool scatter) {
+int layout_t(odesat_solver *s, void *const pair[2], const double *dsrc, double *ddst, int64_t items, int stride,
+             int comp, int64_t r0, int64_t count, bool scatter) {
     const size_t total = (size_t)count * items;
     if (!total) return ODESAT_OK;
     const int threads = 256;
     const size_t blocks = (total + threads - 1) / threads;
+    const uint8_t *par = pair[1] ? s->par : nullptr;
+    T *b1 = pair[1] ? (T *)pair[1] : (T *)pair[0];
     if (scatter)
-        hipLaunchKernelGGL((k_scatter<T>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, (T *)dev, dsrc,
-                           (int)items, s->W, r0, count);
+        hipLaunchKernelGGL((k_scatter<T>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, (T *)pair[0], b1, par,
+                           dsrc, (int)items, s->W, stride, comp, r0, count);
     else
         hipLaunchKernelGGL((k_gather<T>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, ddst,
-                           (const T *)dev, (int)items, s->W, r0, count);
+                           (const T *)pair[0], (const T *)b1, par, (int)items, s->W, stride, comp, r0, count);
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
 }
 
-int layout(odesat_solver *s, void *dev, const double *dsrc, double *ddst, int64_t items, int64_t r0,
-           int64_t count, bool scatter) {
-    return s->dtype == ODESAT_F64 ? layout_t<double>(s, dev, dsrc, ddst, items, r0, count, scatter)
-                                  : layout_t<float>(s, dev, dsrc, ddst, items, r0, count, scatter);
+int layout(odesat_solver *s, void *const pair[2], const double *dsrc, double *ddst, int64_t items, int stride,
+           int comp, int64_t r0, int64_t count, bool scatter) {
+    return s->dtype == ODESAT_F64 ? layout_t<double>(s, pair, dsrc, ddst, items, stride, comp, r0, count, scatter)
+                                  : layout_t<float>(s, pair, dsrc, ddst, items, stride, comp, r0, count, scatter);
 }
 
-// host f64 [count][items] <-> device layout, through a device staging buffer
-int upload_items(odesat_solver *s, void *dev, const double *host, int64_t items, int64_t r0, int64_t count) {
+// stride 1: a voltage array; stride 2, comp 0 / 1: the xs / xl half of a clause-memory array
+int upload_items(odesat_solver *s, void *const pair[2], const double *host, int64_t items, int stride, int comp,
+                 int64_t r0, int64_t count) {
     if (!host || !items || !count) return ODESAT_OK;
     void *stage = nullptr;
     const size_t bytes = (size_t)count * items * sizeof(double);
     HIP_TRY(hipMalloc(&stage, bytes));
     hipError_t e = hipMemcpyAsync(stage, host, bytes, hipMemcpyHostToDevice, s->stream);
-    int rc = e == hipSuccess ? layout(s, dev, (const double *)stage, nullptr, items, r0, count, true)
+    int rc = e == hipSuccess ? layout(s, pair, (const double *)stage, nullptr, items, stride, comp, r0, count, true)
                              : fail(ODESAT_EDEVICE, hipGetErrorString(e));
     hipError_t e2 = hipStreamSynchronize(s->stream);
     (void)hipFree(stage);
@@ -923,12 +393,13 @@ int upload_items(odesat_solver *s, void *dev, const double *host, int64_t items,
     return ODESAT_OK;
 }
 
-int download_items(odesat_solver *s, const void *dev, double *host, int64_t items, int64_t r0, int64_t count) {
+int download_items(odesat_solver *s, void *const pair[2], double *host, int64_t items, int stride, int comp,
+                   int64_t r0, int64_t count) {
     if (!host || !items || !count) return ODESAT_OK;
     void *stage = nullptr;
     const size_t bytes = (size_t)count * items * sizeof(double);
     HIP_TRY(hipMalloc(&stage, bytes));
-    int rc = layout(s, const_cast<void *>(dev), nullptr, (double *)stage, items, r0, count, false);
+    int rc = layout(s, pair, nullptr, (double *)stage, items, stride, comp, r0, count, false);
     hipError_t e = rc ? hipSuccess : hipMemcpyAsync(host, stage, bytes, hipMemcpyDeviceToHost, s->stream);
     hipError_t e2 = hipStreamSynchronize(s->stream);
     (void)hipFree(stage);
@@ -960,19 +431,24 @@ int check_solver(odesat_solver *s) {
     return ODESAT_OK;
 }
 
-template <typename T> int init_t(odesat_solver *s, uint64_t seed, int64_t replica0) {
+// v = counter RNG (or 0), xs = init_short_term_memory, xl = 1 into buffer 0; every group's
+// current buffer becomes 0
+template <typename T> int init_t(odesat_solver *s, uint64_t seed, int64_t replica0, bool zero_v) {
     const size_t total = std::max(state_elems(s, s->n), state_elems(s, s->m));
     if (!total) return ODESAT_OK;
     const int threads = 256;
     const size_t blocks = (total + threads - 1) / threads;
-    hipLaunchKernelGGL((k_init<T>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, (T *)s->v, (T *)s->xs,
-                       (T *)s->xl, s->cptr, s->lits, (int)s->n, (int)s->m, s->G, s->W, (int)s->B, seed, replica0);
+    hipLaunchKernelGGL((k_init<T>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, (T *)s->v[0],
+                       (T *)s->c[0], s->cptr, s->lits, (int)s->n, (int)s->m, s->G, s->W, (int)s->B, seed, replica0,
+                       zero_v ? 1 : 0);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemsetAsync(s->par, 0, s->G, s->stream));
     return ODESAT_OK;
 }
 
-int init_dispatch(odesat_solver *s, uint64_t seed, int64_t replica0) {
-    return s->dtype == ODESAT_F64 ? init_t<double>(s, seed, replica0) : init_t<float>(s, seed, replica0);
+int init_dispatch(odesat_solver *s, uint64_t seed, int64_t replica0, bool zero_v) {
+    return s->dtype == ODESAT_F64 ? init_t<double>(s, seed, replica0, zero_v)
+                                  : init_t<float>(s, seed, replica0, zero_v);
 }
 
 double default_zeta(const odesat_solver *s) {  // system.rs:164-173
@@ -981,13 +457,12 @@ double default_zeta(const odesat_solver *s) {  // system.rs:164-173
 }
 
 void pick_chunk(odesat_solver *s, int64_t replicas) {
-    // one chunk = state + contribution buffer of chunk_groups groups
+    // TWOPASS: one chunk's state + contribution buffer stays inside the 256 MiB Infinity Cache
     const int64_t per_group = (s->n + 2 * s->m + s->L) * s->W * (int64_t)s->tsize;
     int64_t groups;
     if (replicas > 0) {
         groups = std::max<int64_t>(1, replicas / s->W);
     } else {
-        // keep one chunk's working set well inside the 256 MiB Infinity Cache
         const int64_t budget = 120ll << 20;
         groups = std::max<int64_t>(1, budget / std::max<int64_t>(per_group, 1));
     }
@@ -1032,7 +507,7 @@ int set_all_active(odesat_solver *s) {
 // ================================================================================================
 // C ABI
 // ================================================================================================
-extern "C" const char *odesat_version(void) { return "odesat_amd 0.2 (gfx950)"; }
+extern "C" const char *odesat_version(void) { return "odesat_amd 0.3 (gfx950)"; }
 
 extern "C" int odesat_device_count(int *count) {
     if (!count) return fail(ODESAT_EINVAL, "null count");
@@ -1051,9 +526,9 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
         (void)hipEventDestroy(p.b);
     }
     for (auto e : s->pool) (void)hipEventDestroy(e);
-    void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->v, s->xs, s->xl, s->w, s->vh, s->vf,
-                    s->xsh, s->xlh, s->xsf, s->xlf, s->dtr, s->err, s->unsat, s->act, s->sat_step,
-                    s->steps_done, s->stop};
+    void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->pc, s->ps, s->empty, s->inc, s->v[0], s->v[1], s->c[0],
+                    s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
+                    s->sat_step, s->steps_done, s->stop};
     for (void *p : ptrs) dfree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
@@ -1068,7 +543,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     if (dtype != ODESAT_F32 && dtype != ODESAT_F64) return fail(ODESAT_EINVAL, "dtype must be ODESAT_F32 or ODESAT_F64");
     const int64_t n = f->varnum, m = f->nclauses(), L = f->nliterals();
     if (n <= 0) return fail(ODESAT_EINVAL, "varnum must be > 0");
-    if (n >= (1ll << 30) || m >= INT_MAX / 4 || L >= INT_MAX || batch >= INT_MAX / 2)
+    if (n >= (1ll << 29) || m >= INT_MAX / 4 || L >= INT_MAX || batch >= INT_MAX / 2)
         return fail(ODESAT_EINVAL, "formula or batch too large");
     for (int64_t s = 0; s < L; ++s)
         if (f->var[s] < 0 || f->var[s] >= n)
@@ -1094,20 +569,20 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     s->m = m;
     s->L = L;
     s->B = batch;
-    // layout: 16-byte lanes once a batch fills 64 lanes of 16 B
-    const int vmax = 16 / (int)s->tsize;
-    if (batch >= 64 * vmax) {
-        s->LW = 64;
-        s->VEC = vmax;
-    } else if (batch >= 128 && vmax >= 2) {
-        s->LW = 64;
-        s->VEC = 2;
-    } else {
-        int lw = 1;
-        while (lw < batch && lw < 64) lw <<= 1;
-        s->LW = lw;
-        s->VEC = 1;
+    // layout: W = min(next pow2 >= batch, 64) replicas per group, one lane per
+    // replica, 64/W items per wave.  Measured on MI355X (config 2, B = 1024): W = 64 beats 32 / 16
+    // by 1.5-1.7x although a smaller group's voltage table would fit an XCD's L2 better -- the
+    // narrower rows cost more in instructions than they save in bytes.  ODESAT_GROUP_WIDTH
+    // overrides (tuning).
+    int lw = 1;
+    while (lw < batch && lw < 64) lw <<= 1;
+    if (const char *ev = std::getenv("ODESAT_GROUP_WIDTH")) {
+        const int want = std::atoi(ev);
+        if (want == 1 || want == 2 || want == 4 || want == 8 || want == 16 || want == 32 || want == 64) lw = want;
     }
+    s->LW = lw;
+    s->VEC = 1;
+    if (const char *ev = std::getenv("ODESAT_RB")) s->rb = std::atoi(ev) == 8 ? 8 : 4;
     s->W = s->LW * s->VEC;
     s->Bp = (batch + s->W - 1) / s->W * s->W;
     s->G = (int)(s->Bp / s->W);
@@ -1115,7 +590,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     s->uniform_k = m > 0 ? (int)(f->clause_ptr[1] - f->clause_ptr[0]) : 0;
     for (int64_t c = 0; c < m && s->uniform_k; ++c)
         if (f->clause_ptr[c + 1] - f->clause_ptr[c] != s->uniform_k) s->uniform_k = 0;
-    if (s->uniform_k != 3) s->uniform_k = 0;  // the specialised kernel is instantiated for 3-SAT
+    if (s->uniform_k != 3) s->uniform_k = 0;  // the specialised kernels are instantiated for 3-SAT
     int rc = ODESAT_OK;
     auto bail = [&](int code) {
         odesat_solver_destroy(s);
@@ -1124,8 +599,9 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "hipStreamCreate failed"));
 
-    // topology: clause CSR, packed literals, variable-major slot positions
-    std::vector<int32_t> cptr(m + 1), lits(L), wpos(L), vptr(n + 1, 0);
+    // topology: clause CSR, packed literals, variable-major slot positions (sorted by slot, i.e.
+    // clause order then literal order: the reference's accumulation order) and their inverse
+    std::vector<int32_t> cptr(m + 1), lits(L), wpos(L), vptr(n + 1, 0), pc(L), ps(L), empty;
     for (int64_t c = 0; c <= m; ++c) cptr[c] = (int32_t)f->clause_ptr[c];
     for (int64_t s2 = 0; s2 < L; ++s2) {
         lits[s2] = (int32_t)((f->var[s2] << 1) | (f->neg[s2] ? 1 : 0));
@@ -1134,21 +610,48 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     for (int64_t i = 0; i < n; ++i) vptr[i + 1] += vptr[i];
     {
         std::vector<int32_t> fill(vptr.begin(), vptr.end() - 1);
-        for (int64_t s2 = 0; s2 < L; ++s2) wpos[s2] = fill[f->var[s2]]++;  // slot order = clause order
+        for (int64_t c = 0; c < m; ++c) {
+            if (cptr[c] == cptr[c + 1]) empty.push_back((int32_t)c);
+            for (int32_t s2 = cptr[c]; s2 < cptr[c + 1]; ++s2) {
+                const int32_t p = fill[f->var[s2]]++;
+                wpos[s2] = p;
+                pc[p] = (int32_t)c;
+                ps[p] = s2;
+            }
+        }
+    }
+    s->n_empty = (int)empty.size();
+    std::vector<Inc> inc;
+    if (s->uniform_k == 3) {  // {clause << 2 | own literal position, lit0, lit1, lit2} per position
+        inc.resize(L);
+        for (int64_t p = 0; p < L; ++p) {
+            const int32_t c = pc[p], s0 = cptr[c];
+            inc[p] = Inc{(c << 2) | (ps[p] - s0), lits[s0], lits[s0 + 1], lits[s0 + 2]};
+        }
     }
     if ((rc = dmalloc(s, (void **)&s->cptr, (m + 1) * 4))) return bail(rc);
     if ((rc = dmalloc(s, (void **)&s->lits, L * 4))) return bail(rc);
     if ((rc = dmalloc(s, (void **)&s->wpos, L * 4))) return bail(rc);
     if ((rc = dmalloc(s, (void **)&s->vptr, (n + 1) * 4))) return bail(rc);
+    if ((rc = dmalloc(s, (void **)&s->pc, L * 4))) return bail(rc);
+    if ((rc = dmalloc(s, (void **)&s->ps, L * 4))) return bail(rc);
+    if ((rc = dmalloc(s, (void **)&s->empty, empty.size() * 4))) return bail(rc);
+    if ((rc = dmalloc(s, (void **)&s->inc, inc.size() * 16))) return bail(rc);
     if (hipMemcpy(s->cptr, cptr.data(), (m + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
         (L && hipMemcpy(s->lits, lits.data(), L * 4, hipMemcpyHostToDevice) != hipSuccess) ||
         (L && hipMemcpy(s->wpos, wpos.data(), L * 4, hipMemcpyHostToDevice) != hipSuccess) ||
+        (L && hipMemcpy(s->pc, pc.data(), L * 4, hipMemcpyHostToDevice) != hipSuccess) ||
+        (L && hipMemcpy(s->ps, ps.data(), L * 4, hipMemcpyHostToDevice) != hipSuccess) ||
+        (!empty.empty() && hipMemcpy(s->empty, empty.data(), empty.size() * 4, hipMemcpyHostToDevice) != hipSuccess) ||
+        (!inc.empty() && hipMemcpy(s->inc, inc.data(), inc.size() * 16, hipMemcpyHostToDevice) != hipSuccess) ||
         hipMemcpy(s->vptr, vptr.data(), (n + 1) * 4, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
-    // state
-    if ((rc = dmalloc(s, &s->v, state_elems(s, n) * s->tsize))) return bail(rc);
-    if ((rc = dmalloc(s, &s->xs, state_elems(s, m) * s->tsize))) return bail(rc);
-    if ((rc = dmalloc(s, &s->xl, state_elems(s, m) * s->tsize))) return bail(rc);
+    // state (double-buffered)
+    for (int b = 0; b < 2; ++b) {
+        if ((rc = dmalloc(s, &s->v[b], state_elems(s, n) * s->tsize))) return bail(rc);
+        if ((rc = dmalloc(s, &s->c[b], 2 * state_elems(s, m) * s->tsize))) return bail(rc);
+    }
+    if ((rc = dmalloc(s, (void **)&s->par, s->G))) return bail(rc);
     if ((rc = dmalloc(s, &s->dtr, s->Bp * s->tsize))) return bail(rc);
     if ((rc = dmalloc(s, &s->err, s->Bp * 8))) return bail(rc);
     if ((rc = dmalloc(s, (void **)&s->unsat, s->Bp * 4))) return bail(rc);
@@ -1159,9 +662,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     if (hipMemsetAsync(s->err, 0, s->Bp * 8, s->stream) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "memset failed"));
     // default state: v = 0, xs = init_short_term_memory, xl = 1
-    if ((rc = init_dispatch(s, 0, 0))) return bail(rc);
-    if (hipMemsetAsync(s->v, 0, state_elems(s, n) * s->tsize, s->stream) != hipSuccess)
-        return bail(fail(ODESAT_EDEVICE, "memset failed"));
+    if ((rc = init_dispatch(s, 0, 0, true))) return bail(rc);
     if ((rc = reset_replicas(s, 0, s->Bp))) return bail(rc);
     if ((rc = set_stop(s, INT_MAX))) return bail(rc);
     *out = s;
@@ -1195,14 +696,22 @@ extern "C" int odesat_set_schedule(odesat_solver *s, int schedule) {
     return ODESAT_OK;
 }
 
+extern "C" int odesat_set_algorithm(odesat_solver *s, int alg) {
+    int rc;
+    if ((rc = check_solver(s))) return rc;
+    if (alg != ODESAT_ALG_FUSED && alg != ODESAT_ALG_TWOPASS) return fail(ODESAT_EINVAL, "bad algorithm");
+    s->alg = alg;
+    return ODESAT_OK;
+}
+
 extern "C" int odesat_set_state(odesat_solver *s, int64_t r0, int64_t count, const double *v, const double *xs,
                                 const double *xl) {
     int rc;
     if ((rc = check_solver(s))) return rc;
     if (r0 < 0 || count < 0 || r0 + count > s->B) return fail(ODESAT_EINVAL, "replica range out of bounds");
-    if ((rc = upload_items(s, s->v, v, s->n, r0, count))) return rc;
-    if ((rc = upload_items(s, s->xs, xs, s->m, r0, count))) return rc;
-    if ((rc = upload_items(s, s->xl, xl, s->m, r0, count))) return rc;
+    if ((rc = upload_items(s, s->v, v, s->n, 1, 0, r0, count))) return rc;
+    if ((rc = upload_items(s, s->c, xs, s->m, 2, 0, r0, count))) return rc;
+    if ((rc = upload_items(s, s->c, xl, s->m, 2, 1, r0, count))) return rc;
     if ((rc = reset_replicas(s, r0, count))) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ODESAT_OK;
@@ -1211,7 +720,7 @@ extern "C" int odesat_set_state(odesat_solver *s, int64_t r0, int64_t count, con
 extern "C" int odesat_init_state(odesat_solver *s, uint64_t seed, int64_t replica0) {
     int rc;
     if ((rc = check_solver(s))) return rc;
-    if ((rc = init_dispatch(s, seed, replica0))) return rc;
+    if ((rc = init_dispatch(s, seed, replica0, false))) return rc;
     if ((rc = reset_replicas(s, 0, s->Bp))) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ODESAT_OK;
@@ -1221,9 +730,9 @@ extern "C" int odesat_get_state(odesat_solver *s, int64_t r0, int64_t count, dou
     int rc;
     if ((rc = check_solver(s))) return rc;
     if (r0 < 0 || count < 0 || r0 + count > s->B) return fail(ODESAT_EINVAL, "replica range out of bounds");
-    if ((rc = download_items(s, s->v, v, s->n, r0, count))) return rc;
-    if ((rc = download_items(s, s->xs, xs, s->m, r0, count))) return rc;
-    if ((rc = download_items(s, s->xl, xl, s->m, r0, count))) return rc;
+    if ((rc = download_items(s, s->v, v, s->n, 1, 0, r0, count))) return rc;
+    if ((rc = download_items(s, s->c, xs, s->m, 2, 0, r0, count))) return rc;
+    if ((rc = download_items(s, s->c, xl, s->m, 2, 1, r0, count))) return rc;
     return ODESAT_OK;
 }
 
@@ -1251,9 +760,10 @@ extern "C" int odesat_compute_derivatives(odesat_solver *s, double zeta, double 
     rc = s->dtype == ODESAT_F64 ? deriv_t<double>(s, zeta) : deriv_t<float>(s, zeta);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
-    if ((rc = download_items(s, s->vh, dv, s->n, 0, s->B))) return rc;
-    if ((rc = download_items(s, s->xsh, dxs, s->m, 0, s->B))) return rc;
-    if ((rc = download_items(s, s->xlh, dxl, s->m, 0, s->B))) return rc;
+    void *const vh[2] = {s->vh, nullptr}, *const ch[2] = {s->ch, nullptr};
+    if ((rc = download_items(s, vh, dv, s->n, 1, 0, 0, s->B))) return rc;
+    if ((rc = download_items(s, ch, dxs, s->m, 2, 0, 0, s->B))) return rc;
+    if ((rc = download_items(s, ch, dxl, s->m, 2, 1, 0, s->B))) return rc;
     if (allsat) {
         std::vector<uint32_t> u(s->Bp);
         HIP_TRY(hipMemcpy(u.data(), s->unsat, s->Bp * 4, hipMemcpyDeviceToHost));
@@ -1333,12 +843,13 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
         return fail(ODESAT_ENOMEM, "hipHostMalloc failed");
     }
     // Schedule: replicas are independent, so with STOP_EACH / STOP_NONE the batch may be stepped
-    // chunk by chunk (all steps of one chunk, then the next): one chunk's state + contribution buffer
-    // stays resident in the Infinity Cache across steps.  STOP_ANY needs lock-step (step-major).
+    // chunk by chunk (all steps of one chunk, then the next).  STOP_ANY needs lock-step.  FUSED has
+    // no per-chunk buffer: its chunk is the whole batch unless CHUNK_MAJOR is forced.
+    const int chunk = s->alg == ODESAT_ALG_TWOPASS || s->schedule == ODESAT_SCHED_CHUNK_MAJOR ? s->chunk_groups : s->G;
     const bool chunk_major = p->stop != ODESAT_STOP_ANY &&
                              (s->schedule == ODESAT_SCHED_CHUNK_MAJOR ||
-                              (s->schedule == ODESAT_SCHED_AUTO && s->G > s->chunk_groups));
-    const int span = chunk_major ? s->chunk_groups : s->G;
+                              (s->schedule == ODESAT_SCHED_AUTO && s->G > chunk));
+    const int span = chunk_major ? chunk : s->G;
     int64_t t_run = 0;
     rc = ODESAT_OK;
     for (int gA = 0; gA < s->G && rc == ODESAT_OK; gA += span) {
@@ -1413,7 +924,10 @@ extern "C" int odesat_profile_read(odesat_solver *s, double *ms, int64_t *launch
 }
 
 extern "C" int64_t odesat_clause_kernel_bytes(const odesat_solver *s) {
-    // per step over the whole batch: v gathered once (4n), xs/xl read + written (16m), in dtype
+    // Algorithmic bytes per step of the dominant kernel over the whole batch, in dtype.
+    // FUSED k_step: v, xs, xl each read and written once (2n + 4m per replica).
+    // TWOPASS k_clause: v gathered once (n), xs / xl read + written (4m).
     if (!s) return -1;
-    return (int64_t)s->B * (s->n + 4 * s->m) * (int64_t)s->tsize;
+    const int64_t per = s->alg == ODESAT_ALG_FUSED ? 2 * s->n + 4 * s->m : s->n + 4 * s->m;
+    return (int64_t)s->B * per * (int64_t)s->tsize;
 }

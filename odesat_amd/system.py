@@ -150,6 +150,10 @@ class Solver:
         """_lib.ODESAT_SCHED_AUTO / _STEP_MAJOR / _CHUNK_MAJOR (results are identical)."""
         check(lib().odesat_set_schedule(self._h, int(schedule)))
 
+    def set_algorithm(self, alg: int):
+        """_lib.ODESAT_ALG_FUSED (default) / _TWOPASS (results are bit-identical)."""
+        check(lib().odesat_set_algorithm(self._h, int(alg)))
+
     def profile(self, enable: bool):
         check(lib().odesat_profile_enable(self._h, 1 if enable else 0))
 
