@@ -142,7 +142,7 @@ def main():
     value = total_replica_steps / wall_max
     ms_per_step = wall_max * 1e3 / args.steps
 
-    # roofline of the dominant kernel (k_clause): algorithmic bytes per launch / mean launch time
+    # roofline of the dominant kernel (k_step): algorithmic bytes per launch / mean launch time
     nlaunch = int(launches[0])
     per_launch_s = ms[0] / 1e3 / nlaunch
     per_launch_bytes = clause_bytes_step * args.steps / nlaunch
@@ -184,7 +184,7 @@ def main():
                                    f"Euler dt=0.01, all replicas stepped (no early exit)",
                        "global_batch": B * world, "batch_per_gpu": B, "n": n, "m": m,
                        "parallelism": f"replica-sharded x{world} (no collectives)"},
-            "roofline": {"bound": "hbm", "kernel": "k_clause_u (clause RHS + fused xs/xl update)",
+            "roofline": {"bound": "hbm", "kernel": "k_step (fused RHS + Euler update, variable-major)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": per_launch_bytes,

@@ -326,6 +326,129 @@ template <typename T> __device__ __forceinline__ void minsec(T val, T &mn, T &se
 }
 
 // ------------------------------------------------------------------------------------------------
+// The 3-SAT incidence stream of one wave (LW = 64: the wave's W replicas of variables [i0, i1)).
+// The wave walks the concatenated incidence lists of its variables as ONE stream of batches of RB
+// incidences, double-buffered: batch k+1's records, voltage gathers and memory row are in flight
+// while batch k computes.  Variable boundaries are crossed inside a batch (uniform branch): the
+// finished variable's v update is written and the next variable's row (prefetched one variable
+// ahead) becomes current.  Accumulation order per variable is unchanged (position order).
+// ------------------------------------------------------------------------------------------------
+template <typename T, int VEC, int RB> struct Batch {
+    Inc rec[RB];
+    Vec<T, VEC> vv[RB][3];
+    Vec<T, 2 * VEC> mem[RB];
+};
+
+template <typename T, int W, int VEC, int MODE, int RB>
+__device__ __forceinline__ void stream_rows3(const KArgs<T> &a, const Bufs<T> &bf, const T *__restrict__ V,
+                                             const T *CM, size_t vbase, size_t cbase, int i0, int i1,
+                                             const T (&h)[VEC], const bool (&on)[VEC], bool all_on,
+                                             bool (&uns)[VEC], T (&e)[VEC]) {
+    const T one = (T)1.0, halfc = (T)0.5;
+    const int P0 = ldc(a.vptr, i0), P1 = ldc(a.vptr, i1);
+    int cur = i0;
+    int cur_end = ldc(a.vptr, i0 + 1);
+    int next_end = i0 + 1 < i1 ? ldc(a.vptr, i0 + 2) : P1;
+    Vec<T, VEC> v_i = ldv<T, VEC>(V + vbase + (size_t)i0 * W);
+    Vec<T, VEC> v_nx = ldv<T, VEC>(V + vbase + (size_t)(i0 + 1 < i1 ? i0 + 1 : i0) * W);
+    T dv[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) dv[k] = (T)0.0;  // :33
+
+    auto finish = [&]() {  // v update of the current variable, then advance (prefetching one ahead)
+        variable_update<T, VEC, MODE>(a, bf, vbase + (size_t)cur * W, v_i, dv, h, on, all_on, e);
+        ++cur;
+        v_i = v_nx;
+        cur_end = next_end;
+        if (cur + 1 < i1) {
+            next_end = ldc(a.vptr, cur + 2);
+            v_nx = ldv<T, VEC>(V + vbase + (size_t)(cur + 1) * W);
+        }
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) dv[k] = (T)0.0;
+    };
+    auto load_recs = [&](Inc (&r)[RB], int q0) {
+#pragma unroll
+        for (int b = 0; b < RB; ++b) r[b] = ldc4(a.inc, q0 + b < P1 ? q0 + b : P1 - 1);
+    };
+    auto issue = [&](Batch<T, VEC, RB> &B, const Inc (&r)[RB]) {
+#pragma unroll
+        for (int b = 0; b < RB; ++b) {
+            B.rec[b] = r[b];
+            B.vv[b][0] = ldv<T, VEC>(V + vbase + (size_t)(r[b].y >> 1) * W);
+            B.vv[b][1] = ldv<T, VEC>(V + vbase + (size_t)(r[b].z >> 1) * W);
+            B.vv[b][2] = ldv<T, VEC>(V + vbase + (size_t)(r[b].w >> 1) * W);
+        }
+#pragma unroll
+        for (int b = 0; b < RB; ++b) B.mem[b] = ldv_nt<T, 2 * VEC>(CM + cbase + (size_t)(r[b].x >> 2) * W * 2);
+    };
+    auto compute = [&](const Batch<T, VEC, RB> &B, int q0) {
+#pragma unroll
+        for (int b = 0; b < RB; ++b) {
+            const int q = q0 + b;
+            if (q < P1) {
+            while (q >= cur_end) finish();  // crossed into the next variable(s) (degree-0 ones too)
+            const int lit[3] = {B.rec[b].y, B.rec[b].z, B.rec[b].w};
+            const int own = B.rec[b].x & 3;
+            const int c = B.rec[b].x >> 2;
+            const int lo = own == 0 ? lit[0] : (own == 1 ? lit[1] : lit[2]);
+            const T qo = (lo & 1) ? (T)-1.0 : (T)1.0;
+            T C[VEC];
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                T mn = inf_v<T>(), sec = inf_v<T>();
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {  // :43-57
+                    const T qj = (lit[j] & 1) ? (T)-1.0 : (T)1.0;
+                    minsec(one - qj * B.vv[b][j].e[k], mn, sec);
+                }
+                C[k] = halfc * mn;  // :60
+                const T xs_m = B.mem[b].e[2 * k], xl_m = B.mem[b].e[2 * k + 1];
+                const T t = xl_m * xs_m;
+                const T tr = (one + a.zeta * xl_m) * (one - xs_m);
+                const T vio = own == 0 ? B.vv[b][0].e[k] : (own == 1 ? B.vv[b][1].e[k] : B.vv[b][2].e[k]);
+                const T val = one - qo * vio;
+                const T g_ = halfc * qo * (val != mn ? mn : sec);                    // :64-70
+                const T r_ = (C[k] == one - qo * vio) ? halfc * (qo - vio) : (T)0.0;  // :73-77
+                dv[k] += t * g_ + tr * r_;                                            // :80
+                if (MODE != M_ADB && own == 0) uns[k] = uns[k] || (on[k] && !(C[k] < (T)0.25));
+            }
+            if (own == 0)  // the clause's first literal owns its memories
+                clause_update<T, VEC, MODE>(a, bf, cbase + (size_t)c * W * 2, C, B.mem[b], h, on, all_on, e);
+            }
+        }
+    };
+
+    if (P0 < P1) {
+        Batch<T, VEC, RB> A, Bb;
+        Inc rn[RB];
+        int qa = P0, qb = P0 + RB;
+        load_recs(rn, qa);
+        issue(A, rn);
+        if (qb < P1) load_recs(rn, qb);
+        for (;;) {
+            const bool hb = qb < P1;
+            if (hb) {
+                issue(Bb, rn);
+                if (qb + RB < P1) load_recs(rn, qb + RB);
+            }
+            compute(A, qa);
+            if (!hb) break;
+            qa = qb + RB;
+            const bool ha = qa < P1;
+            if (ha) {
+                issue(A, rn);
+                if (qa + RB < P1) load_recs(rn, qa + RB);
+            }
+            compute(Bb, qb);
+            if (!ha) break;
+            qb = qa + RB;
+        }
+    }
+    while (cur < i1) finish();  // the last variable(s), degree-0 tails included
+}
+
+// ------------------------------------------------------------------------------------------------
 // k_step (FUSED): one RHS (+ update) per launch, variable-major.  K > 0: every clause has K
 // literals (random k-SAT) -- RB incidences per batch, all their loads issued before the first use.
 // K == 0: mixed clause widths, one incidence at a time.
@@ -354,6 +477,13 @@ __global__ __launch_bounds__(256) void k_step(KArgs<T> a) {
     for (int k = 0; k < VEC; ++k) {
         uns[k] = false;
         e[k] = (T)0.0;
+    }
+    if constexpr (LW == 64 && K == 3) {
+        const int i0 = __builtin_amdgcn_readfirstlane(geo.tile * a.rows);
+        const int i1 = min(i0 + a.rows, a.n);
+        if (i0 < i1) stream_rows3<T, W, VEC, MODE, RB>(a, bf, V, CM, vbase, cbase, i0, i1, h, on, all_on, uns, e);
+        flush_flags<T, VEC, MODE>(a, geo.r0, on, uns, e);
+        return;
     }
     for (int row = 0; row < a.rows; ++row) {
         int i = (geo.tile * a.rows + row) * IPR + geo.isub;
