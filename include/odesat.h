@@ -164,11 +164,18 @@ int odesat_set_chunk_replicas(odesat_solver *s, int64_t replicas);
 #define ODESAT_SCHED_CHUNK_MAJOR 2 /* every chunk: all steps, then the next chunk */
 int odesat_set_schedule(odesat_solver *s, int schedule);
 /* Per-step algorithm (results are bit-identical):
- * FUSED   = one variable-major kernel per RHS, clauses recomputed from L2-resident voltages;
- * TWOPASS = clause kernel writing per-literal contributions + variable kernel summing them. */
+ * FUSED    = one variable-major kernel per RHS, clauses recomputed from L2-resident voltages;
+ * TWOPASS  = clause kernel writing per-literal contributions + variable kernel summing them;
+ * RESIDENT = persistent kernel, one workgroup per replica group with its voltages in LDS for many
+ *            steps (odesat_simulate only; single-step calls use FUSED).  Available when the
+ *            solver's group layout was chosen for it (the default when the voltages fit in LDS). */
 #define ODESAT_ALG_FUSED 0
 #define ODESAT_ALG_TWOPASS 1
+#define ODESAT_ALG_RESIDENT 2
 int odesat_set_algorithm(odesat_solver *s, int alg);
+/* The algorithm odesat_simulate uses (ODESAT_ALG_*), and the solver's replica group width. */
+int odesat_get_algorithm(const odesat_solver *s);
+int odesat_group_width(const odesat_solver *s);
 
 #ifdef __cplusplus
 }

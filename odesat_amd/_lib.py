@@ -16,7 +16,7 @@ ODESAT_OK, ODESAT_EINVAL, ODESAT_ENOMEM, ODESAT_EDEVICE, ODESAT_ESTATE = 0, -1, 
 ODESAT_F32, ODESAT_F64 = 0, 1
 ODESAT_STOP_EACH, ODESAT_STOP_ANY, ODESAT_STOP_NONE = 0, 1, 2
 ODESAT_SCHED_AUTO, ODESAT_SCHED_STEP_MAJOR, ODESAT_SCHED_CHUNK_MAJOR = 0, 1, 2
-ODESAT_ALG_FUSED, ODESAT_ALG_TWOPASS = 0, 1
+ODESAT_ALG_FUSED, ODESAT_ALG_TWOPASS, ODESAT_ALG_RESIDENT = 0, 1, 2
 
 
 class OdesatError(RuntimeError):
@@ -73,6 +73,8 @@ SIGNATURES = {
     "odesat_set_chunk_replicas": (C.c_int, [_P, _i64]),
     "odesat_set_schedule": (C.c_int, [_P, C.c_int]),
     "odesat_set_algorithm": (C.c_int, [_P, C.c_int]),
+    "odesat_get_algorithm": (C.c_int, [_P]),
+    "odesat_group_width": (C.c_int, [_P]),
 }
 
 _lib = None

@@ -18,6 +18,7 @@
 #include "../../include/odesat.h"
 #include "cnf.hpp"
 #include "kernels.hpp"
+#include "resident.hpp"
 
 using odesat::fail;
 using namespace odk;
@@ -54,6 +55,11 @@ struct odesat_solver {
     uint8_t *act = nullptr;
     int64_t *sat_step = nullptr, *steps_done = nullptr;
     int32_t *stop = nullptr;
+    // RESIDENT (resident.hpp): group width W == res_R replicas per workgroup, clause tiles
+    int res_R = 0;  // 0 = the layout does not admit the resident kernel
+    int res_ntiles = 0, res_ts = 0;
+    int32_t *res_cl = nullptr, *res_tc = nullptr, *res_tseg = nullptr;
+    int2 *res_seg = nullptr;
     int64_t bytes = 0;
     // profiling
     bool profile = false;
@@ -272,7 +278,7 @@ int step_groups(odesat_solver *s, int step, T dt, T zeta, int gA, int gB) {
     a.dt = dt;
     a.zeta = zeta;
     int rc;
-    if (s->alg == ODESAT_ALG_FUSED) {
+    if (s->alg != ODESAT_ALG_TWOPASS) {  // FUSED (RESIDENT's single steps too)
         a.g0 = gA;
         a.ng = gB - gA;
         return launch_kernel<T, LW, VEC, MODE>(s, a, K_STEP);
@@ -340,6 +346,146 @@ int dispatch_step(odesat_solver *s, int step, bool adaptive, double dt, double z
                   int gA, int gB) {
     return s->dtype == ODESAT_F64 ? enqueue_step<double>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB)
                                   : enqueue_step<float>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB);
+}
+
+// ---- RESIDENT ---------------------------------------------------------------------------------
+constexpr size_t RES_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS budget (static flags take < 1 KiB)
+
+size_t res_lds_bytes(int64_t n, int R, int ts, size_t tsize, bool adaptive) {
+    return ((adaptive ? 3 : 2) * (size_t)n * R + 2 * (size_t)ts * R) * tsize;
+}
+
+// Tile slot capacity for R replicas per workgroup (0 = the voltages do not fit in LDS).
+int res_tile_slots(int64_t n, int uniform_k, int R, size_t tsize) {
+    if (n >= 65536) return 0;  // packed slot word: 16-bit variable, 17-bit literal
+    if (uniform_k == 3) {
+        const int ts = 3 * (RES_THREADS / R);
+        return res_lds_bytes(n, R, ts, tsize, true) <= RES_LDS_MAX ? ts : 0;
+    }
+    const size_t fixed = res_lds_bytes(n, R, 0, tsize, true);
+    if (fixed >= RES_LDS_MAX) return 0;
+    const size_t ts = std::min<size_t>(32767, (RES_LDS_MAX - fixed) / (2 * (size_t)R * tsize));
+    return ts >= 256 ? (int)ts : 0;
+}
+
+// Clause tiles: consecutive clauses, at most ts slots (3-SAT: 1024 / R clauses) per tile.  Per tile,
+// the slots sorted by (variable, slot) give each slot its position in the tile's contribution
+// buffer; each run of one variable is a fold segment {var, start | end << 16}.
+int build_resident(odesat_solver *s, const odesat_cnf *f, int R, int ts) {
+    const int64_t m = s->m, L = s->L;
+    std::vector<int32_t> tc{0}, tseg{0}, cl(L);
+    std::vector<int2> seg;
+    const int64_t max_clauses = RES_THREADS / R;
+    int64_t c = 0;
+    while (c < m) {
+        const int64_t c0 = c;
+        int64_t slots = 0;
+        while (c < m && c - c0 < (s->uniform_k == 3 ? max_clauses : 4 * max_clauses)) {
+            const int64_t k = f->clause_ptr[c + 1] - f->clause_ptr[c];
+            if (slots + k > ts) break;
+            slots += k;
+            ++c;
+        }
+        if (c == c0) return fail(ODESAT_EINVAL, "clause wider than a resident tile");
+        const int64_t sA = f->clause_ptr[c0], sB = f->clause_ptr[c];
+        std::vector<int64_t> order((size_t)(sB - sA));
+        for (int64_t k = 0; k < sB - sA; ++k) order[k] = sA + k;
+        std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return f->var[x] < f->var[y]; });
+        int64_t start = 0;
+        for (int64_t p = 0; p < (int64_t)order.size(); ++p) {
+            const int64_t sl = order[p];
+            const int32_t lit = (int32_t)((f->var[sl] << 1) | (f->neg[sl] ? 1 : 0));
+            cl[sl] = (int32_t)(p << RES_LIT_BITS) | lit;
+            if (p + 1 == (int64_t)order.size() || f->var[order[p + 1]] != f->var[sl]) {
+                seg.push_back(make_int2((int)f->var[sl], (int)(start | ((p + 1) << 16))));
+                start = p + 1;
+            }
+        }
+        tc.push_back((int32_t)c);
+        tseg.push_back((int32_t)seg.size());
+    }
+    s->res_ntiles = (int)(tc.size() - 1);
+    s->res_ts = ts;
+    int rc;
+    if ((rc = dmalloc(s, (void **)&s->res_cl, cl.size() * 4))) return rc;
+    if ((rc = dmalloc(s, (void **)&s->res_tc, tc.size() * 4))) return rc;
+    if ((rc = dmalloc(s, (void **)&s->res_tseg, tseg.size() * 4))) return rc;
+    if ((rc = dmalloc(s, (void **)&s->res_seg, seg.size() * 8))) return rc;
+    if ((!cl.empty() && hipMemcpy(s->res_cl, cl.data(), cl.size() * 4, hipMemcpyHostToDevice) != hipSuccess) ||
+        hipMemcpy(s->res_tc, tc.data(), tc.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(s->res_tseg, tseg.data(), tseg.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        (!seg.empty() && hipMemcpy(s->res_seg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice) != hipSuccess))
+        return fail(ODESAT_EDEVICE, "resident topology upload failed");
+    s->res_R = R;
+    return ODESAT_OK;
+}
+
+template <typename T, int R, bool ADA, bool K3> int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
+    static bool attr_set = false;  // per instantiation
+    const size_t lds = res_lds_bytes(s->n, R, s->res_ts, sizeof(T), ADA);
+    if (!attr_set) {
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)RES_LDS_MAX));
+        attr_set = true;
+    }
+    {
+        Timed tm(s, 0);
+        hipLaunchKernelGGL((k_resident<T, R, ADA, K3>), dim3(s->G), dim3(RES_THREADS), lds, s->stream, a);
+    }
+    HIP_TRY(hipGetLastError());
+    return ODESAT_OK;
+}
+
+template <typename T>
+int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
+                    int stop_mode) {
+    RArgs<T> a{};
+    a.cl = s->res_cl;
+    a.cptr = s->cptr;
+    a.tc = s->res_tc;
+    a.tseg = s->res_tseg;
+    a.seg = s->res_seg;
+    a.v0 = (T *)s->v[0];
+    a.v1 = (T *)s->v[1];
+    a.c0 = (T *)s->c[0];
+    a.c1 = (T *)s->c[1];
+    a.par = s->par;
+    a.cf = (T *)s->cf;
+    a.ch = (T *)s->ch;
+    a.dtr = (T *)s->dtr;
+    a.act = s->act;
+    a.sat_step = s->sat_step;
+    a.steps_done = s->steps_done;
+    a.stop = s->stop;
+    a.n = (int32_t)s->n;
+    a.m = (int32_t)s->m;
+    a.ntiles = s->res_ntiles;
+    a.ts = s->res_ts;
+    a.step0 = step0;
+    a.nsteps = nsteps;
+    a.stop_mode = stop_mode;
+    a.dt = (T)dt;
+    a.zeta = (T)zeta;
+    a.xl_max = (T)1e4 * (T)s->m;  // system.rs:95
+    a.tol = tol;
+    const bool k3 = s->uniform_k == 3;
+    auto go = [&](auto rr) -> int {
+        constexpr int R = decltype(rr)::value;
+        if (adaptive) return k3 ? launch_resident_k<T, R, true, true>(s, a) : launch_resident_k<T, R, true, false>(s, a);
+        return k3 ? launch_resident_k<T, R, false, true>(s, a) : launch_resident_k<T, R, false, false>(s, a);
+    };
+    switch (s->res_R) {
+        case 1: return go(IC<1>{});
+        case 2: return go(IC<2>{});
+        case 4: return go(IC<4>{});
+        default: return fail(ODESAT_EINVAL, "resident layout not available");
+    }
+}
+
+int dispatch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
+                      int stop_mode) {
+    return s->dtype == ODESAT_F64 ? launch_resident<double>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode)
+                                  : launch_resident<float>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode);
 }
 
 template <typename T> int deriv_t(odesat_solver *s, double zeta) {
@@ -528,7 +674,7 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     for (auto e : s->pool) (void)hipEventDestroy(e);
     void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->pc, s->ps, s->empty, s->inc, s->v[0], s->v[1], s->c[0],
                     s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
-                    s->sat_step, s->steps_done, s->stop};
+                    s->sat_step, s->steps_done, s->stop, s->res_cl, s->res_tc, s->res_tseg, s->res_seg};
     for (void *p : ptrs) dfree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
@@ -569,16 +715,30 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     s->m = m;
     s->L = L;
     s->B = batch;
-    // layout: W = min(next pow2 >= batch, 64) replicas per group, one lane per
-    // replica, 64/W items per wave.  Measured on MI355X (config 2, B = 1024): W = 64 beats 32 / 16
-    // by 1.5-1.7x although a smaller group's voltage table would fit an XCD's L2 better -- the
-    // narrower rows cost more in instructions than they save in bytes.  ODESAT_GROUP_WIDTH
-    // overrides (tuning).
-    int lw = 1;
-    while (lw < batch && lw < 64) lw <<= 1;
+    s->uniform_k = m > 0 ? (int)(f->clause_ptr[1] - f->clause_ptr[0]) : 0;
+    for (int64_t c = 0; c < m && s->uniform_k; ++c)
+        if (f->clause_ptr[c + 1] - f->clause_ptr[c] != s->uniform_k) s->uniform_k = 0;
+    if (s->uniform_k != 3) s->uniform_k = 0;  // the specialised kernels are instantiated for 3-SAT
+    // layout.  When the voltages of a replica fit in LDS, the group width is the
+    // RESIDENT kernel's replicas per workgroup R (1, 2 or 4: as many as fit while there are still
+    // >= 256 workgroups) and RESIDENT is the default.  Otherwise W = min(next pow2 >= batch, 64)
+    // for FUSED (measured on MI355X, config 2: W = 64 beats 32 / 16 by 1.5-1.7x).
+    // ODESAT_GROUP_WIDTH overrides (tuning; RESIDENT only if that width admits it).
+    int lw = 1, res_r = 0;
+    if (res_tile_slots(n, s->uniform_k, 1, s->tsize) > 0) {
+        res_r = 1;
+        while (res_r < 4 && res_tile_slots(n, s->uniform_k, 2 * res_r, s->tsize) > 0 && batch >= 2 * res_r * 256)
+            res_r *= 2;
+        lw = res_r;
+    } else {
+        while (lw < batch && lw < 64) lw <<= 1;
+    }
     if (const char *ev = std::getenv("ODESAT_GROUP_WIDTH")) {
         const int want = std::atoi(ev);
-        if (want == 1 || want == 2 || want == 4 || want == 8 || want == 16 || want == 32 || want == 64) lw = want;
+        if (want == 1 || want == 2 || want == 4 || want == 8 || want == 16 || want == 32 || want == 64) {
+            lw = want;
+            res_r = (want <= 4 && res_tile_slots(n, s->uniform_k, want, s->tsize) > 0) ? want : 0;
+        }
     }
     s->LW = lw;
     s->VEC = 1;
@@ -587,10 +747,6 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     s->Bp = (batch + s->W - 1) / s->W * s->W;
     s->G = (int)(s->Bp / s->W);
     pick_chunk(s, 0);
-    s->uniform_k = m > 0 ? (int)(f->clause_ptr[1] - f->clause_ptr[0]) : 0;
-    for (int64_t c = 0; c < m && s->uniform_k; ++c)
-        if (f->clause_ptr[c + 1] - f->clause_ptr[c] != s->uniform_k) s->uniform_k = 0;
-    if (s->uniform_k != 3) s->uniform_k = 0;  // the specialised kernels are instantiated for 3-SAT
     int rc = ODESAT_OK;
     auto bail = [&](int code) {
         odesat_solver_destroy(s);
@@ -646,6 +802,10 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         (!inc.empty() && hipMemcpy(s->inc, inc.data(), inc.size() * 16, hipMemcpyHostToDevice) != hipSuccess) ||
         hipMemcpy(s->vptr, vptr.data(), (n + 1) * 4, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
+    if (res_r > 0) {
+        if ((rc = build_resident(s, f, res_r, res_tile_slots(n, s->uniform_k, res_r, s->tsize)))) return bail(rc);
+        s->alg = ODESAT_ALG_RESIDENT;
+    }
     // state (double-buffered)
     for (int b = 0; b < 2; ++b) {
         if ((rc = dmalloc(s, &s->v[b], state_elems(s, n) * s->tsize))) return bail(rc);
@@ -699,10 +859,20 @@ extern "C" int odesat_set_schedule(odesat_solver *s, int schedule) {
 extern "C" int odesat_set_algorithm(odesat_solver *s, int alg) {
     int rc;
     if ((rc = check_solver(s))) return rc;
-    if (alg != ODESAT_ALG_FUSED && alg != ODESAT_ALG_TWOPASS) return fail(ODESAT_EINVAL, "bad algorithm");
+    if (alg != ODESAT_ALG_FUSED && alg != ODESAT_ALG_TWOPASS && alg != ODESAT_ALG_RESIDENT)
+        return fail(ODESAT_EINVAL, "bad algorithm");
+    if (alg == ODESAT_ALG_RESIDENT && s->res_R == 0)
+        return fail(ODESAT_EINVAL, "RESIDENT needs the voltages of a replica group in LDS: this solver's layout "
+                                   "(group width " + std::to_string(s->W) + ") does not admit it");
     s->alg = alg;
     return ODESAT_OK;
 }
+
+extern "C" int odesat_get_algorithm(const odesat_solver *s) {
+    return s ? s->alg : fail(ODESAT_EINVAL, "null solver");
+}
+
+extern "C" int odesat_group_width(const odesat_solver *s) { return s ? s->W : fail(ODESAT_EINVAL, "null solver"); }
 
 extern "C" int odesat_set_state(odesat_solver *s, int64_t r0, int64_t count, const double *v, const double *xs,
                                 const double *xl) {
@@ -812,6 +982,53 @@ extern "C" int odesat_euler_step(odesat_solver *s, double tol, double *dt, doubl
     return single_step(s, true, tol, 0.0, zeta, dt, allsat);
 }
 
+// odesat_simulate for RESIDENT: launches of many steps (STOP_ANY: one step per launch, so no
+// replica runs past the step at which another one satisfied the formula), polled every `poll`
+// steps.
+static int finish_simulate(odesat_solver *s, const odesat_params *p, bool adaptive, int64_t t_run,
+                           int64_t *first_sat_step, int64_t *steps_done, double *dt_out, int64_t *steps_run) {
+    int rc;
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (steps_run) *steps_run = t_run;
+    if (first_sat_step) HIP_TRY(hipMemcpy(first_sat_step, s->sat_step, s->B * 8, hipMemcpyDeviceToHost));
+    if (steps_done) HIP_TRY(hipMemcpy(steps_done, s->steps_done, s->B * 8, hipMemcpyDeviceToHost));
+    if (dt_out) {
+        if (!adaptive) {
+            for (int64_t r = 0; r < s->B; ++r) dt_out[r] = p->dt;
+        } else if ((rc = get_dt(s, dt_out))) {
+            return rc;
+        }
+    }
+    return s->profile ? ODESAT_OK : drain_profile(s);
+}
+
+static int simulate_resident(odesat_solver *s, const odesat_params *p, bool adaptive, double zeta, double tol,
+                             int poll, int64_t *first_sat_step, int64_t *steps_done, double *dt_out,
+                             int64_t *steps_run) {
+    int rc = ODESAT_OK;
+    const int per_launch = p->stop == ODESAT_STOP_ANY ? 1 : (p->stop == ODESAT_STOP_EACH ? poll : 64);
+    int32_t h_stop = INT_MAX;
+    std::vector<uint8_t> h_act(s->Bp);
+    int64_t t = 0;
+    while (t < p->max_steps) {
+        const int k = (int)std::min<int64_t>(per_launch, p->max_steps - t);
+        if ((rc = dispatch_resident(s, (int)t, k, adaptive, p->dt, zeta, tol, p->stop))) return rc;
+        t += k;
+        if (p->stop != ODESAT_STOP_NONE && t % poll == 0 && t < p->max_steps) {
+            HIP_TRY(hipMemcpyAsync(&h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipMemcpyAsync(h_act.data(), s->act, s->Bp, hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            if (p->stop == ODESAT_STOP_ANY && h_stop != INT_MAX) break;
+            if (p->stop == ODESAT_STOP_EACH) {
+                bool any = false;
+                for (int64_t r = 0; r < s->B && !any; ++r) any = h_act[r] != 0;
+                if (!any) break;
+            }
+        }
+    }
+    return finish_simulate(s, p, adaptive, t, first_sat_step, steps_done, dt_out, steps_run);
+}
+
 extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t *first_sat_step,
                                int64_t *steps_done, double *dt_out, int64_t *steps_run) {
     int rc;
@@ -835,6 +1052,8 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
         if (adaptive && (rc = put_dt(s, nullptr, 0.01))) return rc;
     }
     const int poll = p->poll_interval > 0 ? p->poll_interval : 32;
+    if (s->alg == ODESAT_ALG_RESIDENT) return simulate_resident(s, p, adaptive, zeta, tol, poll, first_sat_step,
+                                                                steps_done, dt_out, steps_run);
     int32_t *h_stop = nullptr;
     uint8_t *h_act = nullptr;
     HIP_TRY(hipHostMalloc((void **)&h_stop, sizeof(int32_t)));

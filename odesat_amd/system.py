@@ -151,8 +151,16 @@ class Solver:
         check(lib().odesat_set_schedule(self._h, int(schedule)))
 
     def set_algorithm(self, alg: int):
-        """_lib.ODESAT_ALG_FUSED (default) / _TWOPASS (results are bit-identical)."""
+        """_lib.ODESAT_ALG_FUSED / _TWOPASS / _RESIDENT (results are bit-identical)."""
         check(lib().odesat_set_algorithm(self._h, int(alg)))
+
+    @property
+    def algorithm(self) -> int:
+        return check(lib().odesat_get_algorithm(self._h))
+
+    @property
+    def group_width(self) -> int:
+        return check(lib().odesat_group_width(self._h))
 
     def profile(self, enable: bool):
         check(lib().odesat_profile_enable(self._h, 1 if enable else 0))

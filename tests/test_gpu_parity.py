@@ -370,16 +370,67 @@ def test_algorithms_identical(name, prec, B):
     f = product_formula(name)
     for adaptive in (False, True):
         out = []
-        for alg in (_lib.ODESAT_ALG_FUSED, _lib.ODESAT_ALG_TWOPASS):
+        for alg in (_lib.ODESAT_ALG_RESIDENT, _lib.ODESAT_ALG_FUSED, _lib.ODESAT_ALG_TWOPASS):
             with Solver(f, B, prec) as s:
+                assert s.algorithm == _lib.ODESAT_ALG_RESIDENT  # these formulas fit in LDS
                 s.set_algorithm(alg)
                 s.init_state(21)
                 r = s.simulate(adaptive=adaptive, dt=0.05, max_steps=80, stop=ODESAT_STOP_EACH, poll_interval=3)
                 out.append((r["first_sat_step"], r["steps_done"], r["dt"], s.get_state()))
-        assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
-        assert same(out[0][2], out[1][2])
-        for x, y in zip(out[0][3], out[1][3]):
-            assert same(x, y)
+        for o in out[1:]:
+            assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1])
+            assert same(out[0][2], o[2])
+            for x, y in zip(out[0][3], o[3]):
+                assert same(x, y)
+
+
+def _run_layout(monkeypatch, f, B, prec, width, **kw):
+    from odesat_amd import _lib
+    if width is None:
+        monkeypatch.delenv("ODESAT_GROUP_WIDTH", raising=False)
+    else:
+        monkeypatch.setenv("ODESAT_GROUP_WIDTH", str(width))
+    with Solver(f, B, prec) as s:
+        alg, w = s.algorithm, s.group_width
+        s.init_state(5)
+        r = s.simulate(**kw)
+        st = s.get_state()
+    monkeypatch.delenv("ODESAT_GROUP_WIDTH", raising=False)
+    return alg, w, r, st
+
+
+@pytest.mark.parametrize("name", ["rand200", "small", "hard"])
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("width", [1, 2, 4])
+@pytest.mark.parametrize("mode", ["fixed-each", "fixed-any", "fixed-none", "adaptive-each", "adaptive-any"])
+def test_resident_widths_match_fused_w64(monkeypatch, name, prec, width, mode):
+    """RESIDENT with R = 1, 2, 4 replicas per workgroup (LDS-resident voltages, tiled clause pass +
+    ordered fold) == FUSED at group width 64: every stop policy, fixed and adaptive steps."""
+    from odesat_amd import _lib
+    f = product_formula(name)
+    adaptive = mode.startswith("adaptive")
+    stop = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[mode.split("-")[1]]
+    kw = dict(adaptive=adaptive, dt=0.05, tol=1e-3, max_steps=150, stop=stop, poll_interval=4)
+    B = 37
+    a1, w1, r1, s1 = _run_layout(monkeypatch, f, B, prec, width, **kw)
+    a2, w2, r2, s2 = _run_layout(monkeypatch, f, B, prec, 64, **kw)
+    assert (a1, w1) == (_lib.ODESAT_ALG_RESIDENT, width) and (a2, w2) == (_lib.ODESAT_ALG_FUSED, 64)
+    assert np.array_equal(r1["first_sat_step"], r2["first_sat_step"])
+    assert np.array_equal(r1["steps_done"], r2["steps_done"]) and r1["steps_run"] == r2["steps_run"]
+    assert same(r1["dt"], r2["dt"])
+    for x, y in zip(s1, s2):
+        assert same(x, y)
+
+
+def test_default_layout_is_resident_for_config2():
+    from odesat_amd import _lib
+    c = wl.CONFIGS["config2"]
+    var, neg = wl.random_ksat(c["n"], c["m"], 3, c["seed"])
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
+    for prec, alg in (("f32", _lib.ODESAT_ALG_RESIDENT), ("f64", _lib.ODESAT_ALG_FUSED)):
+        with Solver(f, 1024, prec) as s:
+            assert s.algorithm == alg
 
 
 def test_frozen_replicas_keep_state_across_buffer_flips():
