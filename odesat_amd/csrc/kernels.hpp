@@ -953,14 +953,15 @@ __global__ void k_init(T *v, T *cm, const int32_t *cptr, const int32_t *lits, in
     }
 }
 
-// compact [count][items] f64 <-> layout [G][items][W] (buffer par[g] of the pair) in dtype T
+// compact [count][items] f64 <-> layout [G][items][W] (buffer par[g] of the pair) in dtype T;
+// imap (clause arrays) maps the caller's clause index to the internal clause order
 template <typename T>
-__global__ void k_scatter(T *b0, T *b1, const uint8_t *par, const double *src, int items, int W, int stride,
-                          int comp, int64_t r0, int64_t count) {
+__global__ void k_scatter(T *b0, T *b1, const uint8_t *par, const double *src, const int32_t *imap, int items, int W,
+                          int stride, int comp, int64_t r0, int64_t count) {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= (size_t)count * items) return;
     const int64_t b = (int64_t)(tid / items);
-    const int i = (int)(tid % items);
+    const int i = imap ? imap[tid % items] : (int)(tid % items);
     const int64_t r = r0 + b;
     const int64_t g = r / W;
     T *dst = (par && par[g]) ? b1 : b0;
@@ -968,12 +969,12 @@ __global__ void k_scatter(T *b0, T *b1, const uint8_t *par, const double *src, i
 }
 
 template <typename T>
-__global__ void k_gather(double *dst, const T *b0, const T *b1, const uint8_t *par, int items, int W, int stride,
-                         int comp, int64_t r0, int64_t count) {
+__global__ void k_gather(double *dst, const T *b0, const T *b1, const uint8_t *par, const int32_t *imap, int items,
+                         int W, int stride, int comp, int64_t r0, int64_t count) {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= (size_t)count * items) return;
     const int64_t b = (int64_t)(tid / items);
-    const int i = (int)(tid % items);
+    const int i = imap ? imap[tid % items] : (int)(tid % items);
     const int64_t r = r0 + b;
     const int64_t g = r / W;
     const T *src = (par && par[g]) ? b1 : b0;

@@ -55,11 +55,13 @@ struct odesat_solver {
     uint8_t *act = nullptr;
     int64_t *sat_step = nullptr, *steps_done = nullptr;
     int32_t *stop = nullptr;
-    // RESIDENT (resident.hpp): group width W == res_R replicas per workgroup, clause tiles
-    int res_R = 0;  // 0 = the layout does not admit the resident kernel
-    int res_ntiles = 0, res_ts = 0;
-    int32_t *res_cl = nullptr, *res_tc = nullptr, *res_tseg = nullptr;
-    int2 *res_seg = nullptr;
+    // RESIDENT (resident.hpp): group width W == res_R replicas per workgroup; clauses are stored
+    // in the internal (tile) order, cmap[original clause] = internal clause
+    int res_R = 0;        // 0 = the layout does not admit the resident kernel
+    bool res_ada = false; // adaptive steps fit in LDS too (else they run FUSED on the same layout)
+    int res_ntiles = 0;
+    int32_t *res_tc = nullptr, *cmap = nullptr;
+    int4 *res_cl4 = nullptr;
     int64_t bytes = 0;
     // profiling
     bool profile = false;
@@ -351,78 +353,51 @@ int dispatch_step(odesat_solver *s, int step, bool adaptive, double dt, double z
 // ---- RESIDENT ---------------------------------------------------------------------------------
 constexpr size_t RES_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS budget (static flags take < 1 KiB)
 
-size_t res_lds_bytes(int64_t n, int R, int ts, size_t tsize, bool adaptive) {
-    return ((adaptive ? 3 : 2) * (size_t)n * R + 2 * (size_t)ts * R) * tsize;
+size_t res_lds_bytes(int64_t n, int R, size_t tsize, bool adaptive) {
+    return (adaptive ? 3 : 2) * (size_t)n * R * tsize;  // v, dv (+ the full-step clone of v)
 }
 
-// Tile slot capacity for R replicas per workgroup (0 = the voltages do not fit in LDS).
-int res_tile_slots(int64_t n, int uniform_k, int R, size_t tsize) {
-    if (n >= 65536) return 0;  // packed slot word: 16-bit variable, 17-bit literal
-    if (uniform_k == 3) {
-        const int ts = 3 * (RES_THREADS / R);
-        return res_lds_bytes(n, R, ts, tsize, true) <= RES_LDS_MAX ? ts : 0;
-    }
-    const size_t fixed = res_lds_bytes(n, R, 0, tsize, true);
-    if (fixed >= RES_LDS_MAX) return 0;
-    const size_t ts = std::min<size_t>(32767, (RES_LDS_MAX - fixed) / (2 * (size_t)R * tsize));
-    return ts >= 256 ? (int)ts : 0;
+bool res_fits(int64_t n, int R, size_t tsize, bool adaptive) {
+    return n < (1ll << 24) && res_lds_bytes(n, R, tsize, adaptive) <= RES_LDS_MAX;
 }
 
-// Clause tiles: consecutive clauses, at most ts slots (3-SAT: 1024 / R clauses) per tile.  Per tile,
-// the slots sorted by (variable, slot) give each slot its position in the tile's contribution
-// buffer; each run of one variable is a fold segment {var, start | end << 16}.
-int build_resident(odesat_solver *s, const odesat_cnf *f, int R, int ts) {
-    const int64_t m = s->m, L = s->L;
-    std::vector<int32_t> tc{0}, tseg{0}, cl(L);
-    std::vector<int2> seg;
-    const int64_t max_clauses = RES_THREADS / R;
-    int64_t c = 0;
-    while (c < m) {
-        const int64_t c0 = c;
-        int64_t slots = 0;
-        while (c < m && c - c0 < (s->uniform_k == 3 ? max_clauses : 4 * max_clauses)) {
-            const int64_t k = f->clause_ptr[c + 1] - f->clause_ptr[c];
-            if (slots + k > ts) break;
-            slots += k;
-            ++c;
-        }
-        if (c == c0) return fail(ODESAT_EINVAL, "clause wider than a resident tile");
-        const int64_t sA = f->clause_ptr[c0], sB = f->clause_ptr[c];
-        std::vector<int64_t> order((size_t)(sB - sA));
-        for (int64_t k = 0; k < sB - sA; ++k) order[k] = sA + k;
-        std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return f->var[x] < f->var[y]; });
-        int64_t start = 0;
-        for (int64_t p = 0; p < (int64_t)order.size(); ++p) {
-            const int64_t sl = order[p];
-            const int32_t lit = (int32_t)((f->var[sl] << 1) | (f->neg[sl] ? 1 : 0));
-            cl[sl] = (int32_t)(p << RES_LIT_BITS) | lit;
-            if (p + 1 == (int64_t)order.size() || f->var[order[p + 1]] != f->var[sl]) {
-                seg.push_back(make_int2((int)f->var[sl], (int)(start | ((p + 1) << 16))));
-                start = p + 1;
-            }
-        }
-        tc.push_back((int32_t)c);
-        tseg.push_back((int32_t)seg.size());
+int res_capacity(int R) { return R == 1 ? ResShape<1>::NL : (R == 2 ? ResShape<2>::NL : ResShape<4>::NL); }
+
+// Var-disjoint clause tiles (resident.hpp): clause c, in the reference's order, goes to the first
+// tile after the last tile holding any of its variables that still has room.  Returns the
+// internal order perm[k] = original clause and the tile starts, or false when the tiling is
+// degenerate (FUSED is then the better kernel).
+bool build_tiles(const odesat_cnf *f, int64_t n, int cap, std::vector<int32_t> &perm, std::vector<int32_t> &tc) {
+    const int64_t m = f->nclauses();
+    std::vector<int32_t> last((size_t)n, -1), tile_of((size_t)m), fill;
+    int32_t first_open = 0;  // every tile before it is full
+    for (int64_t c = 0; c < m; ++c) {
+        int32_t t = 0;
+        for (int64_t sl = f->clause_ptr[c]; sl < f->clause_ptr[c + 1]; ++sl) t = std::max(t, last[f->var[sl]] + 1);
+        t = std::max(t, first_open);
+        while (t < (int32_t)fill.size() && fill[t] >= cap) ++t;
+        if (t == (int32_t)fill.size()) fill.push_back(0);
+        fill[t] += 1;
+        while (first_open < (int32_t)fill.size() && fill[first_open] >= cap) ++first_open;
+        tile_of[c] = t;
+        for (int64_t sl = f->clause_ptr[c]; sl < f->clause_ptr[c + 1]; ++sl) last[f->var[sl]] = t;
     }
-    s->res_ntiles = (int)(tc.size() - 1);
-    s->res_ts = ts;
-    int rc;
-    if ((rc = dmalloc(s, (void **)&s->res_cl, cl.size() * 4))) return rc;
-    if ((rc = dmalloc(s, (void **)&s->res_tc, tc.size() * 4))) return rc;
-    if ((rc = dmalloc(s, (void **)&s->res_tseg, tseg.size() * 4))) return rc;
-    if ((rc = dmalloc(s, (void **)&s->res_seg, seg.size() * 8))) return rc;
-    if ((!cl.empty() && hipMemcpy(s->res_cl, cl.data(), cl.size() * 4, hipMemcpyHostToDevice) != hipSuccess) ||
-        hipMemcpy(s->res_tc, tc.data(), tc.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(s->res_tseg, tseg.data(), tseg.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-        (!seg.empty() && hipMemcpy(s->res_seg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice) != hipSuccess))
-        return fail(ODESAT_EDEVICE, "resident topology upload failed");
-    s->res_R = R;
-    return ODESAT_OK;
+    // a var-disjoint tile holds at most n slots and `cap` clauses: fall back to FUSED only when the
+    // tiling is far from that bound (e.g. one variable in every clause)
+    const int64_t nt = (int64_t)fill.size(), L = f->nliterals();
+    const int64_t bound = std::max<int64_t>((m + cap - 1) / cap, (L + n - 1) / n);
+    if (nt > 8 * bound + 16) return false;
+    tc.assign((size_t)nt + 1, 0);
+    for (int64_t t = 0; t < nt; ++t) tc[t + 1] = tc[t] + fill[t];
+    std::vector<int32_t> pos(tc.begin(), tc.end() - 1);
+    perm.assign((size_t)m, 0);
+    for (int64_t c = 0; c < m; ++c) perm[pos[tile_of[c]]++] = (int32_t)c;  // original order inside a tile
+    return true;
 }
 
 template <typename T, int R, bool ADA, bool K3> int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     static bool attr_set = false;  // per instantiation
-    const size_t lds = res_lds_bytes(s->n, R, s->res_ts, sizeof(T), ADA);
+    const size_t lds = res_lds_bytes(s->n, R, sizeof(T), ADA);
     if (!attr_set) {
         HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)RES_LDS_MAX));
@@ -430,7 +405,7 @@ template <typename T, int R, bool ADA, bool K3> int launch_resident_k(odesat_sol
     }
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_resident<T, R, ADA, K3>), dim3(s->G), dim3(RES_THREADS), lds, s->stream, a);
+        hipLaunchKernelGGL((k_resident<T, R, ADA, K3>), dim3(s->G), dim3(ResShape<R>::NTH), lds, s->stream, a);
     }
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
@@ -440,11 +415,10 @@ template <typename T>
 int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
                     int stop_mode) {
     RArgs<T> a{};
-    a.cl = s->res_cl;
+    a.cl4 = s->res_cl4;
     a.cptr = s->cptr;
+    a.lits = s->lits;
     a.tc = s->res_tc;
-    a.tseg = s->res_tseg;
-    a.seg = s->res_seg;
     a.v0 = (T *)s->v[0];
     a.v1 = (T *)s->v[1];
     a.c0 = (T *)s->c[0];
@@ -460,7 +434,6 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
     a.n = (int32_t)s->n;
     a.m = (int32_t)s->m;
     a.ntiles = s->res_ntiles;
-    a.ts = s->res_ts;
     a.step0 = step0;
     a.nsteps = nsteps;
     a.stop_mode = stop_mode;
@@ -506,12 +479,13 @@ int layout_t(odesat_solver *s, void *const pair[2], const double *dsrc, double *
     const size_t blocks = (total + threads - 1) / threads;
     const uint8_t *par = pair[1] ? s->par : nullptr;
     T *b1 = pair[1] ? (T *)pair[1] : (T *)pair[0];
+    const int32_t *imap = stride == 2 ? s->cmap : nullptr;  // clause arrays: caller order -> internal order
     if (scatter)
         hipLaunchKernelGGL((k_scatter<T>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, (T *)pair[0], b1, par,
-                           dsrc, (int)items, s->W, stride, comp, r0, count);
+                           dsrc, imap, (int)items, s->W, stride, comp, r0, count);
     else
         hipLaunchKernelGGL((k_gather<T>), dim3((unsigned)blocks), dim3(threads), 0, s->stream, ddst,
-                           (const T *)pair[0], (const T *)b1, par, (int)items, s->W, stride, comp, r0, count);
+                           (const T *)pair[0], (const T *)b1, par, imap, (int)items, s->W, stride, comp, r0, count);
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
 }
@@ -674,7 +648,7 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     for (auto e : s->pool) (void)hipEventDestroy(e);
     void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->pc, s->ps, s->empty, s->inc, s->v[0], s->v[1], s->c[0],
                     s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
-                    s->sat_step, s->steps_done, s->stop, s->res_cl, s->res_tc, s->res_tseg, s->res_seg};
+                    s->sat_step, s->steps_done, s->stop, s->res_tc, s->cmap, s->res_cl4};
     for (void *p : ptrs) dfree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
@@ -725,10 +699,9 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     // for FUSED (measured on MI355X, config 2: W = 64 beats 32 / 16 by 1.5-1.7x).
     // ODESAT_GROUP_WIDTH overrides (tuning; RESIDENT only if that width admits it).
     int lw = 1, res_r = 0;
-    if (res_tile_slots(n, s->uniform_k, 1, s->tsize) > 0) {
+    if (res_fits(n, 1, s->tsize, false)) {
         res_r = 1;
-        while (res_r < 4 && res_tile_slots(n, s->uniform_k, 2 * res_r, s->tsize) > 0 && batch >= 2 * res_r * 256)
-            res_r *= 2;
+        while (res_r < 4 && res_fits(n, 2 * res_r, s->tsize, false) && batch >= 2 * res_r * 256) res_r *= 2;
         lw = res_r;
     } else {
         while (lw < batch && lw < 64) lw <<= 1;
@@ -737,8 +710,19 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         const int want = std::atoi(ev);
         if (want == 1 || want == 2 || want == 4 || want == 8 || want == 16 || want == 32 || want == 64) {
             lw = want;
-            res_r = (want <= 4 && res_tile_slots(n, s->uniform_k, want, s->tsize) > 0) ? want : 0;
+            res_r = (want <= 4 && res_fits(n, want, s->tsize, false)) ? want : 0;
         }
+    }
+    // the internal clause order: var-disjoint tiles for RESIDENT, else the file order
+    std::vector<int32_t> perm, tiles;
+    if (res_r > 0 && !build_tiles(f, n, res_capacity(res_r), perm, tiles)) res_r = 0;
+    if (res_r == 0 && !std::getenv("ODESAT_GROUP_WIDTH")) {
+        lw = 1;
+        while (lw < batch && lw < 64) lw <<= 1;
+    }
+    if (res_r == 0) {
+        perm.resize(m);
+        for (int64_t c = 0; c < m; ++c) perm[c] = (int32_t)c;
     }
     s->LW = lw;
     s->VEC = 1;
@@ -755,24 +739,34 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "hipStreamCreate failed"));
 
-    // topology: clause CSR, packed literals, variable-major slot positions (sorted by slot, i.e.
-    // clause order then literal order: the reference's accumulation order) and their inverse
-    std::vector<int32_t> cptr(m + 1), lits(L), wpos(L), vptr(n + 1, 0), pc(L), ps(L), empty;
-    for (int64_t c = 0; c <= m; ++c) cptr[c] = (int32_t)f->clause_ptr[c];
-    for (int64_t s2 = 0; s2 < L; ++s2) {
-        lits[s2] = (int32_t)((f->var[s2] << 1) | (f->neg[s2] ? 1 : 0));
-        vptr[f->var[s2] + 1] += 1;
+    // topology, in the internal clause order (perm[k] = original clause; cmap is its inverse):
+    // clause CSR, packed literals, variable-major slot positions (sorted by ORIGINAL slot, i.e. the
+    // reference's clause-then-literal accumulation order) and their inverse
+    std::vector<int32_t> cptr(m + 1), lits(L), wpos(L), vptr(n + 1, 0), pc(L), ps(L), empty, cmap(m);
+    cptr[0] = 0;
+    for (int64_t k = 0; k < m; ++k) {
+        const int64_t c = perm[k];
+        cmap[c] = (int32_t)k;
+        const int64_t len = f->clause_ptr[c + 1] - f->clause_ptr[c];
+        cptr[k + 1] = cptr[k] + (int32_t)len;
+        for (int64_t j = 0; j < len; ++j) {
+            const int64_t so = f->clause_ptr[c] + j;
+            lits[cptr[k] + j] = (int32_t)((f->var[so] << 1) | (f->neg[so] ? 1 : 0));
+        }
+        if (len == 0) empty.push_back((int32_t)k);
     }
+    for (int64_t s2 = 0; s2 < L; ++s2) vptr[f->var[s2] + 1] += 1;
     for (int64_t i = 0; i < n; ++i) vptr[i + 1] += vptr[i];
     {
         std::vector<int32_t> fill(vptr.begin(), vptr.end() - 1);
-        for (int64_t c = 0; c < m; ++c) {
-            if (cptr[c] == cptr[c + 1]) empty.push_back((int32_t)c);
-            for (int32_t s2 = cptr[c]; s2 < cptr[c + 1]; ++s2) {
-                const int32_t p = fill[f->var[s2]]++;
-                wpos[s2] = p;
-                pc[p] = (int32_t)c;
-                ps[p] = s2;
+        for (int64_t c = 0; c < m; ++c) {  // original order
+            const int32_t k = cmap[c];
+            for (int64_t j = 0; j < f->clause_ptr[c + 1] - f->clause_ptr[c]; ++j) {
+                const int32_t p = fill[f->var[f->clause_ptr[c] + j]]++;
+                const int32_t si = cptr[k] + (int32_t)j;
+                wpos[si] = p;
+                pc[p] = k;
+                ps[p] = si;
             }
         }
     }
@@ -802,8 +796,20 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         (!inc.empty() && hipMemcpy(s->inc, inc.data(), inc.size() * 16, hipMemcpyHostToDevice) != hipSuccess) ||
         hipMemcpy(s->vptr, vptr.data(), (n + 1) * 4, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
+    if ((rc = dmalloc(s, (void **)&s->cmap, m * 4))) return bail(rc);
+    if (m && hipMemcpy(s->cmap, cmap.data(), m * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
     if (res_r > 0) {
-        if ((rc = build_resident(s, f, res_r, res_tile_slots(n, s->uniform_k, res_r, s->tsize)))) return bail(rc);
+        std::vector<int4> cl4(s->uniform_k == 3 ? m : 0);
+        for (size_t k = 0; k < cl4.size(); ++k) cl4[k] = make_int4(lits[3 * k], lits[3 * k + 1], lits[3 * k + 2], 0);
+        if ((rc = dmalloc(s, (void **)&s->res_tc, tiles.size() * 4))) return bail(rc);
+        if ((rc = dmalloc(s, (void **)&s->res_cl4, cl4.size() * 16))) return bail(rc);
+        if (hipMemcpy(s->res_tc, tiles.data(), tiles.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            (!cl4.empty() && hipMemcpy(s->res_cl4, cl4.data(), cl4.size() * 16, hipMemcpyHostToDevice) != hipSuccess))
+            return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
+        s->res_R = res_r;
+        s->res_ada = res_fits(n, res_r, s->tsize, true);
+        s->res_ntiles = (int)tiles.size() - 1;
         s->alg = ODESAT_ALG_RESIDENT;
     }
     // state (double-buffered)
@@ -1052,7 +1058,7 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
         if (adaptive && (rc = put_dt(s, nullptr, 0.01))) return rc;
     }
     const int poll = p->poll_interval > 0 ? p->poll_interval : 32;
-    if (s->alg == ODESAT_ALG_RESIDENT) return simulate_resident(s, p, adaptive, zeta, tol, poll, first_sat_step,
+    if (s->alg == ODESAT_ALG_RESIDENT && (!adaptive || s->res_ada)) return simulate_resident(s, p, adaptive, zeta, tol, poll, first_sat_step,
                                                                 steps_done, dt_out, steps_run);
     int32_t *h_stop = nullptr;
     uint8_t *h_act = nullptr;

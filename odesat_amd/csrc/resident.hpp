@@ -1,37 +1,38 @@
 // resident.hpp -- the LDS-resident persistent integrator (ALG_RESIDENT; included by odesat_hip.hip).
 //
-// One workgroup owns R replicas (the solver's group width W == R) for a whole launch of `nsteps`
-// Euler steps.  Its voltages v[n][R] live in LDS for the launch; per step only the clause memories
-// stream through HBM, read once and written once (in place), coalesced ([m][R][2] per group).
+// One workgroup owns R replicas (the solver's group width W == R) for a launch of `nsteps` Euler
+// steps.  Its voltages v[n][R] and derivative accumulators dv[n][R] live in LDS for the launch; per
+// step only the clause memories stream through HBM, read once and written once (in place),
+// coalesced.
 //
-// Per step the clauses are walked in tiles of consecutive clauses:
-//   clause phase  lane = (clause, replica): gather the clause's literal voltages from LDS, min /
-//                 second-min, C, the memories' update (system.rs:43-95), and each literal's
-//                 contribution G/R (:64-80) into a tile buffer w (LDS) at the slot's position in the
-//                 tile's variable-sorted order;
-//   fold          lane = (segment, replica): a segment is one variable's slots inside the tile; the
-//                 lane adds them, in order, to dv[var] (LDS).  Tiles are folded in clause order, so
-//                 every dv[i] is the reference's left fold over (clause, literal) -- bit-identical.
-// w is double-buffered: tile t+1's clause phase runs between the same two barriers as tile t's
-// fold.  After the last tile the variable phase applies :96 and resets dv.
-// Adaptive steps (system.rs:111-139) run two such passes per step: the first writes the full-step
-// and first-half memories to scratch, the second the second half in place plus max_error.
+// Clause tiles (built on the host): the clauses are stored in an internal order
+// made of tiles such that (1) no two clauses of one tile share a variable and (2) for every
+// variable, the tiles of its clauses increase in the reference's clause order.  A tile's lanes
+// (lane = (clause, replica)) can then add their contributions G/R (system.rs:64-80) straight into
+// dv[var] (LDS, no atomics, no contribution buffer): within a tile every dv[i] receives at most
+// one clause's terms (in literal order, by one lane), and tiles run in order with a barrier between
+// them, so every dv[i] is the reference's left fold over (clause, literal) -- bit-identical.
+// After the last tile the variable phase applies :96 and resets dv.  Adaptive steps
+// (system.rs:111-139) run two passes per step: the first writes the full-step and first-half
+// memories to scratch, the second the second half in place plus max_error.
 #pragma once
 
 #include "kernels.hpp"
 
 namespace odk {
 
-constexpr int RES_THREADS = 1024;
-constexpr int RES_LIT_BITS = 17;  // packed slot word: (tile-local position << 17) | literal
-constexpr int RES_LIT_MASK = (1 << RES_LIT_BITS) - 1;
+// Threads per workgroup: 512 for one replica (two workgroups share a CU), 1024 for R = 2, 4.
+template <int R> struct ResShape {
+    static constexpr int NTH = R == 1 ? 512 : 1024;
+    static constexpr int NL = NTH / R;  // clause lanes = tile capacity in clauses
+};
+constexpr int RES_DEPTH = 4;  // tiles in flight per lane (3-SAT register prefetch ring)
 
 template <typename T> struct RArgs {
-    const int32_t *__restrict__ cl;    // [L] packed slot words, clause-major (file order)
-    const int32_t *__restrict__ cptr;  // [m+1]
-    const int32_t *__restrict__ tc;    // [ntiles+1] first clause of each tile
-    const int32_t *__restrict__ tseg;  // [ntiles+1] first segment of each tile
-    const int2 *__restrict__ seg;      // [nseg] {var, start | end << 16} (tile-local positions)
+    const int4 *__restrict__ cl4;      // [m] 3-SAT: the clause's literals (var << 1 | neg), internal order
+    const int32_t *__restrict__ cptr;  // [m+1] internal clause -> first slot
+    const int32_t *__restrict__ lits;  // [L] literals by internal slot
+    const int32_t *__restrict__ tc;    // [ntiles+1] first internal clause of each tile
     T *v0, *v1, *c0, *c1;              // state buffers, group layout with W == R
     const uint8_t *par;
     T *cf, *ch;                        // adaptive scratch memories (full step, first half)
@@ -39,20 +40,10 @@ template <typename T> struct RArgs {
     uint8_t *act;
     int64_t *sat_step, *steps_done;
     int32_t *stop;
-    int32_t n, m, ntiles, ts;          // ts: slot capacity of one tile buffer
+    int32_t n, m, ntiles;
     int32_t step0, nsteps, stop_mode;
     T dt, zeta, xl_max;
     double tol;
-};
-
-// Everything one lane loads for one tile (3-SAT): its clause's packed slot words and memories,
-// and its (at most 3: a tile has <= 3 * NL segments) fold segments.
-constexpr int RES_SPL = 3;
-template <typename T> struct TileLoad {
-    int32_t w0, w1, w2;
-    Vec<T, 2> mem, full;
-    int2 sg[RES_SPL];
-    bool ok;
 };
 
 // Pass kinds: P_FIXED one fixed step in place; P_ADA1 full + first half candidates to scratch;
@@ -60,31 +51,29 @@ template <typename T> struct TileLoad {
 enum Pass : int { P_FIXED = 0, P_ADA1 = 1, P_ADA2 = 2 };
 
 template <typename T, int R> struct ResCtx {
-    T *vL, *dvL, *vfL, *wL;  // LDS
-    T *cf, *ch;              // this group's adaptive scratch memories
-    int r, lc;               // this lane's replica and clause-lane index
-    static constexpr int NL = RES_THREADS / R;
+    T *vL, *dvL, *vfL;  // LDS
+    T *cf, *ch;         // this group's adaptive scratch memories
+    int r, lc;          // this lane's replica and clause-lane index
+};
+
+// Everything one lane loads for one tile (3-SAT): its clause's literals and memories.
+template <typename T> struct TileLoad {
+    int4 lit;
+    Vec<T, 2> mem, full;
+    bool ok;
 };
 
 template <typename T, int R, int PK>
-__device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> &g, const T *CM, int t,
-                                          TileLoad<T> &x) {
-    constexpr int NL = ResCtx<T, R>::NL;
-    const int c = t * NL + g.lc;  // 3-SAT tiles are NL clauses wide
-    x.ok = c < a.m;
-    const int cc = x.ok ? c : t * NL;  // a valid clause of the tile (every tile is non-empty)
-    const int s0 = ldc(a.tseg, t), s1 = ldc(a.tseg, t + 1);
-#pragma unroll
-    for (int k = 0; k < RES_SPL; ++k) {
-        const int sidx = s0 + g.lc + k * NL;
-        x.sg[k] = sidx < s1 ? a.seg[sidx] : make_int2(0, 0);
-    }
-    x.w0 = a.cl[(size_t)cc * 3];
-    x.w1 = a.cl[(size_t)cc * 3 + 1];
-    x.w2 = a.cl[(size_t)cc * 3 + 2];
-    const size_t ci = ((size_t)cc * R + g.r) * 2;
-    x.mem = ldv<T, 2>((PK == P_ADA2 ? g.ch : CM) + ci);
-    if (PK == P_ADA2) x.full = ldv<T, 2>(g.cf + ci);
+__device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CM, int t,
+                                          TileLoad<T> &ld) {
+    const int c0 = ldc(a.tc, t);
+    const int c = c0 + x.lc;
+    ld.ok = c < ldc(a.tc, t + 1);
+    const int cc = ld.ok ? c : c0;  // a valid clause of the tile (tiles are non-empty)
+    ld.lit = a.cl4[cc];
+    const size_t ci = ((size_t)cc * R + x.r) * 2;
+    ld.mem = ldv<T, 2>((PK == P_ADA2 ? x.ch : CM) + ci);
+    if (PK == P_ADA2) ld.full = ldv<T, 2>(x.cf + ci);
 }
 
 // Memory update of one clause (system.rs:84-85, 94-95 / :124-132); returns the max_error terms.
@@ -122,21 +111,23 @@ __device__ __forceinline__ T res_mem_update(const RArgs<T> &a, const ResCtx<T, R
     return e;
 }
 
-// Clause phase of tile t (3-SAT) from prefetched loads.
+// One 3-SAT clause of tile t from its prefetched loads: C, the memories, and the three terms added
+// to dv (in literal order).
 template <typename T, int R, int PK>
 __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t,
-                                            const TileLoad<T> &ld, T *wbuf, bool on, T h, bool &uns, T &e) {
+                                            const TileLoad<T> &ld, bool on, T h, bool &uns, T &e) {
     if (!ld.ok) return;
     const T one = (T)1.0, halfc = (T)0.5;
-    const int c = t * ResCtx<T, R>::NL + x.lc;
-    const int w[3] = {ld.w0, ld.w1, ld.w2};
+    const int c = ldc(a.tc, t) + x.lc;
+    const int lit[3] = {ld.lit.x, ld.lit.y, ld.lit.z};
+    int idx[3];
     T v[3], q[3], val[3];
     T mn = inf_v<T>(), sec = inf_v<T>();
 #pragma unroll
     for (int j = 0; j < 3; ++j) {  // :43-57
-        const int lit = w[j] & RES_LIT_MASK;
-        q[j] = (lit & 1) ? (T)-1.0 : (T)1.0;
-        v[j] = x.vL[(lit >> 1) * R + x.r];
+        idx[j] = (lit[j] >> 1) * R + x.r;
+        q[j] = (lit[j] & 1) ? (T)-1.0 : (T)1.0;
+        v[j] = x.vL[idx[j]];
         val[j] = one - q[j] * v[j];
         minsec(val[j], mn, sec);
     }
@@ -144,128 +135,99 @@ __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R
     const T xs_m = ld.mem.e[0], xl_m = ld.mem.e[1];
     const T tt = xl_m * xs_m;
     const T tr = (one + a.zeta * xl_m) * (one - xs_m);
+    T d[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const T g_ = halfc * q[j] * (val[j] != mn ? mn : sec);                  // :64-70
         const T r_ = (C == one - q[j] * v[j]) ? halfc * (q[j] - v[j]) : (T)0.0;  // :73-77
-        wbuf[(w[j] >> RES_LIT_BITS) * R + x.r] = tt * g_ + tr * r_;            // :80 term
+        d[j] = tt * g_ + tr * r_;
     }
-    if (PK != P_ADA2) uns = uns || (on && !(C < (T)0.25));  // :88
-    const T ee = res_mem_update<T, R, PK>(a, x, CM, ((size_t)c * R + x.r) * 2, C, ld.mem, ld.full, on, h);
-    e = dmax(e, ee);
-}
-
-// Clause phase of tile t, any clause width (empty clauses included); no prefetch.
-template <typename T, int R, int PK>
-__device__ __forceinline__ void res_clause_any(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t, T *wbuf,
-                                               bool on, T h, bool &uns, T &e) {
-    const T one = (T)1.0, halfc = (T)0.5;
-    const int c1 = ldc(a.tc, t + 1);
-    for (int c = ldc(a.tc, t) + x.lc; c < c1; c += ResCtx<T, R>::NL) {
-        const int s0 = a.cptr[c], s1 = a.cptr[c + 1];
-        const size_t ci = ((size_t)c * R + x.r) * 2;
-        const Vec<T, 2> mem = ldv<T, 2>((PK == P_ADA2 ? x.ch : CM) + ci);
-        Vec<T, 2> full{};
-        if (PK == P_ADA2) full = ldv<T, 2>(x.cf + ci);
-        T mn = inf_v<T>(), sec = inf_v<T>();
-        for (int s = s0; s < s1; ++s) {
-            const int lit = a.cl[s] & RES_LIT_MASK;
-            const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
-            minsec(one - q * x.vL[(lit >> 1) * R + x.r], mn, sec);
-        }
-        const T C = halfc * mn;
-        const T tt = mem.e[1] * mem.e[0];
-        const T tr = (one + a.zeta * mem.e[1]) * (one - mem.e[0]);
-        for (int s = s0; s < s1; ++s) {
-            const int w = a.cl[s];
-            const int lit = w & RES_LIT_MASK;
-            const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
-            const T vi = x.vL[(lit >> 1) * R + x.r];
-            const T val = one - q * vi;
-            const T g_ = halfc * q * (val != mn ? mn : sec);
-            const T r_ = (C == one - q * vi) ? halfc * (q - vi) : (T)0.0;
-            wbuf[(w >> RES_LIT_BITS) * R + x.r] = tt * g_ + tr * r_;
-        }
-        if (PK != P_ADA2) uns = uns || (on && !(C < (T)0.25));
-        e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, ci, C, mem, full, on, h));
-    }
-}
-
-// One fold segment: the variable's slots of the tile, added in order to its dv.
-template <typename T, int R>
-__device__ __forceinline__ void res_fold_seg(const ResCtx<T, R> &x, int2 sg, const T *wbuf) {
-    const int start = sg.y & 0xFFFF, end = (int)((uint32_t)sg.y >> 16);
-    if (start >= end) return;
-    T d = x.dvL[sg.x * R + x.r];
-    for (int p = start; p < end; ++p) d += wbuf[p * R + x.r];
-    x.dvL[sg.x * R + x.r] = d;
-}
-
-// Fold of tile t (segments loaded here).
-template <typename T, int R>
-__device__ __forceinline__ void res_fold(const RArgs<T> &a, const ResCtx<T, R> &x, int t, const T *wbuf) {
-    const int s0 = ldc(a.tseg, t), s1 = ldc(a.tseg, t + 1);
-    for (int s = s0 + x.lc; s < s1; s += ResCtx<T, R>::NL) res_fold_seg<T, R>(x, a.seg[s], wbuf);
-}
-
-// One iteration of the 3-SAT tile pipeline: fold tile t-1 (slot P), clause phase of tile t (slot
-// Cc), refill slot P with tile t-1+RES_DEPTH, barrier.
-constexpr int RES_DEPTH = 4;
-template <typename T, int R, int PK>
-__device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t, TileLoad<T> &P,
-                                          const TileLoad<T> &Cc, bool on, T h, bool &uns, T &e) {
-    const int NT_ = a.ntiles;
-    if (t > NT_) return;  // uniform
-    T *w0 = x.wL, *w1 = x.wL + (size_t)a.ts * R;
-    if (t >= 1) {
-        const T *wb = ((t - 1) & 1) ? w1 : w0;
+    // :80 -- a clause may repeat a variable: same lane, literal order
 #pragma unroll
-        for (int k = 0; k < RES_SPL; ++k) res_fold_seg<T, R>(x, P.sg[k], wb);
+    for (int j = 0; j < 3; ++j) x.dvL[idx[j]] += d[j];
+    if (PK != P_ADA2) uns = uns || (on && !(C < (T)0.25));  // :88
+    e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, ((size_t)c * R + x.r) * 2, C, ld.mem, ld.full, on, h));
+}
+
+// Tile t, any clause width (empty clauses included); loads issued here.
+template <typename T, int R, int PK>
+__device__ __forceinline__ void res_clause_any(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t, bool on,
+                                               T h, bool &uns, T &e) {
+    const T one = (T)1.0, halfc = (T)0.5;
+    const int c = ldc(a.tc, t) + x.lc;
+    if (c >= ldc(a.tc, t + 1)) return;
+    const int s0 = a.cptr[c], s1 = a.cptr[c + 1];
+    const size_t ci = ((size_t)c * R + x.r) * 2;
+    const Vec<T, 2> mem = ldv<T, 2>((PK == P_ADA2 ? x.ch : CM) + ci);
+    Vec<T, 2> full{};
+    if (PK == P_ADA2) full = ldv<T, 2>(x.cf + ci);
+    T mn = inf_v<T>(), sec = inf_v<T>();
+    for (int s = s0; s < s1; ++s) {
+        const int lit = a.lits[s];
+        const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
+        minsec(one - q * x.vL[(lit >> 1) * R + x.r], mn, sec);
     }
-    if (t < NT_) res_clause3<T, R, PK>(a, x, CM, t, Cc, (t & 1) ? w1 : w0, on, h, uns, e);
-    if (t >= 1 && t - 1 + RES_DEPTH < NT_) res_load3<T, R, PK>(a, x, CM, t - 1 + RES_DEPTH, P);
+    const T C = halfc * mn;
+    const T tt = mem.e[1] * mem.e[0];
+    const T tr = (one + a.zeta * mem.e[1]) * (one - mem.e[0]);
+    for (int s = s0; s < s1; ++s) {
+        const int lit = a.lits[s];
+        const int idx = (lit >> 1) * R + x.r;
+        const T q = (lit & 1) ? (T)-1.0 : (T)1.0;
+        const T vi = x.vL[idx];
+        const T val = one - q * vi;
+        const T g_ = halfc * q * (val != mn ? mn : sec);
+        const T r_ = (C == one - q * vi) ? halfc * (q - vi) : (T)0.0;
+        x.dvL[idx] += tt * g_ + tr * r_;
+    }
+    if (PK != P_ADA2) uns = uns || (on && !(C < (T)0.25));
+    e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, ci, C, mem, full, on, h));
+}
+
+// One step of the 3-SAT tile pipeline: tile t from slot S, then S is refilled with tile
+// t + RES_DEPTH; barrier (the next tile may touch the same dv entries).
+template <typename T, int R, int PK>
+__device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t, TileLoad<T> &S,
+                                          bool on, T h, bool &uns, T &e) {
+    if (t >= a.ntiles) return;  // uniform
+    res_clause3<T, R, PK>(a, x, CM, t, S, on, h, uns, e);
+    if (t + RES_DEPTH < a.ntiles) res_load3<T, R, PK>(a, x, CM, t + RES_DEPTH, S);
     __syncthreads();
 }
 
 // One RHS pass over all tiles: dv (LDS) accumulates; memories are read from the pass's source and
-// written by kind.  Ends with a barrier (dv complete, w free).
+// written by kind.  Ends with a barrier (dv complete).
 template <typename T, int R, int PK, bool K3>
 __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, bool on, T h,
                                          bool &uns, T &e) {
     const int NT_ = a.ntiles;
-    if (NT_ == 0) {
-        __syncthreads();
-        return;
-    }
-    T *w0 = x.wL, *w1 = x.wL + (size_t)a.ts * R;
     if constexpr (K3) {
         static_assert(RES_DEPTH == 4, "the pipeline below is unrolled for 4 slots");
         TileLoad<T> b0, b1, b2, b3;
-        res_load3<T, R, PK>(a, x, CM, 0, b0);
+        if (0 < NT_) res_load3<T, R, PK>(a, x, CM, 0, b0);
         if (1 < NT_) res_load3<T, R, PK>(a, x, CM, 1, b1);
         if (2 < NT_) res_load3<T, R, PK>(a, x, CM, 2, b2);
         if (3 < NT_) res_load3<T, R, PK>(a, x, CM, 3, b3);
-        for (int t0 = 0; t0 <= NT_; t0 += 4) {
-            res_iter3<T, R, PK>(a, x, CM, t0, b3, b0, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CM, t0 + 1, b0, b1, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CM, t0 + 2, b1, b2, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CM, t0 + 3, b2, b3, on, h, uns, e);
+        for (int t0 = 0; t0 < NT_; t0 += 4) {
+            res_iter3<T, R, PK>(a, x, CM, t0, b0, on, h, uns, e);
+            res_iter3<T, R, PK>(a, x, CM, t0 + 1, b1, on, h, uns, e);
+            res_iter3<T, R, PK>(a, x, CM, t0 + 2, b2, on, h, uns, e);
+            res_iter3<T, R, PK>(a, x, CM, t0 + 3, b3, on, h, uns, e);
         }
     } else {
-        res_clause_any<T, R, PK>(a, x, CM, 0, w0, on, h, uns, e);
-        __syncthreads();
         for (int t = 0; t < NT_; ++t) {
-            res_fold<T, R>(a, x, t, (t & 1) ? w1 : w0);
-            if (t + 1 < NT_) res_clause_any<T, R, PK>(a, x, CM, t + 1, (t & 1) ? w0 : w1, on, h, uns, e);
+            res_clause_any<T, R, PK>(a, x, CM, t, on, h, uns, e);
             __syncthreads();
         }
     }
+    if (NT_ == 0) __syncthreads();
 }
 
 template <typename T, int R, bool ADAPTIVE, bool K3>
-__global__ __launch_bounds__(RES_THREADS) void k_resident(RArgs<T> a) {
+__global__ __launch_bounds__(ResShape<R>::NTH) void k_resident(RArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char res_smem[];
     using U = typename Bits<T>::U;
+    constexpr int NTH = ResShape<R>::NTH, NL = ResShape<R>::NL;
     __shared__ uint32_t unsL[R];
     __shared__ U errL[R];
     __shared__ T dtL[R];
@@ -273,7 +235,6 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(RArgs<T> a) {
     __shared__ int skipL;
     const int g = blockIdx.x;
     const int tid = threadIdx.x;
-    constexpr int NL = ResCtx<T, R>::NL;
     ResCtx<T, R> x;
     x.r = tid % R;
     x.lc = tid / R;
@@ -281,7 +242,6 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(RArgs<T> a) {
     x.vL = reinterpret_cast<T *>(res_smem);
     x.dvL = x.vL + nR;
     x.vfL = x.dvL + nR;
-    x.wL = ADAPTIVE ? x.vfL + nR : x.vfL;
     const bool p = a.par[g] != 0;
     T *V = (p ? a.v1 : a.v0) + (size_t)g * nR;
     T *CM = (p ? a.c1 : a.c0) + (size_t)g * a.m * R * 2;
@@ -308,7 +268,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(RArgs<T> a) {
 #pragma unroll
     for (int j = 0; j < R; ++j) any = any || actL[j] != 0;
     if (skipL || !any) return;  // uniform
-    for (size_t i = tid; i < nR; i += RES_THREADS) {
+    for (size_t i = tid; i < nR; i += NTH) {
         x.vL[i] = V[i];
         x.dvL[i] = (T)0.0;  // :33
     }
@@ -333,7 +293,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(RArgs<T> a) {
                 done += 1;
                 if (unsL[tid] == 0u) {  // allsat: the step was still taken (:148-152)
                     if (sat < 0) sat = step;
-                    if (a.stop_mode == ODESAT_STOP_EACH) act = 0;             // simulate() breaks (:193)
+                    if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                 // simulate() breaks (:193)
                     if (a.stop_mode == ODESAT_STOP_ANY) atomicMin(a.stop, step);  // simulate_inter (:291)
                 }
             }
@@ -349,7 +309,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(RArgs<T> a) {
                 x.dvL[idx] = (T)0.0;
                 if (st) {
                     const T v = x.vL[idx];
-                    x.vfL[idx] = dmin(dmax(v + h * d, (T)-1.0), (T)1.0);  // full-step clone
+                    x.vfL[idx] = dmin(dmax(v + h * d, (T)-1.0), (T)1.0);    // full-step clone
                     x.vL[idx] = dmin(dmax(v + half * d, (T)-1.0), (T)1.0);  // first half step
                 }
             }
@@ -397,7 +357,7 @@ __global__ __launch_bounds__(RES_THREADS) void k_resident(RArgs<T> a) {
         for (int j = 0; j < R; ++j) still = still || actL[j] != 0;
         if (!still) break;  // uniform
     }
-    for (size_t i = tid; i < nR; i += RES_THREADS) V[i] = x.vL[i];
+    for (size_t i = tid; i < nR; i += NTH) V[i] = x.vL[i];
     if (tid < R) {
         const int rg = g * R + tid;
         a.act[rg] = (uint8_t)act;

@@ -19,7 +19,8 @@ with Solver(f, B, os.environ.get("DTYPE", "f32")) as s:
     if CHUNK:
         s.set_chunk_replicas(CHUNK)
     s.set_schedule(SCHED)
-    s.set_algorithm(int(os.environ.get("ALG", "0")))
+    if "ALG" in os.environ:
+        s.set_algorithm(int(os.environ["ALG"]))
     s.init_state(42)
     s.simulate(dt=0.01, max_steps=K, stop=ODESAT_STOP_NONE)
     s.synchronize()

@@ -428,9 +428,9 @@ def test_default_layout_is_resident_for_config2():
     var, neg = wl.random_ksat(c["n"], c["m"], 3, c["seed"])
     cp, v_, n_ = wl.formula_arrays(var, neg)
     f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
-    for prec, alg in (("f32", _lib.ODESAT_ALG_RESIDENT), ("f64", _lib.ODESAT_ALG_FUSED)):
+    for prec in ("f32", "f64"):  # f64: v and dv (160,000 B) fit; adaptive steps then run FUSED
         with Solver(f, 1024, prec) as s:
-            assert s.algorithm == alg
+            assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.group_width in (1, 2)
 
 
 def test_frozen_replicas_keep_state_across_buffer_flips():
