@@ -694,15 +694,14 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         if (f->clause_ptr[c + 1] - f->clause_ptr[c] != s->uniform_k) s->uniform_k = 0;
     if (s->uniform_k != 3) s->uniform_k = 0;  // the specialised kernels are instantiated for 3-SAT
     // layout.  When the voltages of a replica fit in LDS, the group width is the
-    // RESIDENT kernel's replicas per workgroup R (1, 2 or 4: as many as fit while there are still
-    // >= 256 workgroups) and RESIDENT is the default.  Otherwise W = min(next pow2 >= batch, 64)
+    // RESIDENT kernel's replicas per workgroup R = 1 (2 and 4 via ODESAT_GROUP_WIDTH) and RESIDENT is
+    // the default.  Otherwise W = min(next pow2 >= batch, 64)
     // for FUSED (measured on MI355X, config 2: W = 64 beats 32 / 16 by 1.5-1.7x).
     // ODESAT_GROUP_WIDTH overrides (tuning; RESIDENT only if that width admits it).
     int lw = 1, res_r = 0;
-    if (res_fits(n, 1, s->tsize, false)) {
+    if (res_fits(n, 1, s->tsize, false)) {  // measured (config 2, B = 1024): R = 1 beats R = 2 by 1.13x
         res_r = 1;
-        while (res_r < 4 && res_fits(n, 2 * res_r, s->tsize, false) && batch >= 2 * res_r * 256) res_r *= 2;
-        lw = res_r;
+        lw = 1;
     } else {
         while (lw < batch && lw < 64) lw <<= 1;
     }
@@ -800,6 +799,8 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     if (m && hipMemcpy(s->cmap, cmap.data(), m * 4, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
     if (res_r > 0) {
+        if (s->uniform_k == 3)  // the 3-SAT pipeline is unrolled by 4: pad with empty tiles
+            while ((tiles.size() - 1) % 4 != 0) tiles.push_back(tiles.back());
         std::vector<int4> cl4(s->uniform_k == 3 ? m : 0);
         for (size_t k = 0; k < cl4.size(); ++k) cl4[k] = make_int4(lits[3 * k], lits[3 * k + 1], lits[3 * k + 2], 0);
         if ((rc = dmalloc(s, (void **)&s->res_tc, tiles.size() * 4))) return bail(rc);

@@ -63,13 +63,16 @@ template <typename T> struct TileLoad {
     bool ok;
 };
 
+// Loads of tile t (t >= ntiles: nothing to do, a valid address is read).  Unconditional, so the
+// ring's loads stay in flight across iterations (no control flow for the wait counters to merge).
 template <typename T, int R, int PK>
 __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CM, int t,
                                           TileLoad<T> &ld) {
-    const int c0 = ldc(a.tc, t);
+    const int tt = min(t, a.ntiles - 1);
+    const int c0 = ldc(a.tc, tt), c1 = ldc(a.tc, tt + 1);
     const int c = c0 + x.lc;
-    ld.ok = c < ldc(a.tc, t + 1);
-    const int cc = ld.ok ? c : c0;  // a valid clause of the tile (tiles are non-empty)
+    ld.ok = t < a.ntiles && c < c1;
+    const int cc = c < c1 ? c : (c1 > 0 ? c1 - 1 : 0);  // a valid clause
     ld.lit = a.cl4[cc];
     const size_t ci = ((size_t)cc * R + x.r) * 2;
     ld.mem = ldv<T, 2>((PK == P_ADA2 ? x.ch : CM) + ci);
@@ -111,23 +114,31 @@ __device__ __forceinline__ T res_mem_update(const RArgs<T> &a, const ResCtx<T, R
     return e;
 }
 
-// One 3-SAT clause of tile t from its prefetched loads: C, the memories, and the three terms added
-// to dv (in literal order).
+// A clause's three dv terms, computed ahead of the barrier that orders their application.
+template <typename T> struct Pend {
+    int idx[3];
+    T d[3];
+    bool ok;
+};
+
+// One 3-SAT clause of tile t from its prefetched loads: C, the memories' update and the three dv
+// terms (system.rs:43-88).  Voltages are read-only during a pass, so this runs one tile ahead of
+// the dv updates.
 template <typename T, int R, int PK>
 __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t,
-                                            const TileLoad<T> &ld, bool on, T h, bool &uns, T &e) {
+                                            const TileLoad<T> &ld, Pend<T> &P, bool on, T h, bool &uns, T &e) {
+    P.ok = ld.ok;
     if (!ld.ok) return;
     const T one = (T)1.0, halfc = (T)0.5;
     const int c = ldc(a.tc, t) + x.lc;
     const int lit[3] = {ld.lit.x, ld.lit.y, ld.lit.z};
-    int idx[3];
     T v[3], q[3], val[3];
     T mn = inf_v<T>(), sec = inf_v<T>();
 #pragma unroll
     for (int j = 0; j < 3; ++j) {  // :43-57
-        idx[j] = (lit[j] >> 1) * R + x.r;
+        P.idx[j] = (lit[j] >> 1) * R + x.r;
         q[j] = (lit[j] & 1) ? (T)-1.0 : (T)1.0;
-        v[j] = x.vL[idx[j]];
+        v[j] = x.vL[P.idx[j]];
         val[j] = one - q[j] * v[j];
         minsec(val[j], mn, sec);
     }
@@ -135,18 +146,28 @@ __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R
     const T xs_m = ld.mem.e[0], xl_m = ld.mem.e[1];
     const T tt = xl_m * xs_m;
     const T tr = (one + a.zeta * xl_m) * (one - xs_m);
-    T d[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
         const T g_ = halfc * q[j] * (val[j] != mn ? mn : sec);                  // :64-70
         const T r_ = (C == one - q[j] * v[j]) ? halfc * (q[j] - v[j]) : (T)0.0;  // :73-77
-        d[j] = tt * g_ + tr * r_;
+        P.d[j] = tt * g_ + tr * r_;
     }
-    // :80 -- a clause may repeat a variable: same lane, literal order
-#pragma unroll
-    for (int j = 0; j < 3; ++j) x.dvL[idx[j]] += d[j];
     if (PK != P_ADA2) uns = uns || (on && !(C < (T)0.25));  // :88
     e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, ((size_t)c * R + x.r) * 2, C, ld.mem, ld.full, on, h));
+}
+
+// :80 for one clause: dv[i_j] += d_j for j = 0, 1, 2 in order.  The three reads are issued
+// together; a variable repeated inside the clause takes the running value, as the sequential
+// updates would.
+template <typename T, int R> __device__ __forceinline__ void res_apply3(const ResCtx<T, R> &x, const Pend<T> &P) {
+    if (!P.ok) return;
+    const T o0 = x.dvL[P.idx[0]], o1 = x.dvL[P.idx[1]], o2 = x.dvL[P.idx[2]];
+    const T a0 = o0 + P.d[0];
+    const T a1 = (P.idx[1] == P.idx[0] ? a0 : o1) + P.d[1];
+    const T a2 = (P.idx[2] == P.idx[1] ? a1 : (P.idx[2] == P.idx[0] ? a0 : o2)) + P.d[2];
+    x.dvL[P.idx[0]] = a0;
+    x.dvL[P.idx[1]] = a1;
+    x.dvL[P.idx[2]] = a2;
 }
 
 // Tile t, any clause width (empty clauses included); loads issued here.
@@ -184,15 +205,18 @@ __device__ __forceinline__ void res_clause_any(const RArgs<T> &a, const ResCtx<T
     e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, ci, C, mem, full, on, h));
 }
 
-// One step of the 3-SAT tile pipeline: tile t from slot S, then S is refilled with tile
-// t + RES_DEPTH; barrier (the next tile may touch the same dv entries).
+// One step of the 3-SAT tile pipeline: the terms of tile t+1 are computed from slot S (which is
+// then refilled with tile t+1+RES_DEPTH), tile t's terms P are applied to dv, barrier (tile t+1
+// may touch the same dv entries).
 template <typename T, int R, int PK>
 __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t, TileLoad<T> &S,
-                                          bool on, T h, bool &uns, T &e) {
-    if (t >= a.ntiles) return;  // uniform
-    res_clause3<T, R, PK>(a, x, CM, t, S, on, h, uns, e);
-    if (t + RES_DEPTH < a.ntiles) res_load3<T, R, PK>(a, x, CM, t + RES_DEPTH, S);
+                                          Pend<T> &P, bool on, T h, bool &uns, T &e) {
+    Pend<T> Q;
+    res_clause3<T, R, PK>(a, x, CM, t + 1, S, Q, on, h, uns, e);  // Q.ok = false past the last tile
+    res_apply3<T, R>(x, P);
+    res_load3<T, R, PK>(a, x, CM, t + 1 + RES_DEPTH, S);
     __syncthreads();
+    P = Q;
 }
 
 // One RHS pass over all tiles: dv (LDS) accumulates; memories are read from the pass's source and
@@ -203,16 +227,25 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
     const int NT_ = a.ntiles;
     if constexpr (K3) {
         static_assert(RES_DEPTH == 4, "the pipeline below is unrolled for 4 slots");
+        // the host pads 3-SAT tilings to a multiple of 4 tiles (empty tiles), so the unrolled loop
+        // below runs whole
+        if (NT_ == 0) {
+            __syncthreads();
+            return;
+        }
         TileLoad<T> b0, b1, b2, b3;
-        if (0 < NT_) res_load3<T, R, PK>(a, x, CM, 0, b0);
-        if (1 < NT_) res_load3<T, R, PK>(a, x, CM, 1, b1);
-        if (2 < NT_) res_load3<T, R, PK>(a, x, CM, 2, b2);
-        if (3 < NT_) res_load3<T, R, PK>(a, x, CM, 3, b3);
-        for (int t0 = 0; t0 < NT_; t0 += 4) {
-            res_iter3<T, R, PK>(a, x, CM, t0, b0, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CM, t0 + 1, b1, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CM, t0 + 2, b2, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CM, t0 + 3, b3, on, h, uns, e);
+        Pend<T> P;
+        res_load3<T, R, PK>(a, x, CM, 0, b0);
+        res_load3<T, R, PK>(a, x, CM, 1, b1);
+        res_load3<T, R, PK>(a, x, CM, 2, b2);
+        res_load3<T, R, PK>(a, x, CM, 3, b3);
+        res_clause3<T, R, PK>(a, x, CM, 0, b0, P, on, h, uns, e);
+        res_load3<T, R, PK>(a, x, CM, RES_DEPTH, b0);
+        for (int t0 = 0; t0 < NT_; t0 += 4) {  // iteration t computes tile t+1 from slot (t+1) % 4
+            res_iter3<T, R, PK>(a, x, CM, t0, b1, P, on, h, uns, e);
+            res_iter3<T, R, PK>(a, x, CM, t0 + 1, b2, P, on, h, uns, e);
+            res_iter3<T, R, PK>(a, x, CM, t0 + 2, b3, P, on, h, uns, e);
+            res_iter3<T, R, PK>(a, x, CM, t0 + 3, b0, P, on, h, uns, e);
         }
     } else {
         for (int t = 0; t < NT_; ++t) {
@@ -220,7 +253,7 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
             __syncthreads();
         }
     }
-    if (NT_ == 0) __syncthreads();
+    if (!K3 && NT_ == 0) __syncthreads();
 }
 
 template <typename T, int R, bool ADAPTIVE, bool K3>

@@ -430,7 +430,7 @@ def test_default_layout_is_resident_for_config2():
     f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
     for prec in ("f32", "f64"):  # f64: v and dv (160,000 B) fit; adaptive steps then run FUSED
         with Solver(f, 1024, prec) as s:
-            assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.group_width in (1, 2)
+            assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.group_width == 1
 
 
 def test_frozen_replicas_keep_state_across_buffer_flips():
