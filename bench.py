@@ -35,7 +35,8 @@ def parse():
     p.add_argument("--cpu-replicas", type=int, default=16)
     p.add_argument("--cpu-steps", type=int, default=300)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--traffic", default=None, help="JSON with per-launch HBM bytes from the PMC passes")
+    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
+                   help="JSON with the dominant kernel's HBM bytes per step from the PMC passes (profiles/)")
     p.add_argument("--extra-batch", type=int, default=256, help="also time this B (configs[1]); 0 = off")
     return p.parse_args()
 
@@ -77,14 +78,17 @@ def max_over_ranks(dist, x, local):
     return float(t.item())
 
 
+STEPS_PER_LAUNCH = 20  # persistent kernel: steps per launch (warmup and timed launches alike)
+
+
 def time_gpu(solver, steps, warmup, dist, local, profile):
     from odesat_amd.system import ODESAT_STOP_NONE
     if warmup:
-        solver.simulate(dt=0.01, max_steps=warmup, stop=ODESAT_STOP_NONE)
+        solver.simulate(dt=0.01, max_steps=warmup, stop=ODESAT_STOP_NONE, poll_interval=STEPS_PER_LAUNCH)
     solver.profile(profile)
     barrier_sync(dist, solver, local)
     t0 = time.perf_counter()
-    solver.simulate(dt=0.01, max_steps=steps, stop=ODESAT_STOP_NONE)
+    solver.simulate(dt=0.01, max_steps=steps, stop=ODESAT_STOP_NONE, poll_interval=STEPS_PER_LAUNCH)
     barrier_sync(dist, solver, local)
     t1 = time.perf_counter()
     ms, launches = solver.profile_read() if profile else (None, None)
@@ -133,30 +137,40 @@ def main():
         s.init_state(42, replica0=rank * batch)
         wall, ms, launches = time_gpu(s, args.steps, args.warmup, dist, local, profile)
         bytes_step = s.clause_kernel_bytes()
+        alg = s.algorithm
         s.close()
-        return wall, ms, launches, bytes_step
+        return wall, ms, launches, bytes_step, alg
 
-    wall, ms, launches, clause_bytes_step = run_batch(B, True)
+    wall, ms, launches, clause_bytes_step, alg = run_batch(B, True)
     wall_max = max_over_ranks(dist, wall, local)
     total_replica_steps = B * world * args.steps
     value = total_replica_steps / wall_max
     ms_per_step = wall_max * 1e3 / args.steps
 
-    # roofline of the dominant kernel (k_step): algorithmic bytes per launch / mean launch time
+    # roofline of the dominant kernel: algorithmic bytes per launch ((8n + 16m) B per
+    # fp32 replica-step x the replica-steps of one launch) / its mean launch time (HIP events on the
+    # solver's stream)
+    from odesat_amd._lib import ODESAT_ALG_RESIDENT
+    kernel = ("k_resident (persistent, LDS-resident voltages, var-disjoint clause tiles)" if alg == ODESAT_ALG_RESIDENT
+              else "k_step (fused RHS + Euler update, variable-major)")
     nlaunch = int(launches[0])
     per_launch_s = ms[0] / 1e3 / nlaunch
-    per_launch_bytes = clause_bytes_step * args.steps / nlaunch
+    steps_per_launch = args.steps / nlaunch
+    per_launch_bytes = clause_bytes_step * steps_per_launch
     achieved = per_launch_bytes / per_launch_s / 1e9
     traffic = None
     if args.traffic and os.path.exists(args.traffic):
         with open(args.traffic) as fh:
-            traffic = json.load(fh).get("clause_kernel_hbm_bytes_per_launch")
+            tj = json.load(fh)
+        if tj.get("kernel", "").split(" ")[0] == kernel.split(" ")[0] and tj.get("batch") == B \
+                and tj.get("dtype") == args.dtype and tj.get("config") == args.config:
+            traffic = tj["hbm_bytes_per_step"] * steps_per_launch  # PMC-measured, same kernel and workload
     tsize = 4 if args.dtype == "f32" else 8
     step_bytes = B * (2 * n + 4 * m) * tsize  # algorithmic per GPU-step: v, xs, xl read + written once
 
     extra = None
     if args.extra_batch and args.extra_batch != B:
-        w2, _, _, _ = run_batch(args.extra_batch, False)
+        w2 = run_batch(args.extra_batch, False)[0]
         w2 = max_over_ranks(dist, w2, local)
         extra = {"batch_per_gpu": args.extra_batch,
                  "value": args.extra_batch * world * args.steps / w2,
@@ -184,7 +198,7 @@ def main():
                                    f"Euler dt=0.01, all replicas stepped (no early exit)",
                        "global_batch": B * world, "batch_per_gpu": B, "n": n, "m": m,
                        "parallelism": f"replica-sharded x{world} (no collectives)"},
-            "roofline": {"bound": "hbm", "kernel": "k_step (fused RHS + Euler update, variable-major)",
+            "roofline": {"bound": "hbm", "kernel": kernel,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": per_launch_bytes,

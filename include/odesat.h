@@ -126,7 +126,8 @@ typedef struct {
     double dt;             /* fixed step size; adaptive starts every replica at 0.01 (:205) */
     double zeta;           /* learning rate; < 0 = density heuristic (system.rs:164-173) */
     int64_t max_steps;     /* > 0 (the reference's None = unbounded is refused) */
-    int32_t poll_interval; /* steps between host polls of the stop condition (0 = default 32) */
+    int32_t poll_interval; /* steps between host polls of the stop condition (0 = default 32); with
+                              ODESAT_ALG_RESIDENT also the steps per kernel launch (STOP_ANY: 1) */
     int32_t reserved;
 } odesat_params;
 

@@ -1013,7 +1013,8 @@ static int simulate_resident(odesat_solver *s, const odesat_params *p, bool adap
                              int poll, int64_t *first_sat_step, int64_t *steps_done, double *dt_out,
                              int64_t *steps_run) {
     int rc = ODESAT_OK;
-    const int per_launch = p->stop == ODESAT_STOP_ANY ? 1 : (p->stop == ODESAT_STOP_EACH ? poll : 64);
+    // launches of `poll` steps (STOP_ANY: 1, so no replica runs past the stop step)
+    const int per_launch = p->stop == ODESAT_STOP_ANY ? 1 : poll;
     int32_t h_stop = INT_MAX;
     std::vector<uint8_t> h_act(s->Bp);
     int64_t t = 0;

@@ -161,6 +161,7 @@ __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R
 // updates would.
 template <typename T, int R> __device__ __forceinline__ void res_apply3(const ResCtx<T, R> &x, const Pend<T> &P) {
     if (!P.ok) return;
+    // (ds_add_f32 instead of this read-modify-write measured 4.3x slower on MI355X)
     const T o0 = x.dvL[P.idx[0]], o1 = x.dvL[P.idx[1]], o2 = x.dvL[P.idx[2]];
     const T a0 = o0 + P.d[0];
     const T a1 = (P.idx[1] == P.idx[0] ? a0 : o1) + P.d[1];

@@ -29,6 +29,6 @@ if [ "${SKIP_PROF:-0}" != 1 ]; then
     export TMPDIR=/tmp
     cd /tmp
     step rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$TAG" -o run --output-format csv -- \
-        python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu --extra-batch 0 || exit $?
+        python3 "$ROOT/bench.py" --no-cpu --extra-batch 0 || exit $?
     find "$OUT/prof_$TAG" -name '*stats*' | head
 fi
