@@ -49,7 +49,9 @@ def dist_setup(args):
     if world > 1:
         import torch
         import torch.distributed as td
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # RCCL ("nccl") on GPU boxes; ODESAT_DIST_BACKEND=gloo rehearses N ranks on one GPU (RCCL
+        # refuses two ranks on one device).  Only host scalars cross ranks (odesat_amd/sharding.py).
+        backend = os.environ.get("ODESAT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         td.init_process_group(backend=backend)
@@ -66,16 +68,6 @@ def barrier_sync(dist, solver, local):
         if torch.cuda.is_available():
             torch.cuda.synchronize(local)
         dist.barrier()
-
-
-def max_over_ranks(dist, x, local):
-    if dist is None:
-        return x
-    import torch
-    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
 
 
 STEPS_PER_LAUNCH = 20  # persistent kernel: steps per launch (warmup and timed launches alike)
@@ -120,6 +112,7 @@ def main():
 
     from odesat_amd import cnf
     from odesat_amd import workloads as wl
+    from odesat_amd.sharding import max_over_ranks, shard_range
     from odesat_amd.system import Solver
 
     c = wl.CONFIGS[args.config]
@@ -134,7 +127,7 @@ def main():
         s = Solver(f, batch, args.dtype, device=local % max(1, device_count()))
         if args.chunk:
             s.set_chunk_replicas(args.chunk)
-        s.init_state(42, replica0=rank * batch)
+        s.init_state(42, replica0=shard_range(rank, world, batch)[0])
         wall, ms, launches = time_gpu(s, args.steps, args.warmup, dist, local, profile)
         bytes_step = s.clause_kernel_bytes()
         alg = s.algorithm
@@ -142,7 +135,7 @@ def main():
         return wall, ms, launches, bytes_step, alg
 
     wall, ms, launches, clause_bytes_step, alg = run_batch(B, True)
-    wall_max = max_over_ranks(dist, wall, local)
+    wall_max = max_over_ranks(dist, wall)
     total_replica_steps = B * world * args.steps
     value = total_replica_steps / wall_max
     ms_per_step = wall_max * 1e3 / args.steps
@@ -171,7 +164,7 @@ def main():
     extra = None
     if args.extra_batch and args.extra_batch != B:
         w2 = run_batch(args.extra_batch, False)[0]
-        w2 = max_over_ranks(dist, w2, local)
+        w2 = max_over_ranks(dist, w2)
         extra = {"batch_per_gpu": args.extra_batch,
                  "value": args.extra_batch * world * args.steps / w2,
                  "ms_per_step": w2 * 1e3 / args.steps}
