@@ -61,7 +61,7 @@ struct odesat_solver {
     bool res_ada = false; // adaptive steps fit in LDS too (else they run FUSED on the same layout)
     int res_ntiles = 0;
     int32_t *res_tc = nullptr, *cmap = nullptr;
-    int4 *res_cl4 = nullptr;
+    int4 *res_cl4 = nullptr;  // [m] literals of internal clause k (3-SAT)
     int64_t bytes = 0;
     // profiling
     bool profile = false;
@@ -367,7 +367,81 @@ int res_capacity(int R) { return R == 1 ? ResShape<1>::NL : (R == 2 ? ResShape<2
 // tile after the last tile holding any of its variables that still has room.  Returns the
 // internal order perm[k] = original clause and the tile starts, or false when the tiling is
 // degenerate (FUSED is then the better kernel).
-bool build_tiles(const odesat_cnf *f, int64_t n, int cap, std::vector<int32_t> &perm, std::vector<int32_t> &tc) {
+// the 6 orders of a 3-literal clause: internal slot q holds original literal kP3[code][q]
+constexpr int kP3[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
+
+// LDS bank layout of one tile (3-SAT).  A 32-lane half-wave is serviced per LDS cycle and a lane's
+// voltage of variable v sits in bank (v*R + r) mod 32, so GS = 32 / R clauses share a half-wave and
+// key(v) = v mod GS decides conflicts.  Clauses are dealt to half-wave groups so each group holds
+// each key at most ~3 times, then each clause's 3 literals are ordered (min / second-min and the
+// G/R terms do not depend on the order of 3 distinct variables) so that each of the 3 gather
+// instructions sees distinct keys.  The dv read-modify-write uses the same addresses + a constant.
+void bank_layout(const odesat_cnf *f, int R, std::vector<int32_t> &cl, std::vector<uint8_t> &code) {
+    const int GS = 32 / R;
+    const int64_t s = (int64_t)cl.size();
+    if (s == 0) return;
+    const int64_t G = (s + GS - 1) / GS;
+    std::vector<int> cap((size_t)G, GS), cnt((size_t)G * GS, 0);
+    cap[G - 1] = (int)(s - (G - 1) * GS);  // every group but the last is full: groups stay aligned
+    std::vector<std::vector<int32_t>> grp((size_t)G);
+    auto key = [&](int32_t c, int j) { return (int)(f->var[f->clause_ptr[c] + j] % GS); };
+    for (int32_t c : cl) {
+        int64_t best = -1;
+        long score = LONG_MAX;
+        for (int64_t g = 0; g < G; ++g) {
+            if ((int)grp[g].size() >= cap[g]) continue;
+            int mx = 0, sum = 0;
+            for (int j = 0; j < 3; ++j) {
+                const int k = cnt[g * GS + key(c, j)];
+                mx = std::max(mx, k);
+                sum += k;
+            }
+            const long sc = (long)mx * 1000000 + (long)sum * 1000 + (long)grp[g].size();
+            if (sc < score) { score = sc; best = g; }
+        }
+        grp[best].push_back(c);
+        for (int j = 0; j < 3; ++j) cnt[best * GS + key(c, j)] += 1;
+    }
+    cl.clear();
+    std::vector<int> ic(3 * (size_t)GS);
+    for (int64_t g = 0; g < G; ++g) {
+        std::fill(ic.begin(), ic.end(), 0);
+        std::vector<int> pc(grp[g].size(), 0);
+        auto distinct = [&](int32_t c) {
+            const int64_t b = f->clause_ptr[c];
+            return f->var[b] != f->var[b + 1] && f->var[b] != f->var[b + 2] && f->var[b + 1] != f->var[b + 2];
+        };
+        auto place = [&](size_t i, int sign) {
+            for (int q = 0; q < 3; ++q) ic[q * GS + key(grp[g][i], kP3[pc[i]][q])] += sign;
+        };
+        for (int pass = 0; pass < 3; ++pass) {
+            for (size_t i = 0; i < grp[g].size(); ++i) {
+                if (pass > 0) place(i, -1);
+                int bestp = 0;
+                long bs = LONG_MAX;
+                for (int pp = 0; pp < (distinct(grp[g][i]) ? 6 : 1); ++pp) {
+                    int mx = 0, sum = 0;
+                    for (int q = 0; q < 3; ++q) {
+                        const int k = ic[q * GS + key(grp[g][i], kP3[pp][q])];
+                        mx = std::max(mx, k);
+                        sum += k;
+                    }
+                    const long sc = (long)mx * 1000 + sum;
+                    if (sc < bs) { bs = sc; bestp = pp; }
+                }
+                pc[i] = bestp;
+                place(i, +1);
+            }
+        }
+        for (size_t i = 0; i < grp[g].size(); ++i) {
+            cl.push_back(grp[g][i]);
+            code[grp[g][i]] = (uint8_t)pc[i];
+        }
+    }
+}
+
+bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, std::vector<int32_t> &perm,
+                 std::vector<int32_t> &tc, std::vector<uint8_t> &code) {
     const int64_t m = f->nclauses();
     std::vector<int32_t> last((size_t)n, -1), tile_of((size_t)m), fill;
     int32_t first_open = 0;  // every tile before it is full
@@ -392,6 +466,17 @@ bool build_tiles(const odesat_cnf *f, int64_t n, int cap, std::vector<int32_t> &
     std::vector<int32_t> pos(tc.begin(), tc.end() - 1);
     perm.assign((size_t)m, 0);
     for (int64_t c = 0; c < m; ++c) perm[pos[tile_of[c]]++] = (int32_t)c;  // original order inside a tile
+    code.assign((size_t)m, 0);  // indexed by ORIGINAL clause here; remapped below
+    if (k3) {
+        for (int64_t t = 0; t < nt; ++t) {
+            std::vector<int32_t> cl(perm.begin() + tc[t], perm.begin() + tc[t + 1]);
+            bank_layout(f, R, cl, code);
+            std::copy(cl.begin(), cl.end(), perm.begin() + tc[t]);
+        }
+    }
+    std::vector<uint8_t> by_internal((size_t)m);
+    for (int64_t k = 0; k < m; ++k) by_internal[k] = code[perm[k]];
+    code.swap(by_internal);
     return true;
 }
 
@@ -714,7 +799,8 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     }
     // the internal clause order: var-disjoint tiles for RESIDENT, else the file order
     std::vector<int32_t> perm, tiles;
-    if (res_r > 0 && !build_tiles(f, n, res_capacity(res_r), perm, tiles)) res_r = 0;
+    std::vector<uint8_t> lorder;  // per internal clause: literal order code (kP3), 0 = file order
+    if (res_r > 0 && !build_tiles(f, n, res_capacity(res_r), res_r, s->uniform_k == 3, perm, tiles, lorder)) res_r = 0;
     if (res_r == 0 && !std::getenv("ODESAT_GROUP_WIDTH")) {
         lw = 1;
         while (lw < batch && lw < 64) lw <<= 1;
@@ -722,6 +808,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     if (res_r == 0) {
         perm.resize(m);
         for (int64_t c = 0; c < m; ++c) perm[c] = (int32_t)c;
+        lorder.assign(m, 0);
     }
     s->LW = lw;
     s->VEC = 1;
@@ -748,9 +835,10 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         cmap[c] = (int32_t)k;
         const int64_t len = f->clause_ptr[c + 1] - f->clause_ptr[c];
         cptr[k + 1] = cptr[k] + (int32_t)len;
-        for (int64_t j = 0; j < len; ++j) {
+        for (int64_t q = 0; q < len; ++q) {  // internal slot q holds original literal j
+            const int64_t j = len == 3 ? kP3[lorder[k]][q] : q;
             const int64_t so = f->clause_ptr[c] + j;
-            lits[cptr[k] + j] = (int32_t)((f->var[so] << 1) | (f->neg[so] ? 1 : 0));
+            lits[cptr[k] + q] = (int32_t)((f->var[so] << 1) | (f->neg[so] ? 1 : 0));
         }
         if (len == 0) empty.push_back((int32_t)k);
     }
@@ -760,9 +848,14 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         std::vector<int32_t> fill(vptr.begin(), vptr.end() - 1);
         for (int64_t c = 0; c < m; ++c) {  // original order
             const int32_t k = cmap[c];
-            for (int64_t j = 0; j < f->clause_ptr[c + 1] - f->clause_ptr[c]; ++j) {
+            const int64_t len = f->clause_ptr[c + 1] - f->clause_ptr[c];
+            for (int64_t j = 0; j < len; ++j) {
                 const int32_t p = fill[f->var[f->clause_ptr[c] + j]]++;
-                const int32_t si = cptr[k] + (int32_t)j;
+                int32_t q = (int32_t)j;  // internal slot of original literal j
+                if (len == 3)
+                    for (int qq = 0; qq < 3; ++qq)
+                        if (kP3[lorder[k]][qq] == j) q = qq;
+                const int32_t si = cptr[k] + q;
                 wpos[si] = p;
                 pc[p] = k;
                 ps[p] = si;
