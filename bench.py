@@ -37,6 +37,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
                    help="JSON with the dominant kernel's HBM bytes per step from the PMC passes (profiles/)")
+    p.add_argument("--alg", default="auto", choices=["auto", "onchip", "resident", "fused", "twopass"],
+                   help="force an algorithm (A/B); auto = the solver's default")
     p.add_argument("--extra-batch", type=int, default=256, help="also time this B (configs[1]); 0 = off")
     return p.parse_args()
 
@@ -127,6 +129,9 @@ def main():
         s = Solver(f, batch, args.dtype, device=local % max(1, device_count()))
         if args.chunk:
             s.set_chunk_replicas(args.chunk)
+        if args.alg != "auto":
+            from odesat_amd import _lib
+            s.set_algorithm(getattr(_lib, "ODESAT_ALG_" + args.alg.upper()))
         s.init_state(42, replica0=shard_range(rank, world, batch)[0])
         wall, ms, launches = time_gpu(s, args.steps, args.warmup, dist, local, profile)
         bytes_step = s.clause_kernel_bytes()
@@ -143,9 +148,10 @@ def main():
     # roofline of the dominant kernel: algorithmic bytes per launch ((8n + 16m) B per
     # fp32 replica-step x the replica-steps of one launch) / its mean launch time (HIP events on the
     # solver's stream)
-    from odesat_amd._lib import ODESAT_ALG_RESIDENT
-    kernel = ("k_resident (persistent, LDS-resident voltages, var-disjoint clause tiles)" if alg == ODESAT_ALG_RESIDENT
-              else "k_step (fused RHS + Euler update, variable-major)")
+    from odesat_amd._lib import ODESAT_ALG_ONCHIP, ODESAT_ALG_RESIDENT
+    kernel = {ODESAT_ALG_RESIDENT: "k_resident (persistent, LDS-resident voltages, var-disjoint clause tiles)",
+              ODESAT_ALG_ONCHIP: "k_onchip (persistent, whole replica state on one CU: v/dv in LDS, clause "
+                                 "memories in VGPRs)"}.get(alg, "k_step (fused RHS + Euler update, variable-major)")
     nlaunch = int(launches[0])
     per_launch_s = ms[0] / 1e3 / nlaunch
     steps_per_launch = args.steps / nlaunch

@@ -153,7 +153,8 @@ int odesat_synchronize(odesat_solver *s);
 int odesat_profile_enable(odesat_solver *s, int enable);
 int odesat_profile_read(odesat_solver *s, double *ms /*[3]*/, int64_t *launches /*[3]*/);
 /* Algorithmic bytes per step of the dominant kernel over the whole batch (roofline):
- * FUSED k_step (2n + 4m) * dtype bytes per replica, TWOPASS k_clause (n + 4m) * dtype bytes. */
+ * FUSED / RESIDENT / ONCHIP (2n + 4m) * dtype bytes per replica (v, xs, xl read and written once),
+ * TWOPASS k_clause (n + 4m) * dtype bytes. */
 int64_t odesat_clause_kernel_bytes(const odesat_solver *s);
 /* Tuning: replicas per chunk (0 = automatic) -- the batch is stepped chunk by chunk so the
  * contribution buffer of one chunk stays resident in the Infinity Cache. */
@@ -173,6 +174,11 @@ int odesat_set_schedule(odesat_solver *s, int schedule);
 #define ODESAT_ALG_FUSED 0
 #define ODESAT_ALG_TWOPASS 1
 #define ODESAT_ALG_RESIDENT 2
+/* ONCHIP   = fixed steps with a replica's WHOLE state on one CU for a launch: v and dv in LDS, the
+ *            clause memories in VGPRs + LDS (onchip.hip); per step only the L2-resident clause
+ *            records are read.  f32 3-SAT formulas whose tiles fit (config 2's size); the default
+ *            when available.  Adaptive steps on such a solver run RESIDENT. */
+#define ODESAT_ALG_ONCHIP 3
 int odesat_set_algorithm(odesat_solver *s, int alg);
 /* The algorithm odesat_simulate uses (ODESAT_ALG_*), and the solver's replica group width. */
 int odesat_get_algorithm(const odesat_solver *s);

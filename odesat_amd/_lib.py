@@ -16,7 +16,7 @@ ODESAT_OK, ODESAT_EINVAL, ODESAT_ENOMEM, ODESAT_EDEVICE, ODESAT_ESTATE = 0, -1, 
 ODESAT_F32, ODESAT_F64 = 0, 1
 ODESAT_STOP_EACH, ODESAT_STOP_ANY, ODESAT_STOP_NONE = 0, 1, 2
 ODESAT_SCHED_AUTO, ODESAT_SCHED_STEP_MAJOR, ODESAT_SCHED_CHUNK_MAJOR = 0, 1, 2
-ODESAT_ALG_FUSED, ODESAT_ALG_TWOPASS, ODESAT_ALG_RESIDENT = 0, 1, 2
+ODESAT_ALG_FUSED, ODESAT_ALG_TWOPASS, ODESAT_ALG_RESIDENT, ODESAT_ALG_ONCHIP = 0, 1, 2, 3
 
 
 class OdesatError(RuntimeError):

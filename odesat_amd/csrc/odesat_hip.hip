@@ -19,6 +19,7 @@
 #include "cnf.hpp"
 #include "kernels.hpp"
 #include "resident.hpp"
+#include "onchip.hpp"
 
 using odesat::fail;
 using namespace odk;
@@ -62,6 +63,11 @@ struct odesat_solver {
     int res_ntiles = 0;
     int32_t *res_tc = nullptr, *cmap = nullptr;
     int4 *res_cl4 = nullptr;  // [m] literals of internal clause k (3-SAT)
+    // ONCHIP (onchip.hip): same tiles as RESIDENT (R = 1, f32, 3-SAT); tiles [0, oc_tr) keep their
+    // memories in VGPRs, [oc_tr, oc_tr + oc_tl) in LDS.  oc_tr == 0: not available
+    int oc_tr = 0, oc_tl = 0;
+    uint64_t *oc_rec = nullptr;  // [tiles][512] slot-major clause records (onchip::make_rec)
+    bool in_range = true;        // every replica's state is in ONCHIP's range (onchip.hip header)
     int64_t bytes = 0;
     // profiling
     bool profile = false;
@@ -480,6 +486,51 @@ bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, std::v
     return true;
 }
 
+// ONCHIP eligibility and slot-major records (onchip.hpp).  tiles = the padded tile starts, lits =
+// the internal-order literals (var << 1 | neg).
+int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std::vector<int32_t> &lits) {
+    if (s->res_R != 1 || s->dtype != ODESAT_F32 || s->uniform_k != 3 || s->n > onchip::MAX_N) return ODESAT_OK;
+    if (const char *ev = std::getenv("ODESAT_ONCHIP"))
+        if (std::atoi(ev) == 0) return ODESAT_OK;
+    const int nt = (int)tiles.size() - 1;
+    if (nt == 0 || s->m == 0) return ODESAT_OK;
+    for (int64_t k = 0; k < s->m; ++k) {  // three distinct variables per clause (independent dv updates)
+        const int32_t x = lits[3 * k] >> 1, y = lits[3 * k + 1] >> 1, z = lits[3 * k + 2] >> 1;
+        if (x == y || x == z || y == z) return ODESAT_OK;
+    }
+    const int64_t budget = (int64_t)onchip::LDS_MAX - (int64_t)onchip::lds_bytes(s->n, 0);
+    const int tl_max = budget > 0 ? (int)(budget / onchip::TILE_LDS) / 4 * 4 : 0;
+    int tr = 0;
+    for (int c : onchip::TR_CHOICES)
+        if (c >= nt) { tr = c; break; }
+    if (tr == 0 && nt - onchip::TR_MAX <= tl_max) tr = onchip::TR_MAX;
+    if (tr == 0) return ODESAT_OK;
+    // slot-major records, padded with empty tiles so every tile a pass touches exists; an empty
+    // slot of lane l points all three literals at sink word n + l % 32 (v = 1.0 there)
+    const int ntp = std::max(nt, tr) + 8;
+    std::vector<uint64_t> rec((size_t)ntp * onchip::NTH);
+    for (int t = 0; t < ntp; ++t)
+        for (int l = 0; l < onchip::NTH; ++l) {
+            const int32_t k = t < nt ? tiles[t] + l : -1;
+            uint64_t r;
+            if (k >= 0 && k < tiles[t + 1]) {
+                const int32_t *q = &lits[3 * (size_t)k];
+                r = onchip::make_rec(4u * (uint32_t)(q[0] >> 1), 4u * (uint32_t)(q[1] >> 1), 4u * (uint32_t)(q[2] >> 1),
+                                     q[0] & 1, q[1] & 1, q[2] & 1);
+            } else {
+                const uint32_t sink = 4u * (uint32_t)(s->n + l % onchip::SINKS);
+                r = onchip::make_rec(sink, sink, sink, false, false, false);
+            }
+            rec[(size_t)t * onchip::NTH + l] = r;
+        }
+    int rc;
+    if ((rc = dmalloc(s, (void **)&s->oc_rec, rec.size() * sizeof(uint64_t)))) return rc;
+    HIP_TRY(hipMemcpy(s->oc_rec, rec.data(), rec.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    s->oc_tr = tr;
+    s->oc_tl = std::max(0, nt - tr);
+    return ODESAT_OK;
+}
+
 template <typename T, int R, bool ADA, bool K3> int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     static bool attr_set = false;  // per instantiation
     const size_t lds = res_lds_bytes(s->n, R, sizeof(T), ADA);
@@ -538,6 +589,36 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
         case 4: return go(IC<4>{});
         default: return fail(ODESAT_EINVAL, "resident layout not available");
     }
+}
+
+int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zeta, int stop_mode) {
+    onchip::Args a{};
+    a.rec = s->oc_rec;
+    a.tc = s->res_tc;
+    a.v0 = (float *)s->v[0];
+    a.v1 = (float *)s->v[1];
+    a.c0 = (float *)s->c[0];
+    a.c1 = (float *)s->c[1];
+    a.par = s->par;
+    a.act = s->act;
+    a.sat_step = s->sat_step;
+    a.steps_done = s->steps_done;
+    a.stop = s->stop;
+    a.n = (int32_t)s->n;
+    a.m = (int32_t)s->m;
+    a.ntiles = s->res_ntiles;
+    a.tl = s->oc_tl;
+    a.step0 = step0;
+    a.nsteps = nsteps;
+    a.stop_mode = stop_mode;
+    a.dt = (float)dt;
+    a.zeta = (float)zeta;
+    a.xl_max = 1e4f * (float)s->m;  // system.rs:95, as (T)1e4 * (T)m
+    {
+        Timed tm(s, 0);
+        HIP_TRY(onchip::launch(s->oc_tr, a, s->G, onchip::lds_bytes(s->n, s->oc_tl), s->stream));
+    }
+    return ODESAT_OK;
 }
 
 int dispatch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
@@ -733,7 +814,7 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     for (auto e : s->pool) (void)hipEventDestroy(e);
     void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->pc, s->ps, s->empty, s->inc, s->v[0], s->v[1], s->c[0],
                     s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
-                    s->sat_step, s->steps_done, s->stop, s->res_tc, s->cmap, s->res_cl4};
+                    s->sat_step, s->steps_done, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec};
     for (void *p : ptrs) dfree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
@@ -905,6 +986,8 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         s->res_ada = res_fits(n, res_r, s->tsize, true);
         s->res_ntiles = (int)tiles.size() - 1;
         s->alg = ODESAT_ALG_RESIDENT;
+        if ((rc = onchip_setup(s, tiles, lits))) return bail(rc);
+        if (s->oc_tr > 0) s->alg = ODESAT_ALG_ONCHIP;
     }
     // state (double-buffered)
     for (int b = 0; b < 2; ++b) {
@@ -959,8 +1042,11 @@ extern "C" int odesat_set_schedule(odesat_solver *s, int schedule) {
 extern "C" int odesat_set_algorithm(odesat_solver *s, int alg) {
     int rc;
     if ((rc = check_solver(s))) return rc;
-    if (alg != ODESAT_ALG_FUSED && alg != ODESAT_ALG_TWOPASS && alg != ODESAT_ALG_RESIDENT)
+    if (alg != ODESAT_ALG_FUSED && alg != ODESAT_ALG_TWOPASS && alg != ODESAT_ALG_RESIDENT && alg != ODESAT_ALG_ONCHIP)
         return fail(ODESAT_EINVAL, "bad algorithm");
+    if (alg == ODESAT_ALG_ONCHIP && s->oc_tr == 0)
+        return fail(ODESAT_EINVAL, "ONCHIP needs an f32 3-SAT formula whose tiles fit one CU's VGPRs + LDS "
+                                   "(group width 1); this solver does not admit it");
     if (alg == ODESAT_ALG_RESIDENT && s->res_R == 0)
         return fail(ODESAT_EINVAL, "RESIDENT needs the voltages of a replica group in LDS: this solver's layout "
                                    "(group width " + std::to_string(s->W) + ") does not admit it");
@@ -983,6 +1069,14 @@ extern "C" int odesat_set_state(odesat_solver *s, int64_t r0, int64_t count, con
     if ((rc = upload_items(s, s->c, xs, s->m, 2, 0, r0, count))) return rc;
     if ((rc = upload_items(s, s->c, xl, s->m, 2, 1, r0, count))) return rc;
     if ((rc = reset_replicas(s, r0, count))) return rc;
+    auto within = [](const double *x, int64_t cnt, double lo, double hi) {
+        if (!x) return true;
+        for (int64_t i = 0; i < cnt; ++i)
+            if (!(x[i] >= lo && x[i] <= hi)) return false;  // NaN fails too
+        return true;
+    };
+    s->in_range = s->in_range && within(v, count * s->n, -1.0, 1.0) && within(xs, count * s->m, -1.0, 1.0) &&
+                  within(xl, count * s->m, 1.0, 1e30);
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ODESAT_OK;
 }
@@ -992,6 +1086,7 @@ extern "C" int odesat_init_state(odesat_solver *s, uint64_t seed, int64_t replic
     if ((rc = check_solver(s))) return rc;
     if ((rc = init_dispatch(s, seed, replica0, false))) return rc;
     if ((rc = reset_replicas(s, 0, s->Bp))) return rc;
+    s->in_range = true;  // v in [-1, 1), xs = +-1, xl = 1
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ODESAT_OK;
 }
@@ -1063,6 +1158,7 @@ static int single_step(odesat_solver *s, bool adaptive, double tol, double dt, d
     HIP_TRY(hipMemcpy(s->sat_step, minus.data(), s->Bp * 8, hipMemcpyHostToDevice));
     if ((rc = dispatch_step(s, 0, adaptive, dt, zeta, tol, ODESAT_STOP_NONE, 0, s->G))) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
+    if (!adaptive) s->in_range = true;  // every replica took a clamped step
     std::vector<int64_t> sat(s->Bp);
     HIP_TRY(hipMemcpy(sat.data(), s->sat_step, s->Bp * 8, hipMemcpyDeviceToHost));
     if (allsat)
@@ -1106,16 +1202,25 @@ static int simulate_resident(odesat_solver *s, const odesat_params *p, bool adap
                              int poll, int64_t *first_sat_step, int64_t *steps_done, double *dt_out,
                              int64_t *steps_run) {
     int rc = ODESAT_OK;
-    // launches of `poll` steps (STOP_ANY: 1, so no replica runs past the stop step)
+    // launches of `poll` steps (STOP_ANY: 1, so no replica runs past the stop step), aligned to the
+    // poll points.  ONCHIP needs in-range states (onchip.hip): when the caller's state may not be,
+    // the first step runs RESIDENT, whose clamps bring every state into range.
     const int per_launch = p->stop == ODESAT_STOP_ANY ? 1 : poll;
+    const bool oc = s->alg == ODESAT_ALG_ONCHIP && !adaptive && std::fabs(zeta) <= 1e6;
     int32_t h_stop = INT_MAX;
     std::vector<uint8_t> h_act(s->Bp);
-    int64_t t = 0;
+    int64_t t = 0, next_poll = poll;
     while (t < p->max_steps) {
-        const int k = (int)std::min<int64_t>(per_launch, p->max_steps - t);
-        if ((rc = dispatch_resident(s, (int)t, k, adaptive, p->dt, zeta, tol, p->stop))) return rc;
+        const bool use_oc = oc && (t > 0 || s->in_range);
+        int k = (int)std::min<int64_t>(std::min<int64_t>(per_launch, next_poll - t), p->max_steps - t);
+        if (oc && !use_oc) k = 1;
+        if ((rc = use_oc ? launch_onchip(s, (int)t, k, p->dt, zeta, p->stop)
+                         : dispatch_resident(s, (int)t, k, adaptive, p->dt, zeta, tol, p->stop)))
+            return rc;
         t += k;
-        if (p->stop != ODESAT_STOP_NONE && t % poll == 0 && t < p->max_steps) {
+        if (t < next_poll) continue;
+        next_poll += poll;
+        if (p->stop != ODESAT_STOP_NONE && t < p->max_steps) {
             HIP_TRY(hipMemcpyAsync(&h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream));
             HIP_TRY(hipMemcpyAsync(h_act.data(), s->act, s->Bp, hipMemcpyDeviceToHost, s->stream));
             HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1127,6 +1232,7 @@ static int simulate_resident(odesat_solver *s, const odesat_params *p, bool adap
             }
         }
     }
+    s->in_range = true;  // every replica took at least one clamped step
     return finish_simulate(s, p, adaptive, t, first_sat_step, steps_done, dt_out, steps_run);
 }
 
@@ -1153,7 +1259,9 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
         if (adaptive && (rc = put_dt(s, nullptr, 0.01))) return rc;
     }
     const int poll = p->poll_interval > 0 ? p->poll_interval : 32;
-    if (s->alg == ODESAT_ALG_RESIDENT && (!adaptive || s->res_ada)) return simulate_resident(s, p, adaptive, zeta, tol, poll, first_sat_step,
+    if (s->alg == ODESAT_ALG_ONCHIP && !adaptive)
+        return simulate_resident(s, p, adaptive, zeta, tol, poll, first_sat_step, steps_done, dt_out, steps_run);
+    if ((s->alg == ODESAT_ALG_RESIDENT || s->alg == ODESAT_ALG_ONCHIP) && (!adaptive || s->res_ada)) return simulate_resident(s, p, adaptive, zeta, tol, poll, first_sat_step,
                                                                 steps_done, dt_out, steps_run);
     int32_t *h_stop = nullptr;
     uint8_t *h_act = nullptr;
@@ -1200,6 +1308,7 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
     (void)hipHostFree(h_act);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(s->stream));
+    s->in_range = true;
     if (steps_run) *steps_run = t_run;
     if (first_sat_step) HIP_TRY(hipMemcpy(first_sat_step, s->sat_step, s->B * 8, hipMemcpyDeviceToHost));
     if (steps_done) HIP_TRY(hipMemcpy(steps_done, s->steps_done, s->B * 8, hipMemcpyDeviceToHost));
@@ -1247,7 +1356,9 @@ extern "C" int64_t odesat_clause_kernel_bytes(const odesat_solver *s) {
     // Algorithmic bytes per step of the dominant kernel over the whole batch, in dtype.
     // FUSED k_step: v, xs, xl each read and written once (2n + 4m per replica).
     // TWOPASS k_clause: v gathered once (n), xs / xl read + written (4m).
+    // RESIDENT / ONCHIP: SURVEY.md §8d's compulsory state traffic, v, xs, xl each read and written
+    // once per replica-step (2n + 4m) -- ONCHIP moves it on chip, not through HBM.
     if (!s) return -1;
-    const int64_t per = s->alg == ODESAT_ALG_FUSED ? 2 * s->n + 4 * s->m : s->n + 4 * s->m;
+    const int64_t per = s->alg == ODESAT_ALG_TWOPASS ? s->n + 4 * s->m : 2 * s->n + 4 * s->m;
     return (int64_t)s->B * per * (int64_t)s->tsize;
 }

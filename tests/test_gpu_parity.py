@@ -368,11 +368,17 @@ def test_algorithms_identical(name, prec, B):
     trajectories, including replicas frozen at different steps (STOP_EACH) and adaptive steps."""
     from odesat_amd import _lib
     f = product_formula(name)
+    with Solver(f, B, prec) as s:
+        default = s.algorithm
+    # these formulas fit in LDS; f32 3-SAT ones fit on chip (ONCHIP, fixed steps; adaptive -> RESIDENT)
+    assert default == (_lib.ODESAT_ALG_ONCHIP if prec == "f32" and name == "rand200" else _lib.ODESAT_ALG_RESIDENT)
+    algs = [_lib.ODESAT_ALG_RESIDENT, _lib.ODESAT_ALG_FUSED, _lib.ODESAT_ALG_TWOPASS]
+    if default == _lib.ODESAT_ALG_ONCHIP:
+        algs.append(_lib.ODESAT_ALG_ONCHIP)
     for adaptive in (False, True):
         out = []
-        for alg in (_lib.ODESAT_ALG_RESIDENT, _lib.ODESAT_ALG_FUSED, _lib.ODESAT_ALG_TWOPASS):
+        for alg in algs:
             with Solver(f, B, prec) as s:
-                assert s.algorithm == _lib.ODESAT_ALG_RESIDENT  # these formulas fit in LDS
                 s.set_algorithm(alg)
                 s.init_state(21)
                 r = s.simulate(adaptive=adaptive, dt=0.05, max_steps=80, stop=ODESAT_STOP_EACH, poll_interval=3)
@@ -414,7 +420,9 @@ def test_resident_widths_match_fused_w64(monkeypatch, name, prec, width, mode):
     B = 37
     a1, w1, r1, s1 = _run_layout(monkeypatch, f, B, prec, width, **kw)
     a2, w2, r2, s2 = _run_layout(monkeypatch, f, B, prec, 64, **kw)
-    assert (a1, w1) == (_lib.ODESAT_ALG_RESIDENT, width) and (a2, w2) == (_lib.ODESAT_ALG_FUSED, 64)
+    onchip = width == 1 and prec == "f32" and name != "small"  # f32 3-SAT at R = 1: ONCHIP by default
+    assert (a1, w1) == (_lib.ODESAT_ALG_ONCHIP if onchip else _lib.ODESAT_ALG_RESIDENT, width)
+    assert (a2, w2) == (_lib.ODESAT_ALG_FUSED, 64)
     assert np.array_equal(r1["first_sat_step"], r2["first_sat_step"])
     assert np.array_equal(r1["steps_done"], r2["steps_done"]) and r1["steps_run"] == r2["steps_run"]
     assert same(r1["dt"], r2["dt"])
@@ -428,9 +436,11 @@ def test_default_layout_is_resident_for_config2():
     var, neg = wl.random_ksat(c["n"], c["m"], 3, c["seed"])
     cp, v_, n_ = wl.formula_arrays(var, neg)
     f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
-    for prec in ("f32", "f64"):  # f64: v and dv (160,000 B) fit; adaptive steps then run FUSED
+    # f32: the whole replica state fits on one CU (ONCHIP); f64: v and dv (160,000 B) fit in LDS
+    # (RESIDENT; adaptive steps then run FUSED)
+    for prec, alg in (("f32", _lib.ODESAT_ALG_ONCHIP), ("f64", _lib.ODESAT_ALG_RESIDENT)):
         with Solver(f, 1024, prec) as s:
-            assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.group_width == 1
+            assert s.algorithm == alg and s.group_width == 1
 
 
 def test_frozen_replicas_keep_state_across_buffer_flips():
@@ -447,3 +457,55 @@ def test_frozen_replicas_keep_state_across_buffer_flips():
         t, sat, _, _, _ = o.simulate(v0[b], xs0[b], xl0[b], dt=0.1, steps=3000)
         assert t == r["steps_done"][b] and sat == (r["first_sat_step"][b] >= 0)
         assert same(v[b], v0[b]) and same(xs[b], xs0[b]) and same(xl[b], xl0[b])
+
+
+# ------------------------------------------------------------------ ONCHIP (onchip.hip) --------
+def _instance(n, m, seed):
+    var, neg = wl.random_ksat(n, m, 3, seed)
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    return cnf.CNFFormula.from_arrays(cp, v_, n_, n), (cp, v_, n_)
+
+
+@pytest.mark.parametrize("stop", ["each", "any", "none"])
+def test_onchip_lds_tiles_match_resident_and_oracle(stop):
+    """n=6000, m=33000 (ratio 5.5): 116 tiles, so ONCHIP keeps 96 tiles' memories in VGPRs and 20
+    in LDS.  ONCHIP == RESIDENT (HBM-streamed memories) bit for bit on every stop policy, and
+    replica 0 == the oracle's f32 restatement."""
+    from odesat_amd import _lib
+    f, (cp, v_, n_) = _instance(6000, 33000, 5)
+    pol = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[stop]
+    B, K = 6, 25
+    out = []
+    for alg in (_lib.ODESAT_ALG_ONCHIP, _lib.ODESAT_ALG_RESIDENT):
+        with Solver(f, B, "f32") as s:
+            s.set_algorithm(alg)
+            s.init_state(9)
+            r = s.simulate(dt=0.05, max_steps=K, stop=pol, poll_interval=10)
+            out.append((r["first_sat_step"], r["steps_done"], s.get_state()))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    for x, y in zip(out[0][2], out[1][2]):
+        assert same(x, y)
+    o = Oracle(cp, v_, n_, 6000, "f32")
+    ov = init_voltages(9, 0, 1, 6000)[0].astype(np.float32)
+    oxs, oxl = o.init_short_term_memory(), np.ones(33000, np.float32)
+    o.simulate(ov, oxs, oxl, dt=np.float32(0.05), steps=int(out[0][1][0]), zeta=np.float32(0.001))
+    v, xs, xl = out[0][2]
+    assert same(v[0], ov) and same(xs[0], oxs) and same(xl[0], oxl)
+
+
+def test_onchip_long_launches_sat_and_freeze():
+    """STOP_EACH over launches of many steps: replicas that satisfy easy.cnf freeze at their own
+    step inside a launch (ONCHIP == FUSED, states and sat steps)."""
+    from odesat_amd import _lib
+    f = product_formula("easy")
+    out = []
+    for alg in (_lib.ODESAT_ALG_ONCHIP, _lib.ODESAT_ALG_FUSED):
+        with Solver(f, 40, "f32") as s:
+            s.set_algorithm(alg)
+            s.init_state(4)
+            r = s.simulate(dt=0.1, max_steps=3000, stop=ODESAT_STOP_EACH, poll_interval=500)
+            out.append((r["first_sat_step"], r["steps_done"], s.get_state()))
+    assert (out[0][0] >= 0).any()
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    for x, y in zip(out[0][2], out[1][2]):
+        assert same(x, y)
