@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libodesat_hip.so")
+LIB_PATH = os.environ.get("ODESAT_LIB") or os.path.join(_HERE, "lib", "libodesat_hip.so")  # override: A/B builds
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "odesat.h")
 
 ODESAT_OK, ODESAT_EINVAL, ODESAT_ENOMEM, ODESAT_EDEVICE, ODESAT_ESTATE = 0, -1, -2, -3, -4

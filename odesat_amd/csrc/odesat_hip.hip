@@ -67,6 +67,7 @@ struct odesat_solver {
     // memories in VGPRs, [oc_tr, oc_tr + oc_tl) in LDS.  oc_tr == 0: not available
     int oc_tr = 0, oc_tl = 0;
     uint64_t *oc_rec = nullptr;  // [tiles][512] slot-major clause records (onchip::make_rec)
+    int64_t oc_rec_bytes = 0;
     bool in_range = true;        // every replica's state is in ONCHIP's range (onchip.hip header)
     int64_t bytes = 0;
     // profiling
@@ -498,8 +499,7 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
         const int32_t x = lits[3 * k] >> 1, y = lits[3 * k + 1] >> 1, z = lits[3 * k + 2] >> 1;
         if (x == y || x == z || y == z) return ODESAT_OK;
     }
-    const int64_t budget = (int64_t)onchip::LDS_MAX - (int64_t)onchip::lds_bytes(s->n, 0);
-    const int tl_max = budget > 0 ? (int)(budget / onchip::TILE_LDS) / 4 * 4 : 0;
+    const int tl_max = onchip::tl_max(s->n);
     int tr = 0;
     for (int c : onchip::TR_CHOICES)
         if (c >= nt) { tr = c; break; }
@@ -524,6 +524,7 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
             rec[(size_t)t * onchip::NTH + l] = r;
         }
     int rc;
+    s->oc_rec_bytes = (int64_t)(rec.size() * sizeof(uint64_t));
     if ((rc = dmalloc(s, (void **)&s->oc_rec, rec.size() * sizeof(uint64_t)))) return rc;
     HIP_TRY(hipMemcpy(s->oc_rec, rec.data(), rec.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
     s->oc_tr = tr;
@@ -594,6 +595,8 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
 int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zeta, int stop_mode) {
     onchip::Args a{};
     a.rec = s->oc_rec;
+    a.rec_bytes = (uint32_t)s->oc_rec_bytes;
+    a.lds = onchip::lds_map(s->n);
     a.tc = s->res_tc;
     a.v0 = (float *)s->v[0];
     a.v1 = (float *)s->v[1];
@@ -612,7 +615,6 @@ int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zet
     a.nsteps = nsteps;
     a.stop_mode = stop_mode;
     a.dt = (float)dt;
-    a.zeta = (float)zeta;
     a.xl_max = 1e4f * (float)s->m;  // system.rs:95, as (T)1e4 * (T)m
     {
         Timed tm(s, 0);
@@ -1206,7 +1208,10 @@ static int simulate_resident(odesat_solver *s, const odesat_params *p, bool adap
     // poll points.  ONCHIP needs in-range states (onchip.hip): when the caller's state may not be,
     // the first step runs RESIDENT, whose clamps bring every state into range.
     const int per_launch = p->stop == ODESAT_STOP_ANY ? 1 : poll;
-    const bool oc = s->alg == ODESAT_ALG_ONCHIP && !adaptive && std::fabs(zeta) <= 1e6;
+    // (the kernel omits the rigidity term and uses med3 clamps: both exact for finite zeta and a
+    // finite, normal dt -- onchip.hip)
+    const double adt = std::fabs(p->dt);
+    const bool oc = s->alg == ODESAT_ALG_ONCHIP && !adaptive && std::fabs(zeta) <= 1e6 && adt >= 1e-30 && adt <= 1e30;
     int32_t h_stop = INT_MAX;
     std::vector<uint8_t> h_act(s->Bp);
     int64_t t = 0, next_poll = poll;

@@ -43,110 +43,159 @@ struct Slot {  // one lane's literal record for one tile
     uint32_t lo, hi;
 };
 
-struct Pend {  // a clause's three dv terms (LDS byte addresses of v; dv is at +DV), applied one tile later
+struct Pend {  // a clause's three dv terms (LDS byte addresses of v; dv is at +DVC), applied one tile later
     uint32_t a0, a1, a2;
     float d0, d1, d2;
 };
 
-typedef const __attribute__((address_space(1))) uint64_t grec;  // global: counts in vmcnt only
+struct Gath {  // a clause's gathered inputs: LDS byte addresses of its voltages, sign word, voltages
+    uint32_t a0, a1, a2, hi;
+    float v0, v1, v2;
+};
 
-// Records of tile t (uniform base, per-lane offset: the SGPR-base form of global_load).
-__device__ __forceinline__ Slot load_rec(const grec *rec, int t, int lane) {
-    const grec *base = rec + (size_t)t * NTH;
-    const uint64_t r = base[lane];
-    return Slot{(uint32_t)r, (uint32_t)(r >> 32)};
+// The records are read with buffer loads: the resource (SGPRs) holds the base, the per-lane offset
+// lane * 8 is one VGPR for the whole launch and the tile offset t * 4096 is a scalar, so a ring
+// refill costs no vector instruction.
+struct Recs {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t voff;  // lane * 8
+    uint32_t soff;  // opaque 0 (see pass())
+};
+__device__ __forceinline__ Slot load_rec(const Recs &R, int t) {
+    typedef int i2 __attribute__((ext_vector_type(2)));
+    const i2 r = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, R.voff, R.soff + (uint32_t)t * (NTH * 8), 0);
+    return Slot{(uint32_t)r.x, (uint32_t)r.y};
 }
 
 typedef __attribute__((address_space(3))) float lfloat;
-__device__ __forceinline__ float lds_f(uint32_t byte_addr, uint32_t off) {
-    return *reinterpret_cast<const lfloat *>(byte_addr + off);
-}
-__device__ __forceinline__ void lds_st(uint32_t byte_addr, uint32_t off, float x) {
-    *reinterpret_cast<lfloat *>(byte_addr + off) = x;
+__device__ __forceinline__ float lds_f(uint32_t byte_addr) { return *reinterpret_cast<const lfloat *>(byte_addr); }
+__device__ __forceinline__ void lds_st(uint32_t byte_addr, float x) { *reinterpret_cast<lfloat *>(byte_addr) = x; }
+typedef __attribute__((address_space(3))) float2 lfloat2;
+__device__ __forceinline__ float2 *lds_f2(uint32_t byte_addr) { return (float2 *)(reinterpret_cast<lfloat2 *>(byte_addr)); }
+
+// The clause's three voltages (system.rs:46-48): LDS reads issued here, consumed by compute().
+__device__ __forceinline__ void gather(const Slot &S, Gath &G) {
+    G.a0 = S.lo & 0xffffu;
+    G.a1 = S.lo >> 16;
+    G.a2 = S.hi & 0xffffu;
+    G.hi = S.hi;
+    G.v0 = lds_f(G.a0);
+    G.v1 = lds_f(G.a1);
+    G.v2 = lds_f(G.a2);
 }
 
-// One clause (system.rs:43-88): C, the three dv terms into P, the sat test, and the memory update
-// in place (:84-85, :94-95).
-__device__ __forceinline__ void clause(const Args &a, const Slot &S, float2 &mem, float h, Pend &P, float &cmax) {
-    P.a0 = S.lo & 0xffffu;
-    P.a1 = S.lo >> 16;
-    P.a2 = S.hi & 0xffffu;
-    const uint32_t s0 = S.hi & 0x80000000u, s1 = (S.hi << 1) & 0x80000000u, s2 = (S.hi << 2) & 0x80000000u;
-    const float v0 = lds_f(P.a0, 0), v1 = lds_f(P.a1, 0), v2 = lds_f(P.a2, 0);
-    const float val0 = 1.0f - __uint_as_float(__float_as_uint(v0) ^ s0);  // 1 - q v  (:47)
-    const float val1 = 1.0f - __uint_as_float(__float_as_uint(v1) ^ s1);
-    const float val2 = 1.0f - __uint_as_float(__float_as_uint(v2) ^ s2);
-    const float mn = fminf(fminf(val0, val1), val2);                // min (:49-55)
-    const float sec = __builtin_amdgcn_fmed3f(val0, val1, val2);     // second min, ties -> min
-    const float C = 0.5f * mn;                                       // :60
+// One clause (system.rs:43-88) from its gathered voltages: the three dv terms into Q, the sat fold,
+// and the memory update in place (:84-85, :94-95), in exact rewritten forms (C = mn / 2 exactly):
+//   C < gamma  <=>  mn < 0.5, so cmax folds the bits of mn (mn >= +0 orders as its bits);
+//   C - 0.25 = 0.5 (mn - 0.5) and C - 0.05 = 0.5 (mn - 0.1) (0.05f is exactly 0.1f / 2), so
+//   h dxs = (h/2) round(A (mn - 0.5)) with A = 20 (xs + eps), and dxl = 2.5 (mn - 0.1);
+//   xl xs G_j = +-round((xl xs / 2) sel_j) = +-round(xl xs sel_j) / 2 with sel_j = mn or sec: the
+//   terms are accumulated unhalved (dv2 = 2 dv, also exact), and the update uses h/2 (:96);
+//   the clamps are med3 (finite arguments: the host requires a finite dt).
+// Scalings by 0.5 / 2 / 2.5 / +-1 are exact here (no subnormals: |A| >= 0.02, |mn - c| >= 2^-26 or 0,
+// |xl xs sel| >= 6e-11 or 0).
+__device__ __forceinline__ void compute(const Args &a, const Gath &G, float2 &mem, float h, float hh, Pend &Q,
+                                        uint32_t &cmax) {
+    const uint32_t s0 = G.hi & 0x80000000u, s1 = (G.hi << 1) & 0x80000000u, s2 = (G.hi << 2) & 0x80000000u;
+    const float val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
+    const float val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
+    const float val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
+    const float mn = fminf(fminf(val0, val1), val2);               // min (:49-55)
+    const float sec = __builtin_amdgcn_fmed3f(val0, val1, val2);    // second min, ties -> min
     const float xs = mem.x, xl = mem.y;
-    const float ht = 0.5f * (xl * xs);
-    P.d0 = __uint_as_float(__float_as_uint(ht * (val0 != mn ? mn : sec)) ^ s0);  // xl xs G (:64-70, :80)
-    P.d1 = __uint_as_float(__float_as_uint(ht * (val1 != mn ? mn : sec)) ^ s1);
-    P.d2 = __uint_as_float(__float_as_uint(ht * (val2 != mn ? mn : sec)) ^ s2);
-    cmax = fmaxf(cmax, C);  // :88 -- unsat iff max C >= gamma (C is never NaN here)
-    asm volatile("" : "+v"(cmax));  // fold now: deferred, it would keep every tile's C live
-    const float dxs = 20.0f * (xs + 0.001f) * (C - 0.25f);      // :84
-    const float dxl = 5.0f * (C - 0.05f);                       // :85
-    mem.x = fminf(fmaxf(xs + h * dxs, 0.001f), 1.0f - 0.001f);  // :94
-    mem.y = fminf(fmaxf(xl + h * dxl, 1.0f), a.xl_max);         // :95
-    asm volatile("" : "+v"(mem.x), "+v"(mem.y));  // update now: sunk into later tiles it keeps C live
+    const float tt = xl * xs;
+    const float tm = tt * mn, ts = tt * sec;
+    Q.a0 = G.a0;
+    Q.a1 = G.a1;
+    Q.a2 = G.a2;
+    Q.d0 = __uint_as_float(__float_as_uint(val0 != mn ? tm : ts) ^ s0);  // 2 xl xs G (:64-70, :80)
+    Q.d1 = __uint_as_float(__float_as_uint(val1 != mn ? tm : ts) ^ s1);
+    Q.d2 = __uint_as_float(__float_as_uint(val2 != mn ? tm : ts) ^ s2);
+    cmax = max(cmax, __float_as_uint(mn));  // :88 -- unsat iff max mn >= 0.5
+    asm volatile("" : "+v"(cmax));          // fold now: deferred, it would keep every tile's mn live
+    const float dxs2 = (20.0f * (xs + 0.001f)) * (mn - 0.5f);  // 2 dxs (:84)
+    const float dxl = 2.5f * (mn - 0.1f);                       // :85
+    mem.x = __builtin_amdgcn_fmed3f(xs + hh * dxs2, 0.001f, 1.0f - 0.001f);  // :94
+    mem.y = __builtin_amdgcn_fmed3f(xl + h * dxl, 1.0f, a.xl_max);           // :95
+    asm volatile("" : "+v"(mem.x), "+v"(mem.y));  // update now: sunk into later tiles it keeps mn live
 }
 
-// :80 for one clause: dv[i_j] += d_j (three distinct variables: independent updates)
-__device__ __forceinline__ void apply(uint32_t DV, const Pend &P) {
-    const float o0 = lds_f(P.a0, DV), o1 = lds_f(P.a1, DV), o2 = lds_f(P.a2, DV);
-    lds_st(P.a0, DV, o0 + P.d0);
-    lds_st(P.a1, DV, o1 + P.d1);
-    lds_st(P.a2, DV, o2 + P.d2);
+// One tile step.  In flight: P = tile t's dv terms, Gn = tile t+1's gathered voltages (read one
+// step earlier), ring = the records of tiles t+2 .. t+5.  The critical chain of a step is tile t's
+// dv read-modify-write (:80; three distinct variables per clause, so the updates are independent)
+// between two barriers: its reads go out first and the writes right after they return.  The
+// voltage gathers of tile t+2 follow (v is constant during a pass) and tile t+1's arithmetic runs
+// while they and the writes drain.  The barrier then orders tile t's dv against tile t+1's.
+__device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &slot2, float2 &mem1, Pend &P, Gath &Gn,
+                                          int t, float h, float hh, uint32_t &cmax) {
+    const float o0 = lds_f(P.a0 + DVC), o1 = lds_f(P.a1 + DVC), o2 = lds_f(P.a2 + DVC);
+    lds_st(P.a0 + DVC, o0 + P.d0);
+    lds_st(P.a1 + DVC, o1 + P.d1);
+    lds_st(P.a2 + DVC, o2 + P.d2);
+    __builtin_amdgcn_sched_barrier(0);
+    Gath G2;
+    gather(slot2, G2);
+    slot2 = load_rec(R, t + 6);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(a, Gn, mem1, h, hh, P, cmax);  // P <- tile t+1's terms (tile t's were written above)
+    __builtin_amdgcn_sched_barrier(0);     // a tile's work stays between its barriers
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    Gn = G2;
 }
 
-// Register tile T of the pass (static T, so mr[] stays in VGPRs): terms of tile T+1 (ring slot
-// (T+1) % 4, refilled with tile T+5), apply tile T's terms P, barrier.  All TR register tiles run
+// LDS byte address of this lane's slot in LDS memory tile lt (onchip.hpp, Lds).
+__device__ __forceinline__ uint32_t mem_addr(const Args &a, int lt, int lane) {
+    const uint32_t base = (uint32_t)lt < a.lds.gap_tiles ? a.lds.gap_base + (uint32_t)lt * TILE_LDS
+                                                         : a.lds.after_base + ((uint32_t)lt - a.lds.gap_tiles) * TILE_LDS;
+    return base + (uint32_t)lane * 8u;
+}
+
+// Register tile T of the pass (static T, so mr[] stays in VGPRs).  All TR register tiles run
 // (tiles past the last one are empty): an early exit would join TR paths after the sequence, and
 // the copies that merge mr[] there double its VGPR footprint.
 template <int TR, int T>
-__device__ __forceinline__ void reg_tile(const Args &a, const grec *rec, uint32_t DV, float2 *memL,
-                                         float2 (&mr)[TR], Slot (&ring)[4], Pend &P, float h, int lane, float &cmax) {
-    Pend Q;
+__device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&mr)[TR], Slot (&ring)[4], Pend &P,
+                                         Gath &Gn, float h, float hh, int lane, uint32_t &cmax) {
     if constexpr (T + 1 < TR) {
-        clause(a, ring[(T + 1) % 4], mr[T + 1], h, Q, cmax);
-    } else {
+        tile_step(a, R, ring[(T + 2) % 4], mr[T + 1], P, Gn, T, h, hh, cmax);
+    } else {  // tile TR is the first LDS tile (if any)
         float2 m = make_float2(0.0f, 0.0f);
-        if (a.tl > 0) m = memL[lane];
-        clause(a, ring[(T + 1) % 4], m, h, Q, cmax);
-        if (a.tl > 0) memL[lane] = m;
+        if (a.tl > 0) m = *lds_f2(mem_addr(a, 0, lane));
+        tile_step(a, R, ring[(T + 2) % 4], m, P, Gn, T, h, hh, cmax);
+        if (a.tl > 0) *lds_f2(mem_addr(a, 0, lane)) = m;
     }
-    apply(DV, P);
-    ring[(T + 1) % 4] = load_rec(rec, T + 5, lane);
-    __builtin_amdgcn_sched_barrier(0);  // a tile's work stays between its barriers
-    __syncthreads();
-    __builtin_amdgcn_sched_barrier(0);
-    P = Q;
 }
 
 template <int TR, int... Ts>
-__device__ __forceinline__ void reg_tiles(std::integer_sequence<int, Ts...>, const Args &a, const grec *rec,
-                                          uint32_t DV, float2 *memL, float2 (&mr)[TR], Slot (&ring)[4], Pend &P,
-                                          float h, int lane, float &cmax) {
-    (reg_tile<TR, Ts>(a, rec, DV, memL, mr, ring, P, h, lane, cmax), ...);
+__device__ __forceinline__ void reg_tiles(std::integer_sequence<int, Ts...>, const Args &a, const Recs &R,
+                                          float2 (&mr)[TR], Slot (&ring)[4], Pend &P, Gath &Gn, float h, float hh,
+                                          int lane, uint32_t &cmax) {
+    (reg_tile<TR, Ts>(a, R, mr, ring, P, Gn, h, hh, lane, cmax), ...);
 }
 
 // One RHS pass + memory update over every tile; ends with a barrier (dv complete).
 template <int TR>
-__device__ __forceinline__ void pass(const Args &a, uint32_t DV, float2 *memL, float2 (&mr)[TR], float h, int lane,
-                                     float &cmax) {
-    // an opaque copy of the record pointer per pass keeps the record loads inside the step loop
-    // (hoisted out of it they would pin hundreds of VGPRs)
-    const grec *rec = (const grec *)a.rec;
-    asm volatile("" : "+s"(rec));
+__device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, int lane, uint32_t &cmax) {
+    Recs R;
+    R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec, 0, (int)a.rec_bytes, 0x00020000);
+    R.voff = (uint32_t)lane * 8u;
+    // an opaque zero per pass keeps the record loads inside the step loop (hoisted out of it they
+    // would pin hundreds of VGPRs)
+    R.soff = 0u;
+    asm volatile("" : "+s"(R.soff));
+    const float hh = 0.5f * h;
     Slot ring[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) ring[s] = load_rec(rec, s, lane);
+    for (int s = 0; s < 4; ++s) ring[s] = load_rec(R, s);
     Pend P;
-    clause(a, ring[0], mr[0], h, P, cmax);
-    ring[0] = load_rec(rec, 4, lane);
-    reg_tiles<TR>(std::make_integer_sequence<int, TR>{}, a, rec, DV, memL, mr, ring, P, h, lane, cmax);
+    Gath G0, Gn;
+    gather(ring[0], G0);
+    ring[0] = load_rec(R, 4);
+    gather(ring[1], Gn);
+    ring[1] = load_rec(R, 5);
+    compute(a, G0, mr[0], h, hh, P, cmax);
+    reg_tiles<TR>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Gn, h, hh, lane, cmax);
     // LDS tiles [TR, TR + tl): tl is a multiple of 4 (the host pads the tiling)
     const int NT = TR + a.tl;
     const int last = a.tl - 1;
@@ -154,15 +203,10 @@ __device__ __forceinline__ void pass(const Args &a, uint32_t DV, float2 *memL, f
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int t = t0 + u;
-            Pend Q;
-            const int lt = min(t + 1 - TR, last);
-            float2 m = memL[lt * NTH + lane];
-            clause(a, ring[(u + 1) % 4], m, h, Q, cmax);
-            memL[lt * NTH + lane] = m;
-            apply(DV, P);
-            ring[(u + 1) % 4] = load_rec(rec, t + 5, lane);
-            __syncthreads();
-            P = Q;
+            const uint32_t ma = mem_addr(a, min(t + 1 - TR, last), lane);
+            float2 m = *lds_f2(ma);
+            tile_step(a, R, ring[(u + 2) % 4], m, P, Gn, t, h, hh, cmax);
+            *lds_f2(ma) = m;
         }
     }
 }
@@ -183,11 +227,9 @@ __device__ __forceinline__ void mem_io(std::integer_sequence<int, Js...>, const 
     (one(std::integral_constant<int, Js>{}), ...);
 }
 
-// LDS map (floats): v[n2] at 0 (v[n .. n2) = sink words, 1.0), dv[n2] at n2 (byte offset DV),
-// two unsat flags, then tl tiles of memories [tl][NTH] float2.
+// The kernel declares no static LDS, so dynamic LDS -- and the records' byte addresses -- start at 0.
 template <int TR>
 __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
     const int g = blockIdx.x, lane = threadIdx.x;
     int act = a.act[g];
     if (!act) return;  // frozen replica (uniform)
@@ -196,44 +238,38 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     float *V = (p ? a.v1 : a.v0) + (size_t)g * a.n;
     float2 *CM = reinterpret_cast<float2 *>((p ? a.c1 : a.c0) + (size_t)g * a.m * 2);
     const int n2 = a.n + SINKS;
-    float *vL = smem, *dvL = smem + n2;
-    int *unsL = reinterpret_cast<int *>(smem + 2 * n2);
-    float2 *memL = reinterpret_cast<float2 *>(smem + 2 * n2 + 2);
-    const uint32_t DV = (uint32_t)(4 * n2);
+    const uint32_t UNS = DVC + 4u * (uint32_t)n2;  // two unsat flags
     int64_t sat = a.sat_step[g], done = a.steps_done[g];
     const cint32 *tc = (const cint32 *)a.tc;
 
     for (int i = lane; i < n2; i += NTH) {
-        vL[i] = i < a.n ? V[i] : 1.0f;
-        dvL[i] = 0.0f;  // :33
+        lds_st(4u * i, i < a.n ? V[i] : 1.0f);
+        lds_st(4u * i + DVC, 0.0f);  // :33
     }
     float2 mr[TR];
     mem_io<TR>(std::make_integer_sequence<int, TR>{}, tc, a.ntiles, CM, mr, lane, true);
     for (int t = 0; t < a.tl; ++t) {
         const int c0 = tc[min(TR + t, a.ntiles)], c1 = tc[min(TR + t + 1, a.ntiles)];
         const int c = c0 + lane;
-        memL[t * NTH + lane] = c < c1 ? CM[c] : make_float2(0.0f, 0.0f);
+        *lds_f2(mem_addr(a, t, lane)) = c < c1 ? CM[c] : make_float2(0.0f, 0.0f);
     }
-    if (lane == 0) {
-        unsL[0] = 0;
-        unsL[1] = 0;
-    }
+    if (lane < 2) lds_st(UNS + 4u * lane, 0.0f);
     __syncthreads();
 
-    const float h = a.dt;
+    const float h = a.dt, hh = 0.5f * a.dt;
     for (int k = 0; k < a.nsteps; ++k) {  // euler_step_fixed (system.rs:141-154)
-        float cmax = 0.0f;
-        pass<TR>(a, DV, memL, mr, h, lane, cmax);
-        if (!(cmax < 0.25f)) unsL[k & 1] = 1;
-        for (int i = lane; i < a.n; i += NTH) {  // :96, dv restarts at 0 (:33)
-            const float d = dvL[i];
-            dvL[i] = 0.0f;
-            vL[i] = fminf(fmaxf(vL[i] + h * d, -1.0f), 1.0f);
+        uint32_t cmax = 0u;
+        pass<TR>(a, mr, h, lane, cmax);
+        if (!(__uint_as_float(cmax) < 0.5f)) lds_st(UNS + 4u * (k & 1), 1.0f);
+        for (int i = lane; i < a.n; i += NTH) {  // :96 (h dv = (h/2) dv2), dv restarts at 0 (:33)
+            const float d2 = lds_f(4u * i + DVC);
+            lds_st(4u * i + DVC, 0.0f);
+            lds_st(4u * i, __builtin_amdgcn_fmed3f(lds_f(4u * i) + hh * d2, -1.0f, 1.0f));
         }
-        if (lane == 0) unsL[(k + 1) & 1] = 0;  // read by everyone before this step's first barrier
+        if (lane == 0) lds_st(UNS + 4u * ((k + 1) & 1), 0.0f);  // read by everyone before this step's first barrier
         __syncthreads();
         done += 1;
-        if (unsL[k & 1] == 0) {  // allsat before the update; the step was still taken (:148-152)
+        if (lds_f(UNS + 4u * (k & 1)) == 0.0f) {  // allsat before the update; the step was still taken (:148-152)
             const int step = a.step0 + k;
             if (sat < 0) sat = step;
             if (a.stop_mode == ODESAT_STOP_ANY && lane == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
@@ -244,7 +280,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         }
     }
 
-    for (int i = lane; i < a.n; i += NTH) V[i] = vL[i];  // written by this lane in the last update
+    for (int i = lane; i < a.n; i += NTH) V[i] = lds_f(4u * i);  // written by this lane in the last update
     {   // opaque copies: the store addresses are recomputed here instead of being kept live (two
         // VGPRs per tile) across the step loop from the loads above
         float2 *CMs = CM;
@@ -255,7 +291,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     for (int t = 0; t < a.tl; ++t) {  // this lane's own LDS slots: no barrier needed
         const int c0 = tc[min(TR + t, a.ntiles)], c1 = tc[min(TR + t + 1, a.ntiles)];
         const int c = c0 + lane;
-        if (c < c1) CM[c] = memL[t * NTH + lane];
+        if (c < c1) CM[c] = *lds_f2(mem_addr(a, t, lane));
     }
     if (lane == 0) {
         a.act[g] = (uint8_t)act;

@@ -2,13 +2,14 @@
 //
 // One workgroup (512 threads, one per CU) owns ONE replica for a launch of many fixed Euler
 // steps, with its whole state on the CU: voltages v[n] and accumulators dv[n] in LDS, clause
-// memories (xs, xl) in VGPRs (the first TR tiles) and LDS (the remaining TL tiles).  Per step
-// nothing but the clause topology (8 B per clause, L2-resident, shared by every CU) is read
-// from the memory hierarchy; HBM sees the state once at launch start and once at launch end.
+// memories (xs, xl) in VGPRs (the first TR tiles) and LDS (the remaining tl tiles).  Per step
+// nothing but the clause records (8 B per clause, L2-resident, shared by every CU) is read from
+// the memory hierarchy; HBM sees the state once at launch start and once at launch end.
 #pragma once
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
 
@@ -17,11 +18,38 @@ namespace onchip {
 constexpr int NTH = 512;           // threads per workgroup = tile capacity in clauses
 constexpr int TILE_LDS = NTH * 8;  // LDS bytes of one LDS-resident tile of memories (float2 per lane)
 constexpr int SINKS = 32;          // sink words after v and after dv (empty slots of lane l use l % 32)
-constexpr int MAX_N = 16352;       // 4 (n + SINKS) < 65536: LDS byte addresses fit the 16-bit record fields
+constexpr uint32_t DVC = 65532;    // LDS byte offset of dv[0] from v[0]: the ds instructions' 16-bit
+                                   // immediate offset, so one address VGPR serves v and dv
+constexpr int MAX_N = (int)(DVC / 4) - SINKS;  // v and its sinks below DVC
 constexpr size_t LDS_MAX = 160 * 1024;
+
+// LDS map (bytes): v[n + SINKS] at 0 (sinks = 1.0), memory tiles in the gap up to DVC, 2 dv[n +
+// SINKS] (twice dv: see onchip.hip) at DVC, two unsat flags, then the remaining memory tiles.
+struct Lds {
+    uint32_t gap_base, gap_tiles, after_base, after_tiles;
+};
+inline Lds lds_map(int64_t n) {
+    Lds L;
+    const uint32_t vend = (uint32_t)(4 * (n + SINKS));
+    L.gap_base = (vend + 7u) & ~7u;
+    L.gap_tiles = L.gap_base < DVC ? (DVC - L.gap_base) / TILE_LDS : 0;
+    L.after_base = ((DVC + vend + 8u) + 7u) & ~7u;
+    L.after_tiles = L.after_base < LDS_MAX ? (uint32_t)((LDS_MAX - L.after_base) / TILE_LDS) : 0;
+    return L;
+}
+inline size_t lds_bytes(int64_t n, int tl) {
+    const Lds L = lds_map(n);
+    const uint32_t after = tl > (int)L.gap_tiles ? (uint32_t)tl - L.gap_tiles : 0u;
+    return (size_t)L.after_base + (size_t)after * TILE_LDS;
+}
+inline int tl_max(int64_t n) {
+    const Lds L = lds_map(n);
+    return (int)(L.gap_tiles + L.after_tiles) / 4 * 4;
+}
 
 struct Args {
     const uint64_t *rec; // [tiles][NTH] slot-major clause records (make_rec), padded with empty tiles
+    uint32_t rec_bytes;
     const int32_t *tc;   // [ntiles + 1] first internal clause of each tile (constant memory reads)
     float *v0, *v1;      // voltages, [B][n] (par selects the buffer holding the current state)
     float *c0, *c1;      // clause memories, [B][m][2] (xs, xl), internal clause order
@@ -31,17 +59,15 @@ struct Args {
     int32_t *stop;       // first stop step (STOP_ANY), INT_MAX = none
     int32_t n, m, ntiles, tl;  // tiles [0, TR) live in VGPRs, [TR, TR + tl) in LDS
     int32_t step0, nsteps, stop_mode;
-    float dt, zeta, xl_max;
+    float dt, xl_max;
+    Lds lds;
 };
 
-// Register-tile counts compiled (template instantiations; VGPRs ~ 54 + 2 TR, 248 at TR = 96).
+// Register-tile counts compiled (template instantiations; VGPRs ~ 50 + 2 TR, ~243 at TR = 96).
 // Every launch runs all TR register tiles (the empty ones cost a barrier each), so the host picks
 // the smallest TR >= ntiles, else TR = 96 plus LDS tiles for the rest.
 constexpr int TR_CHOICES[] = {8, 16, 24, 32, 40, 48, 56, 64, 72, 80, 88, 96};
 constexpr int TR_MAX = 96;
-
-// LDS bytes of a launch: v and dv with their sinks, two flags, tl tiles of memories.
-inline size_t lds_bytes(int64_t n, int tl) { return (size_t)8 * (n + SINKS) + 8 + (size_t)tl * TILE_LDS; }
 
 // Record of one clause slot (8 bytes): lo = a0 | a1 << 16, hi = a2 | neg0 << 31 | neg1 << 30 |
 // neg2 << 29, with a_j = 4 * var_j the LDS byte address of the literal's voltage.

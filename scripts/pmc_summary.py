@@ -12,7 +12,7 @@ for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
         short = name.split("(")[0].replace("void ", "")
         agg[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in sorted(agg.items()):
-    if any(x in k for x in ("k_step", "k_clause", "k_variable", "k_status", "k_resident")):
+    if any(x in k for x in ("k_step", "k_clause", "k_variable", "k_status", "k_resident", "k_onchip")):
         n = len(next(iter(d.values())))
         print(k, "launches=%d" % n)
         for c, v in sorted(d.items()):
