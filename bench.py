@@ -72,7 +72,7 @@ def barrier_sync(dist, solver, local):
         dist.barrier()
 
 
-STEPS_PER_LAUNCH = 20  # persistent kernel: steps per launch (warmup and timed launches alike)
+STEPS_PER_LAUNCH = 50  # persistent kernel: steps per launch (the state crosses HBM once per launch)
 
 
 def time_gpu(solver, steps, warmup, dist, local, profile):

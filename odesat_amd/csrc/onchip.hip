@@ -73,7 +73,7 @@ __device__ __forceinline__ void lds_st(uint32_t byte_addr, float x) { *reinterpr
 typedef __attribute__((address_space(3))) float2 lfloat2;
 __device__ __forceinline__ float2 *lds_f2(uint32_t byte_addr) { return (float2 *)(reinterpret_cast<lfloat2 *>(byte_addr)); }
 
-// The clause's three voltages (system.rs:46-48): LDS reads issued here, consumed by compute().
+// The clause's three voltages (system.rs:46-48): LDS reads issued here, consumed by front().
 __device__ __forceinline__ void gather(const Slot &S, Gath &G) {
     G.a0 = S.lo & 0xffffu;
     G.a1 = S.lo >> 16;
@@ -84,8 +84,8 @@ __device__ __forceinline__ void gather(const Slot &S, Gath &G) {
     G.v2 = lds_f(G.a2);
 }
 
-// One clause (system.rs:43-88) from its gathered voltages: the three dv terms into Q, the sat fold,
-// and the memory update in place (:84-85, :94-95), in exact rewritten forms (C = mn / 2 exactly):
+// One clause (system.rs:43-88), in two halves that run one tile step apart (so a step interleaves
+// two independent halves of two tiles).  Exact rewritten forms (C = mn / 2 exactly):
 //   C < gamma  <=>  mn < 0.5, so cmax folds the bits of mn (mn >= +0 orders as its bits);
 //   C - 0.25 = 0.5 (mn - 0.5) and C - 0.05 = 0.5 (mn - 0.1) (0.05f is exactly 0.1f / 2), so
 //   h dxs = (h/2) round(A (mn - 0.5)) with A = 20 (xs + eps), and dxl = 2.5 (mn - 0.1);
@@ -94,23 +94,39 @@ __device__ __forceinline__ void gather(const Slot &S, Gath &G) {
 //   the clamps are med3 (finite arguments: the host requires a finite dt).
 // Scalings by 0.5 / 2 / 2.5 / +-1 are exact here (no subnormals: |A| >= 0.02, |mn - c| >= 2^-26 or 0,
 // |xl xs sel| >= 6e-11 or 0).
-__device__ __forceinline__ void compute(const Args &a, const Gath &G, float2 &mem, float h, float hh, Pend &Q,
-                                        uint32_t &cmax) {
+struct Front {  // first half: literal values and their min / second min
+    uint32_t a0, a1, a2, hi;
+    float val0, val1, val2, mn, sec;
+};
+
+__device__ __forceinline__ void front(const Gath &G, Front &F) {
+    F.a0 = G.a0;
+    F.a1 = G.a1;
+    F.a2 = G.a2;
+    F.hi = G.hi;
     const uint32_t s0 = G.hi & 0x80000000u, s1 = (G.hi << 1) & 0x80000000u, s2 = (G.hi << 2) & 0x80000000u;
-    const float val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
-    const float val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
-    const float val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
-    const float mn = fminf(fminf(val0, val1), val2);               // min (:49-55)
-    const float sec = __builtin_amdgcn_fmed3f(val0, val1, val2);    // second min, ties -> min
+    F.val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
+    F.val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
+    F.val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
+    F.mn = fminf(fminf(F.val0, F.val1), F.val2);                  // min (:49-55)
+    F.sec = __builtin_amdgcn_fmed3f(F.val0, F.val1, F.val2);       // second min, ties -> min
+}
+
+// Second half: the three dv terms into Q, the sat fold and the memory update in place
+// (:60-88, :94-95).
+__device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem, float h, float hh, Pend &Q,
+                                     uint32_t &cmax) {
+    const uint32_t s0 = F.hi & 0x80000000u, s1 = (F.hi << 1) & 0x80000000u, s2 = (F.hi << 2) & 0x80000000u;
+    const float mn = F.mn;
     const float xs = mem.x, xl = mem.y;
     const float tt = xl * xs;
-    const float tm = tt * mn, ts = tt * sec;
-    Q.a0 = G.a0;
-    Q.a1 = G.a1;
-    Q.a2 = G.a2;
-    Q.d0 = __uint_as_float(__float_as_uint(val0 != mn ? tm : ts) ^ s0);  // 2 xl xs G (:64-70, :80)
-    Q.d1 = __uint_as_float(__float_as_uint(val1 != mn ? tm : ts) ^ s1);
-    Q.d2 = __uint_as_float(__float_as_uint(val2 != mn ? tm : ts) ^ s2);
+    const float tm = tt * mn, ts = tt * F.sec;
+    Q.a0 = F.a0;
+    Q.a1 = F.a1;
+    Q.a2 = F.a2;
+    Q.d0 = __uint_as_float(__float_as_uint(F.val0 != mn ? tm : ts) ^ s0);  // 2 xl xs G (:64-70, :80)
+    Q.d1 = __uint_as_float(__float_as_uint(F.val1 != mn ? tm : ts) ^ s1);
+    Q.d2 = __uint_as_float(__float_as_uint(F.val2 != mn ? tm : ts) ^ s2);
     cmax = max(cmax, __float_as_uint(mn));  // :88 -- unsat iff max mn >= 0.5
     asm volatile("" : "+v"(cmax));          // fold now: deferred, it would keep every tile's mn live
     const float dxs2 = (20.0f * (xs + 0.001f)) * (mn - 0.5f);  // 2 dxs (:84)
@@ -120,28 +136,30 @@ __device__ __forceinline__ void compute(const Args &a, const Gath &G, float2 &me
     asm volatile("" : "+v"(mem.x), "+v"(mem.y));  // update now: sunk into later tiles it keeps mn live
 }
 
-// One tile step.  In flight: P = tile t's dv terms, Gn = tile t+1's gathered voltages (read one
-// step earlier), ring = the records of tiles t+2 .. t+5.  The critical chain of a step is tile t's
-// dv read-modify-write (:80; three distinct variables per clause, so the updates are independent)
-// between two barriers: its reads go out first and the writes right after they return.  The
-// voltage gathers of tile t+2 follow (v is constant during a pass) and tile t+1's arithmetic runs
-// while they and the writes drain.  The barrier then orders tile t's dv against tile t+1's.
-__device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &slot2, float2 &mem1, Pend &P, Gath &Gn,
-                                          int t, float h, float hh, uint32_t &cmax) {
+// One tile step.  In flight: P = tile t's dv terms, Fn = tile t+1's first half, Gn = tile t+2's
+// gathered voltages, ring = the records of tiles t+3 .. t+6.  The critical chain of a step is tile
+// t's dv read-modify-write (:80; three distinct variables per clause, so the updates are
+// independent) between two barriers: its reads go out first and the writes right after they
+// return.  The voltage gathers of tile t+3 follow (v is constant during a pass), then tile t+1's
+// second half and tile t+2's first half -- independent, so they interleave -- while the writes
+// and the gathers drain.  The barrier then orders tile t's dv against tile t+1's.
+__device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &slot3, float2 &mem1, Pend &P, Front &Fn,
+                                          Gath &Gn, int t, float h, float hh, uint32_t &cmax) {
     const float o0 = lds_f(P.a0 + DVC), o1 = lds_f(P.a1 + DVC), o2 = lds_f(P.a2 + DVC);
     lds_st(P.a0 + DVC, o0 + P.d0);
     lds_st(P.a1 + DVC, o1 + P.d1);
     lds_st(P.a2 + DVC, o2 + P.d2);
     __builtin_amdgcn_sched_barrier(0);
-    Gath G2;
-    gather(slot2, G2);
-    slot2 = load_rec(R, t + 6);
+    Gath G3;
+    gather(slot3, G3);
+    slot3 = load_rec(R, t + 7);
     __builtin_amdgcn_sched_barrier(0);
-    compute(a, Gn, mem1, h, hh, P, cmax);  // P <- tile t+1's terms (tile t's were written above)
-    __builtin_amdgcn_sched_barrier(0);     // a tile's work stays between its barriers
+    back(a, Fn, mem1, h, hh, P, cmax);  // P <- tile t+1's terms (tile t's were written above)
+    front(Gn, Fn);                      // Fn <- tile t+2's first half
+    __builtin_amdgcn_sched_barrier(0);  // a tile's work stays between its barriers
     __syncthreads();
     __builtin_amdgcn_sched_barrier(0);
-    Gn = G2;
+    Gn = G3;
 }
 
 // LDS byte address of this lane's slot in LDS memory tile lt (onchip.hpp, Lds).
@@ -156,22 +174,22 @@ __device__ __forceinline__ uint32_t mem_addr(const Args &a, int lt, int lane) {
 // the copies that merge mr[] there double its VGPR footprint.
 template <int TR, int T>
 __device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&mr)[TR], Slot (&ring)[4], Pend &P,
-                                         Gath &Gn, float h, float hh, int lane, uint32_t &cmax) {
+                                         Front &Fn, Gath &Gn, float h, float hh, int lane, uint32_t &cmax) {
     if constexpr (T + 1 < TR) {
-        tile_step(a, R, ring[(T + 2) % 4], mr[T + 1], P, Gn, T, h, hh, cmax);
+        tile_step(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, cmax);
     } else {  // tile TR is the first LDS tile (if any)
         float2 m = make_float2(0.0f, 0.0f);
         if (a.tl > 0) m = *lds_f2(mem_addr(a, 0, lane));
-        tile_step(a, R, ring[(T + 2) % 4], m, P, Gn, T, h, hh, cmax);
+        tile_step(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, cmax);
         if (a.tl > 0) *lds_f2(mem_addr(a, 0, lane)) = m;
     }
 }
 
 template <int TR, int... Ts>
 __device__ __forceinline__ void reg_tiles(std::integer_sequence<int, Ts...>, const Args &a, const Recs &R,
-                                          float2 (&mr)[TR], Slot (&ring)[4], Pend &P, Gath &Gn, float h, float hh,
-                                          int lane, uint32_t &cmax) {
-    (reg_tile<TR, Ts>(a, R, mr, ring, P, Gn, h, hh, lane, cmax), ...);
+                                          float2 (&mr)[TR], Slot (&ring)[4], Pend &P, Front &Fn, Gath &Gn, float h,
+                                          float hh, int lane, uint32_t &cmax) {
+    (reg_tile<TR, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax), ...);
 }
 
 // One RHS pass + memory update over every tile; ends with a barrier (dv complete).
@@ -189,13 +207,18 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
 #pragma unroll
     for (int s = 0; s < 4; ++s) ring[s] = load_rec(R, s);
     Pend P;
-    Gath G0, Gn;
+    Gath G0, G1, Gn;
     gather(ring[0], G0);
     ring[0] = load_rec(R, 4);
-    gather(ring[1], Gn);
+    gather(ring[1], G1);
     ring[1] = load_rec(R, 5);
-    compute(a, G0, mr[0], h, hh, P, cmax);
-    reg_tiles<TR>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Gn, h, hh, lane, cmax);
+    gather(ring[2], Gn);
+    ring[2] = load_rec(R, 6);
+    Front F0, Fn;
+    front(G0, F0);
+    front(G1, Fn);
+    back(a, F0, mr[0], h, hh, P, cmax);
+    reg_tiles<TR>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax);
     // LDS tiles [TR, TR + tl): tl is a multiple of 4 (the host pads the tiling)
     const int NT = TR + a.tl;
     const int last = a.tl - 1;
@@ -205,7 +228,7 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
             const int t = t0 + u;
             const uint32_t ma = mem_addr(a, min(t + 1 - TR, last), lane);
             float2 m = *lds_f2(ma);
-            tile_step(a, R, ring[(u + 2) % 4], m, P, Gn, t, h, hh, cmax);
+            tile_step(a, R, ring[(u + 3) % 4], m, P, Fn, Gn, t, h, hh, cmax);
             *lds_f2(ma) = m;
         }
     }
