@@ -27,7 +27,7 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--batch", type=int, default=1024, help="replicas per GPU")
     p.add_argument("--config", default="config2")
     p.add_argument("--dtype", default="f32", choices=["f32", "f64"])
@@ -35,11 +35,14 @@ def parse():
     p.add_argument("--cpu-replicas", type=int, default=16)
     p.add_argument("--cpu-steps", type=int, default=300)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_r01.json"),
-                   help="JSON with the dominant kernel's HBM bytes per step from the PMC passes (profiles/)")
+    p.add_argument("--traffic-dir", default=os.path.join(ROOT, "profiles"),
+                   help="directory of traffic_<kernel>.json files: the dominant kernel's HBM bytes per launch "
+                        "from the PMC passes (scripts/make_traffic.py)")
     p.add_argument("--alg", default="auto", choices=["auto", "onchip", "resident", "fused", "twopass"],
                    help="force an algorithm (A/B); auto = the solver's default")
     p.add_argument("--extra-batch", type=int, default=256, help="also time this B (configs[1]); 0 = off")
+    p.add_argument("--no-ab", action="store_true",
+                   help="skip the in-run A/B line of the HBM-streaming kernel (k_resident) on the same workload")
     return p.parse_args()
 
 
@@ -124,14 +127,14 @@ def main():
     f = cnf.CNFFormula.from_arrays(cp, v_, n_, n)
     B = args.batch
 
-    def run_batch(batch, profile):
-        from odesat_amd import device_count
+    def run_batch(batch, profile, alg_name=None):
+        from odesat_amd import _lib, device_count
         s = Solver(f, batch, args.dtype, device=local % max(1, device_count()))
         if args.chunk:
             s.set_chunk_replicas(args.chunk)
-        if args.alg != "auto":
-            from odesat_amd import _lib
-            s.set_algorithm(getattr(_lib, "ODESAT_ALG_" + args.alg.upper()))
+        alg_name = alg_name or args.alg
+        if alg_name != "auto":
+            s.set_algorithm(getattr(_lib, "ODESAT_ALG_" + alg_name.upper()))
         s.init_state(42, replica0=shard_range(rank, world, batch)[0])
         wall, ms, launches = time_gpu(s, args.steps, args.warmup, dist, local, profile)
         bytes_step = s.clause_kernel_bytes()
@@ -139,33 +142,57 @@ def main():
         s.close()
         return wall, ms, launches, bytes_step, alg
 
+    def roofline(alg, ms, launches, clause_bytes_step):
+        """Dominant kernel: algorithmic bytes per launch ((8n + 16m) B per fp32
+        replica-step -- v, xs, xl read and written once -- x the replica-steps of one launch) / its mean
+        launch time (HIP events on the solver's stream); traffic = PMC HBM bytes per launch of the same
+        kernel and workload (profiles/traffic_<kernel>.json), or None."""
+        from odesat_amd._lib import ODESAT_ALG_ONCHIP, ODESAT_ALG_RESIDENT
+        kernel = {ODESAT_ALG_RESIDENT: "k_resident (persistent; v in LDS, clause memories streamed through HBM "
+                                       "every step)",
+                  ODESAT_ALG_ONCHIP: "k_onchip (persistent; the whole replica state on one CU: v/dv in LDS, "
+                                     "clause memories in VGPRs)"}.get(alg, "k_step (fused RHS + Euler update)")
+        short = kernel.split(" ")[0]
+        nlaunch = int(launches[0])
+        per_launch_s = ms[0] / 1e3 / nlaunch
+        steps_per_launch = args.steps / nlaunch
+        per_launch_bytes = clause_bytes_step * steps_per_launch
+        achieved = per_launch_bytes / per_launch_s / 1e9
+        traffic = None
+        tpath = os.path.join(args.traffic_dir, f"traffic_{short}.json")
+        if os.path.exists(tpath):
+            with open(tpath) as fh:
+                tj = json.load(fh)
+            if tj.get("batch") == B and tj.get("dtype") == args.dtype and tj.get("config") == args.config \
+                    and tj.get("steps_per_launch") == steps_per_launch:
+                traffic = tj["hbm_bytes_per_launch"]
+        r = {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+             "algorithmic_bytes_per_launch": per_launch_bytes, "mean_launch_us": per_launch_s * 1e6,
+             "launches": nlaunch, "steps_per_launch": steps_per_launch}
+        if alg == ODESAT_ALG_ONCHIP:
+            r["note"] = ("k_onchip keeps v, dv and the clause memories on the CU for a whole launch: HBM moves "
+                         "the state once per launch (traffic), so the algorithmic rate can exceed the HBM peak; "
+                         "the binding resources are the CU's LDS and VALU issue (DESIGN.md). ab_hbm_streaming is "
+                         "the HBM-bound kernel on the same workload.")
+        return r
+
     wall, ms, launches, clause_bytes_step, alg = run_batch(B, True)
     wall_max = max_over_ranks(dist, wall)
     total_replica_steps = B * world * args.steps
     value = total_replica_steps / wall_max
     ms_per_step = wall_max * 1e3 / args.steps
-
-    # roofline of the dominant kernel: algorithmic bytes per launch ((8n + 16m) B per
-    # fp32 replica-step x the replica-steps of one launch) / its mean launch time (HIP events on the
-    # solver's stream)
-    from odesat_amd._lib import ODESAT_ALG_ONCHIP, ODESAT_ALG_RESIDENT
-    kernel = {ODESAT_ALG_RESIDENT: "k_resident (persistent, LDS-resident voltages, var-disjoint clause tiles)",
-              ODESAT_ALG_ONCHIP: "k_onchip (persistent, whole replica state on one CU: v/dv in LDS, clause "
-                                 "memories in VGPRs)"}.get(alg, "k_step (fused RHS + Euler update, variable-major)")
-    nlaunch = int(launches[0])
-    per_launch_s = ms[0] / 1e3 / nlaunch
-    steps_per_launch = args.steps / nlaunch
-    per_launch_bytes = clause_bytes_step * steps_per_launch
-    achieved = per_launch_bytes / per_launch_s / 1e9
-    traffic = None
-    if args.traffic and os.path.exists(args.traffic):
-        with open(args.traffic) as fh:
-            tj = json.load(fh)
-        if tj.get("kernel", "").split(" ")[0] == kernel.split(" ")[0] and tj.get("batch") == B \
-                and tj.get("dtype") == args.dtype and tj.get("config") == args.config:
-            traffic = tj["hbm_bytes_per_step"] * steps_per_launch  # PMC-measured, same kernel and workload
+    roof = roofline(alg, ms, launches, clause_bytes_step)
     tsize = 4 if args.dtype == "f32" else 8
     step_bytes = B * (2 * n + 4 * m) * tsize  # algorithmic per GPU-step: v, xs, xl read + written once
+
+    from odesat_amd._lib import ODESAT_ALG_ONCHIP
+    ab = None
+    if alg == ODESAT_ALG_ONCHIP and not args.no_ab:
+        w3, ms3, l3, b3, a3 = run_batch(B, True, "resident")
+        w3 = max_over_ranks(dist, w3)
+        ab = {"value": B * world * args.steps / w3, "ms_per_step": w3 * 1e3 / args.steps,
+              "roofline": roofline(a3, ms3, l3, b3)}
 
     extra = None
     if args.extra_batch and args.extra_batch != B:
@@ -197,15 +224,12 @@ def main():
                                    f"Euler dt=0.01, all replicas stepped (no early exit)",
                        "global_batch": B * world, "batch_per_gpu": B, "n": n, "m": m,
                        "parallelism": f"replica-sharded x{world} (no collectives)"},
-            "roofline": {"bound": "hbm", "kernel": kernel,
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes_per_launch": per_launch_bytes,
-                         "mean_launch_us": per_launch_s * 1e6, "launches": nlaunch},
+            "roofline": roof,
             "step_kernels_ms": {"clause": ms[0], "variable": ms[1], "status": ms[2]},
             "step_algorithmic_GBps": step_bytes * args.steps / wall / 1e9,
             "cpu_baseline": cpu,
             "extra_batch": extra,
+            "ab_hbm_streaming": ab,
         }
         print(json.dumps(out))
     if dist is not None:

@@ -9,7 +9,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        short = name.split("(")[0].replace("void ", "")
+        short = name.replace("(anonymous namespace)", "anon").split("(")[0].replace("void ", "")
         agg[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in sorted(agg.items()):
     if any(x in k for x in ("k_step", "k_clause", "k_variable", "k_status", "k_resident", "k_onchip")):

@@ -22,6 +22,6 @@ with Solver(f, B, os.environ.get("DTYPE", "f32")) as s:
     if "ALG" in os.environ:
         s.set_algorithm(int(os.environ["ALG"]))
     s.init_state(42)
-    s.simulate(dt=0.01, max_steps=K, stop=ODESAT_STOP_NONE)
+    s.simulate(dt=0.01, max_steps=K, stop=ODESAT_STOP_NONE, poll_interval=K)  # one launch of K steps
     s.synchronize()
 print("done", B, K, CHUNK, SCHED)
