@@ -184,6 +184,52 @@ int odesat_set_algorithm(odesat_solver *s, int alg);
 int odesat_get_algorithm(const odesat_solver *s);
 int odesat_group_width(const odesat_solver *s);
 
+/* --------------------------------------------- one instance across GPUs ------- */
+
+/* The fixed Euler step (system.rs:141-154) of ONE replica whose formula is partitioned over `world`
+ * ranks, one process per GPU; the caller runs the collective (RCCL all-gather / all-reduce on the
+ * device buffers; odesat_amd/partition.py builds the local topology below).  Two partitions:
+ *   ODESAT_PART_CLAUSES    rank r holds a slice of the clauses and a full v[n].  odesat_part_rhs
+ *                          writes the partial dv of every variable (out[0..n)) and the rank's unsat
+ *                          count (out[n]); the caller all-reduces (sum) out and calls
+ *                          odesat_part_apply.  Matches the reference within a tolerance (the sum
+ *                          across ranks reorders the fold; bit-exact at world = 1).
+ *   ODESAT_PART_VARIABLES  rank r holds variables [v0, v1) and every clause touching them.
+ *                          odesat_part_rhs writes the updated voltages of [v0, v1) (out[0..S)) and
+ *                          its unsat count (out[S]); the caller all-gathers the world blocks of
+ *                          S + 1 floats, which are the next step's voltages (variable i at
+ *                          i + i / S).  Bit-exact for any world size.
+ * world = the number of ranks.  Local topology: clause_ptr[mloc + 1], var[L], neg[L] of the local clauses in the reference's clause
+ * order; var_ptr[v1 - v0 + 1] / inc_slot[] = for each variable of [v0, v1), its local literal slots
+ * in clause-then-literal order; block = S (VARIABLES) or 0 (CLAUSES, plain v[n]).  m = the global
+ * clause count (xl's upper clamp, system.rs:95).  Device pointers v / out / dvsum are the caller's;
+ * `stream` is a hipStream_t (NULL = the default stream). */
+#define ODESAT_PART_CLAUSES 0
+#define ODESAT_PART_VARIABLES 1
+typedef struct odesat_part odesat_part;
+int odesat_part_create(int device, int world, int64_t n, int64_t m, int64_t mloc, const int64_t *clause_ptr,
+                       const int64_t *var, const uint8_t *neg, int64_t v0, int64_t v1,
+                       const int64_t *var_ptr, const int64_t *inc_slot, int64_t block,
+                       odesat_part **out);
+void odesat_part_destroy(odesat_part *p);
+int64_t odesat_part_device_bytes(const odesat_part *p);
+/* the local clauses' memories, in local clause order (f64 host arrays of mloc) */
+int odesat_part_set_memories(odesat_part *p, const double *xs, const double *xl);
+int odesat_part_get_memories(odesat_part *p, double *xs, double *xl);
+/* Enqueue one right-hand side + memory update; apply = 0 (CLAUSES) or 1 (VARIABLES).  Before it,
+ * the previous step's global unsat count (read from v's flag slots or out[n]) is folded into the
+ * replica's bookkeeping; stop = 1: the first allsat step freezes the replica (simulate,
+ * system.rs:193) and later steps are no-ops, so callers may poll at any interval. */
+int odesat_part_rhs(odesat_part *p, const float *v, float *out, double dt, double zeta, int apply,
+                    int stop, void *stream);
+/* CLAUSES: v[i] = clamp(v[i] + dt * dvsum[i]) after the all-reduce (system.rs:96) */
+int odesat_part_apply(odesat_part *p, float *v, const float *dvsum, double dt, void *stream);
+/* Restart the bookkeeping (steps done 0, no sat step, not frozen). */
+int odesat_part_reset(odesat_part *p, void *stream);
+/* Fold the last step's unsat count and read the bookkeeping (synchronises `stream`). */
+int odesat_part_status(odesat_part *p, const float *v, const float *out, int apply, int stop,
+                       void *stream, int64_t *steps_done, int64_t *sat_step, int32_t *frozen);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,7 @@ ODESAT_F32, ODESAT_F64 = 0, 1
 ODESAT_STOP_EACH, ODESAT_STOP_ANY, ODESAT_STOP_NONE = 0, 1, 2
 ODESAT_SCHED_AUTO, ODESAT_SCHED_STEP_MAJOR, ODESAT_SCHED_CHUNK_MAJOR = 0, 1, 2
 ODESAT_ALG_FUSED, ODESAT_ALG_TWOPASS, ODESAT_ALG_RESIDENT, ODESAT_ALG_ONCHIP = 0, 1, 2, 3
+ODESAT_PART_CLAUSES, ODESAT_PART_VARIABLES = 0, 1
 
 
 class OdesatError(RuntimeError):
@@ -75,15 +76,45 @@ SIGNATURES = {
     "odesat_set_algorithm": (C.c_int, [_P, C.c_int]),
     "odesat_get_algorithm": (C.c_int, [_P]),
     "odesat_group_width": (C.c_int, [_P]),
+    "odesat_part_create": (C.c_int, [C.c_int, C.c_int, _i64, _i64, _i64, _i64p, _i64p, _u8p, _i64, _i64, _i64p,
+                                     _i64p, _i64, C.POINTER(_P)]),
+    "odesat_part_destroy": (None, [_P]),
+    "odesat_part_device_bytes": (_i64, [_P]),
+    "odesat_part_set_memories": (C.c_int, [_P, _dp, _dp]),
+    "odesat_part_get_memories": (C.c_int, [_P, _dp, _dp]),
+    "odesat_part_rhs": (C.c_int, [_P, _P, _P, C.c_double, C.c_double, C.c_int, C.c_int, _P]),
+    "odesat_part_apply": (C.c_int, [_P, _P, _P, C.c_double, _P]),
+    "odesat_part_reset": (C.c_int, [_P, _P]),
+    "odesat_part_status": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, _P, _i64p, _i64p, C.POINTER(C.c_int32)]),
 }
 
 _lib = None
+
+
+def _adopt_torch_runtime():
+    """One HIP runtime per process.  PyTorch ships its own libamdhip64 and loads it by file name; if
+    this library (linked against the system libamdhip64.so.7) is loaded first, a later `import
+    torch` brings a second runtime and torch then sees no GPU.  Loading torch's runtime first, by
+    path and RTLD_GLOBAL (torch itself is not imported), makes both resolve to it in either import
+    order.  ODESAT_HIP_RUNTIME=system keeps the system runtime (processes that never use torch)."""
+    if os.environ.get("ODESAT_HIP_RUNTIME") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    d = os.path.join(os.path.dirname(spec.origin), "lib")
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        p = os.path.join(d, name)
+        if os.path.exists(p):
+            C.CDLL(p, mode=C.RTLD_GLOBAL)
 
 
 def lib():
     """Load the in-tree libodesat_hip.so (raises if it was not built)."""
     global _lib
     if _lib is None:
+        _adopt_torch_runtime()
         if not os.path.exists(LIB_PATH):
             raise OdesatError(ODESAT_EDEVICE, f"{LIB_PATH} not built: run `make -C odesat_amd/csrc` "
                                               "or `python -c 'import __graft_entry__ as g; g.build()'`")

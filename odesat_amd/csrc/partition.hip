@@ -1,0 +1,391 @@
+// partition.hip -- one very large instance split across GPUs (BASELINE configs[4]):
+// the fixed Euler step (system.rs:141-154) of a single replica whose clauses are partitioned over
+// `world` ranks, one process per GPU.  The collective is the caller's (torch.distributed over RCCL);
+// this file provides the per-rank kernels and their C ABI (include/odesat.h, odesat_part_*).
+//
+// Two partitions (the host builds the local topology, odesat_amd/partition.py):
+//   CLAUSES    rank r owns a contiguous slice of the clauses and a full copy of v.  A step writes
+//              the PARTIAL dv of every variable (its clauses' terms, folded in clause order) plus
+//              its unsat flag; the ranks all-reduce (sum) that vector and apply the same update.
+//              The summation order across ranks differs from the reference's fold: results match
+//              it within a tolerance (bit-exact at world = 1).
+//   VARIABLES  rank r owns variables [v0, v1) and EVERY clause touching them (clauses that span
+//              ranks are evaluated -- identically -- by each rank that holds them).  A step folds
+//              the complete dv of its own variables in the reference's clause order and writes
+//              their updated voltages plus its unsat flag into a send block; the ranks
+//              all-gather the blocks, which form the next step's voltage array.  Bit-exact for any
+//              world size, and the exchange is half an all-reduce's bytes.
+// Gathered voltage layout (VARIABLES): world blocks of (S voltages, 1 unsat flag), so variable i
+// sits at i + i / S.  CLAUSES uses a plain v[n] (stride 0).
+//
+// Arithmetic: the reference's expressions in the reference's order (system.rs:43-96), f32, with
+// the rigidity term -- identical to the oracle's f32 restatement for any state.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/odesat.h"
+#include "cnf.hpp"
+
+using odesat::fail;
+
+// Device bookkeeping of the replica (the partitioned analogue of act / sat_step / steps_done).
+struct PartStat {
+    int64_t steps_done;  // steps taken (a frozen replica takes no more)
+    int64_t sat_step;    // 0-based step whose pre-update state was allsat, -1 = none yet
+    int32_t frozen;      // simulate() has stopped (system.rs:193): later steps are no-ops
+    int32_t pad;
+};
+
+struct odesat_part {
+    int device = 0, world = 1;
+    int64_t n = 0, m = 0, mloc = 0, L = 0, v0 = 0, v1 = 0, S = 0, voff = 0;
+    int32_t *cptr = nullptr, *lits = nullptr, *cstart = nullptr, *deg = nullptr, *islot = nullptr;
+    float *xs = nullptr, *xl = nullptr, *w = nullptr;
+    PartStat *stat = nullptr;
+    int64_t bytes = 0;
+};
+
+namespace {
+
+#define PART_TRY(expr)                                                                        \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(ODESAT_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+// Folds the previous step's global unsat flag(s) (VARIABLES: the world flag slots of the gathered
+// voltages; CLAUSES: dvsum[n] after the all-reduce) into the replica's bookkeeping, then counts the
+// step about to be taken.  stop = 1: an allsat step freezes the replica (simulate, system.rs:193).
+__global__ void k_part_status(PartStat *st, const float *flags, int64_t stride, int count, int stop, int take) {
+    if (threadIdx.x != 0) return;
+    if (st->steps_done > 0 && !st->frozen && st->sat_step < 0) {
+        float u = 0.0f;
+        for (int r = 0; r < count; ++r) u += flags[(int64_t)r * stride];
+        if (u == 0.0f) {
+            st->sat_step = st->steps_done - 1;
+            if (stop) st->frozen = 1;
+        }
+    }
+    if (take && !st->frozen) st->steps_done += 1;
+}
+
+// Local clauses, one thread each: C (system.rs:43-60), each literal's term xl xs G + (1 + zeta xl)
+// (1 - xs) R into w[slot] (:62-80), the memory update (:84-85, :94-95) and the unsat flag (:88).
+// lits hold the voltage's index in v's layout (premapped on the host) << 1 | neg.
+__global__ __launch_bounds__(256) void k_part_clause(const int32_t *__restrict__ cptr, const int32_t *__restrict__ lits,
+                                                     const float *__restrict__ v, float *__restrict__ xs,
+                                                     float *__restrict__ xl, float *__restrict__ w, int32_t mloc, float dt,
+                                                     float zeta, float xl_max, float *__restrict__ unsat,
+                                                     const PartStat *__restrict__ st) {
+    if (st->frozen) return;  // uniform
+    const int32_t c = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    bool uns = false;
+    if (c < mloc) {
+        const int32_t s0 = cptr[c], s1 = cptr[c + 1];
+        const float one = 1.0f, halfc = 0.5f;
+        float mn = __builtin_huge_valf(), sec = __builtin_huge_valf();
+        for (int32_t s = s0; s < s1; ++s) {  // :43-57, strict <
+            const int32_t lit = lits[s];
+            const float q = (lit & 1) ? -1.0f : 1.0f;
+            const float val = one - q * v[lit >> 1];
+            const bool lt = val < mn;
+            sec = lt ? mn : (val < sec ? val : sec);
+            mn = lt ? val : mn;
+        }
+        const float C = halfc * mn;  // :60
+        const float xs_m = xs[c], xl_m = xl[c];
+        for (int32_t s = s0; s < s1; ++s) {  // :62-80
+            const int32_t lit = lits[s];
+            const float q = (lit & 1) ? -1.0f : 1.0f;
+            const float vi = v[lit >> 1];
+            const float val = one - q * vi;
+            const float g = halfc * q * (val != mn ? mn : sec);
+            const float r = (C == one - q * vi) ? halfc * (q - vi) : 0.0f;
+            w[s] = xl_m * xs_m * g + (one + zeta * xl_m) * (one - xs_m) * r;
+        }
+        const float dxs = 20.0f * (xs_m + 0.001f) * (C - 0.25f);  // :84
+        const float dxl = 5.0f * (C - 0.05f);                      // :85
+        xs[c] = fminf(fmaxf(xs_m + dt * dxs, 0.001f), 1.0f - 0.001f);  // :94
+        xl[c] = fminf(fmaxf(xl_m + dt * dxl, one), xl_max);           // :95
+        uns = !(C < 0.25f);                                            // :88
+    }
+    // one flag store per workgroup that has an unsat clause, skipped once the flag is visibly set
+    if (__syncthreads_or(uns) && threadIdx.x == 0 && *(volatile float *)unsat == 0.0f) *unsat = 1.0f;
+}
+
+// Variables [v0, v1), one thread each: dv = the fold of the local terms in clause order (:33, :80).
+// The incidences are sliced-ELL: chunk k of 64 variables stores its j-th incidences contiguously
+// ([chunk][j][64], padded to the chunk's largest degree), so the slot loads coalesce.
+// CLAUSES (apply == 0): out[i] = partial dv[i].  VARIABLES (apply == 1): out[i - v0] = the updated
+// voltage (:96), v[i + voff] being variable i in the gathered layout.
+__global__ __launch_bounds__(256) void k_part_var(const int32_t *__restrict__ cstart, const int32_t *__restrict__ deg,
+                                                  const int32_t *__restrict__ islot, const float *__restrict__ w,
+                                                  const float *__restrict__ v, int32_t voff, int32_t v0, int32_t v1,
+                                                  float dt, int apply, float *__restrict__ out,
+                                                  const PartStat *__restrict__ st) {
+    const int32_t k = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int32_t i = v0 + k;
+    if (i >= v1) return;
+    if (st->frozen) {  // the replica stopped: v is re-sent unchanged, no dv
+        if (apply) out[k] = v[i + voff];
+        else out[i] = 0.0f;
+        return;
+    }
+    const int32_t *p = islot + cstart[k >> 6] + (k & 63);
+    const int32_t d = deg[k];
+    float dv = 0.0f;
+    for (int32_t j = 0; j < d; ++j) dv += w[p[64 * j]];
+    if (apply) out[k] = fminf(fmaxf(v[i + voff] + dt * dv, -1.0f), 1.0f);
+    else out[i] = dv;
+}
+
+// CLAUSES: v[i] = clamp(v[i] + dt * dvsum[i]) after the all-reduce (:96).
+__global__ __launch_bounds__(256) void k_part_apply(float *__restrict__ v, const float *__restrict__ dvsum, int32_t n,
+                                                    float dt, const PartStat *__restrict__ st) {
+    const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (st->frozen) return;
+    if (i < n) v[i] = fminf(fmaxf(v[i] + dt * dvsum[i], -1.0f), 1.0f);
+}
+
+template <typename T> int upload(odesat_part *p, T **dst, const int64_t *src, int64_t count) {
+    std::vector<T> h((size_t)count);
+    for (int64_t k = 0; k < count; ++k) h[k] = (T)src[k];
+    PART_TRY(hipMalloc((void **)dst, std::max<size_t>(16, (size_t)count * sizeof(T))));
+    p->bytes += (int64_t)count * (int64_t)sizeof(T);
+    if (count) PART_TRY(hipMemcpy(*dst, h.data(), (size_t)count * sizeof(T), hipMemcpyHostToDevice));
+    return ODESAT_OK;
+}
+
+unsigned blocks_for(int64_t items) { return (unsigned)std::max<int64_t>(1, (items + 255) / 256); }
+
+}  // namespace
+
+extern "C" void odesat_part_destroy(odesat_part *p) {
+    if (!p) return;
+    (void)hipSetDevice(p->device);
+    void *ptrs[] = {p->cptr, p->lits, p->cstart, p->deg, p->islot, p->xs, p->xl, p->w, p->stat};
+    for (void *q : ptrs)
+        if (q) (void)hipFree(q);
+    delete p;
+}
+
+extern "C" int odesat_part_create(int device, int world, int64_t n, int64_t m, int64_t mloc, const int64_t *clause_ptr, const int64_t *var,
+                                  const uint8_t *neg, int64_t v0, int64_t v1, const int64_t *var_ptr,
+                                  const int64_t *inc_slot, int64_t block, odesat_part **out) {
+    if (!out) return fail(ODESAT_EINVAL, "null out");
+    *out = nullptr;
+    if (world < 1 || n <= 0 || m < 0 || mloc < 0 || mloc > m || !clause_ptr || v0 < 0 || v1 < v0 || v1 > n ||
+        block < 0 || (block > 0 && v1 - v0 > block))
+        return fail(ODESAT_EINVAL, "bad partition arguments");
+    if (n >= (1ll << 29) || m >= INT32_MAX) return fail(ODESAT_EINVAL, "formula too large");
+    const int64_t L = clause_ptr[mloc] - clause_ptr[0];
+    if (L < 0 || L >= INT32_MAX || (L && (!var || !neg))) return fail(ODESAT_EINVAL, "bad local clause arrays");
+    for (int64_t c = 0; c < mloc; ++c)
+        if (clause_ptr[c + 1] < clause_ptr[c]) return fail(ODESAT_EINVAL, "clause_ptr must be non-decreasing");
+    for (int64_t s = 0; s < L; ++s)
+        if (var[s] < 0 || var[s] >= n) return fail(ODESAT_EINVAL, "variable out of range");
+    const int64_t nv = v1 - v0;
+    if (nv && (!var_ptr || var_ptr[0] != 0)) return fail(ODESAT_EINVAL, "bad var_ptr");
+    const int64_t ninc = nv ? var_ptr[nv] : 0;
+    for (int64_t k = 0; k < ninc; ++k)
+        if (inc_slot[k] < 0 || inc_slot[k] >= L) return fail(ODESAT_EINVAL, "incidence slot out of range");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(ODESAT_EDEVICE, "no HIP device available (odesat_amd has no CPU fallback)");
+    if (device < 0 || device >= ndev) return fail(ODESAT_EINVAL, "device index out of range");
+    PART_TRY(hipSetDevice(device));
+    auto *p = new (std::nothrow) odesat_part();
+    if (!p) return fail(ODESAT_ENOMEM, "out of memory");
+    p->device = device;
+    p->world = world;
+    p->n = n;
+    p->m = m;
+    p->mloc = mloc;
+    p->L = L;
+    p->v0 = v0;
+    p->v1 = v1;
+    p->S = block;
+    // literals carry the voltage's index in v's layout: VARIABLES' gathered blocks put variable i at
+    // i + i / S (so no division runs on the device)
+    std::vector<int64_t> cp((size_t)mloc + 1), lits((size_t)L);
+    for (int64_t c = 0; c <= mloc; ++c) cp[c] = clause_ptr[c] - clause_ptr[0];
+    for (int64_t s = 0; s < L; ++s) {
+        const int64_t gi = block > 0 ? var[s] + var[s] / block : var[s];
+        lits[s] = (gi << 1) | (neg[s] ? 1 : 0);
+    }
+    // sliced-ELL incidences: chunks of 64 variables, [chunk][j][64], padded with slot 0 (never read:
+    // a lane stops at its own degree)
+    const int64_t nchunk = (nv + 63) / 64;
+    std::vector<int64_t> deg((size_t)std::max<int64_t>(nv, 1), 0), cstart((size_t)nchunk + 1, 0);
+    for (int64_t k = 0; k < nv; ++k) deg[k] = var_ptr[k + 1] - var_ptr[k];
+    for (int64_t ch = 0; ch < nchunk; ++ch) {
+        int64_t mx = 0;
+        for (int64_t k = ch * 64; k < std::min(nv, ch * 64 + 64); ++k) mx = std::max(mx, deg[k]);
+        cstart[ch + 1] = cstart[ch] + 64 * mx;
+    }
+    if (cstart[nchunk] >= INT32_MAX) {
+        odesat_part_destroy(p);
+        return fail(ODESAT_EINVAL, "too many incidences");
+    }
+    std::vector<int64_t> ell((size_t)std::max<int64_t>(cstart[nchunk], 1), 0);
+    for (int64_t k = 0; k < nv; ++k)
+        for (int64_t j = 0; j < deg[k]; ++j) ell[cstart[k / 64] + 64 * j + (k % 64)] = inc_slot[var_ptr[k] + j];
+    p->voff = block > 0 ? v0 / block : 0;
+    int rc;
+    if ((rc = upload(p, &p->cptr, cp.data(), mloc + 1)) || (rc = upload(p, &p->lits, lits.data(), L)) ||
+        (rc = upload(p, &p->cstart, cstart.data(), nchunk + 1)) || (rc = upload(p, &p->deg, deg.data(), nv)) ||
+        (rc = upload(p, &p->islot, ell.data(), cstart[nchunk]))) {
+        odesat_part_destroy(p);
+        return rc;
+    }
+    for (float **b : {&p->xs, &p->xl}) {
+        if (hipMalloc((void **)b, std::max<size_t>(16, (size_t)mloc * 4)) != hipSuccess) {
+            odesat_part_destroy(p);
+            return fail(ODESAT_ENOMEM, "hipMalloc failed");
+        }
+        p->bytes += mloc * 4;
+    }
+    if (hipMalloc((void **)&p->stat, sizeof(PartStat)) != hipSuccess ||
+        hipMemset(p->stat, 0, sizeof(PartStat)) != hipSuccess) {
+        odesat_part_destroy(p);
+        return fail(ODESAT_ENOMEM, "hipMalloc failed");
+    }
+    {
+        const PartStat s0{0, -1, 0, 0};
+        if (hipMemcpy(p->stat, &s0, sizeof(s0), hipMemcpyHostToDevice) != hipSuccess) {
+            odesat_part_destroy(p);
+            return fail(ODESAT_EDEVICE, "hipMemcpy failed");
+        }
+    }
+    if (hipMalloc((void **)&p->w, std::max<size_t>(16, (size_t)L * 4)) != hipSuccess) {
+        odesat_part_destroy(p);
+        return fail(ODESAT_ENOMEM, "hipMalloc failed");
+    }
+    p->bytes += L * 4;
+    *out = p;
+    return ODESAT_OK;
+}
+
+extern "C" int64_t odesat_part_device_bytes(const odesat_part *p) { return p ? p->bytes : -1; }
+
+extern "C" int odesat_part_set_memories(odesat_part *p, const double *xs, const double *xl) {
+    if (!p || !xs || !xl) return fail(ODESAT_EINVAL, "null argument");
+    PART_TRY(hipSetDevice(p->device));
+    std::vector<float> a((size_t)p->mloc), b((size_t)p->mloc);
+    for (int64_t c = 0; c < p->mloc; ++c) {
+        a[c] = (float)xs[c];
+        b[c] = (float)xl[c];
+    }
+    if (p->mloc) {
+        PART_TRY(hipMemcpy(p->xs, a.data(), p->mloc * 4, hipMemcpyHostToDevice));
+        PART_TRY(hipMemcpy(p->xl, b.data(), p->mloc * 4, hipMemcpyHostToDevice));
+    }
+    return ODESAT_OK;
+}
+
+extern "C" int odesat_part_get_memories(odesat_part *p, double *xs, double *xl) {
+    if (!p) return fail(ODESAT_EINVAL, "null part");
+    PART_TRY(hipSetDevice(p->device));
+    PART_TRY(hipDeviceSynchronize());
+    std::vector<float> a((size_t)p->mloc), b((size_t)p->mloc);
+    if (p->mloc) {
+        PART_TRY(hipMemcpy(a.data(), p->xs, p->mloc * 4, hipMemcpyDeviceToHost));
+        PART_TRY(hipMemcpy(b.data(), p->xl, p->mloc * 4, hipMemcpyDeviceToHost));
+    }
+    for (int64_t c = 0; c < p->mloc; ++c) {
+        if (xs) xs[c] = a[c];
+        if (xl) xl[c] = b[c];
+    }
+    return ODESAT_OK;
+}
+
+// Where the previous step's unsat count(s) live: VARIABLES world flag slots of the gathered v,
+// CLAUSES out[n] (the all-reduced partial vector).
+static void flag_src(const odesat_part *p, const float *v, const float *out, int apply, const float **f, int64_t *stride,
+                     int *count) {
+    if (apply) {
+        *f = v + p->S;
+        *stride = p->S + 1;
+        *count = p->world;
+    } else {
+        *f = out + p->n;
+        *stride = 0;
+        *count = 1;
+    }
+}
+
+extern "C" int odesat_part_rhs(odesat_part *p, const float *v, float *out, double dt, double zeta, int apply, int stop,
+                               void *stream) {
+    if (!p || !v || !out) return fail(ODESAT_EINVAL, "null argument");
+    if (apply != 0 && apply != 1) return fail(ODESAT_EINVAL, "apply must be 0 (CLAUSES) or 1 (VARIABLES)");
+    if (apply == 1 && p->S == 0) return fail(ODESAT_EINVAL, "VARIABLES needs a block size");
+    PART_TRY(hipSetDevice(p->device));
+    hipStream_t st = (hipStream_t)stream;
+    const float *f;
+    int64_t stride;
+    int count;
+    flag_src(p, v, out, apply, &f, &stride, &count);
+    hipLaunchKernelGGL(k_part_status, dim3(1), dim3(64), 0, st, p->stat, f, stride, count, stop ? 1 : 0, 1);
+    PART_TRY(hipGetLastError());
+    // this step's unsat count goes after the written block: out[S] (send block) or out[n]
+    float *unsat = apply ? out + p->S : out + p->n;
+    PART_TRY(hipMemsetAsync(unsat, 0, 4, st));
+    const float xl_max = 1e4f * (float)p->m;  // system.rs:95, as the oracle's (T)1e4 * (T)m
+    if (p->mloc)
+        hipLaunchKernelGGL(k_part_clause, dim3(blocks_for(p->mloc)), dim3(256), 0, st, p->cptr, p->lits, v, p->xs,
+                           p->xl, p->w, (int32_t)p->mloc, (float)dt, (float)zeta, xl_max, unsat, p->stat);
+    PART_TRY(hipGetLastError());
+    if (p->v1 > p->v0)
+        hipLaunchKernelGGL(k_part_var, dim3(blocks_for(p->v1 - p->v0)), dim3(256), 0, st, p->cstart, p->deg, p->islot,
+                           p->w, v, (int32_t)p->voff, (int32_t)p->v0, (int32_t)p->v1, (float)dt, apply, out, p->stat);
+    PART_TRY(hipGetLastError());
+    return ODESAT_OK;
+}
+
+extern "C" int odesat_part_apply(odesat_part *p, float *v, const float *dvsum, double dt, void *stream) {
+    if (!p || !v || !dvsum) return fail(ODESAT_EINVAL, "null argument");
+    PART_TRY(hipSetDevice(p->device));
+    hipLaunchKernelGGL(k_part_apply, dim3(blocks_for(p->n)), dim3(256), 0, (hipStream_t)stream, v, dvsum,
+                       (int32_t)p->n, (float)dt, p->stat);
+    PART_TRY(hipGetLastError());
+    return ODESAT_OK;
+}
+
+extern "C" int odesat_part_reset(odesat_part *p, void *stream) {
+    if (!p) return fail(ODESAT_EINVAL, "null part");
+    PART_TRY(hipSetDevice(p->device));
+    const PartStat s0{0, -1, 0, 0};
+    PART_TRY(hipMemcpyAsync(p->stat, &s0, sizeof(s0), hipMemcpyHostToDevice, (hipStream_t)stream));
+    PART_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return ODESAT_OK;
+}
+
+extern "C" int odesat_part_status(odesat_part *p, const float *v, const float *out, int apply, int stop, void *stream,
+                                  int64_t *steps_done, int64_t *sat_step, int32_t *frozen) {
+    if (!p || !v || !out) return fail(ODESAT_EINVAL, "null argument");
+    PART_TRY(hipSetDevice(p->device));
+    hipStream_t st = (hipStream_t)stream;
+    const float *f;
+    int64_t stride;
+    int count;
+    flag_src(p, v, out, apply, &f, &stride, &count);
+    hipLaunchKernelGGL(k_part_status, dim3(1), dim3(64), 0, st, p->stat, f, stride, count, stop ? 1 : 0, 0);
+    PART_TRY(hipGetLastError());
+    PartStat h;
+    PART_TRY(hipMemcpyAsync(&h, p->stat, sizeof(h), hipMemcpyDeviceToHost, st));
+    PART_TRY(hipStreamSynchronize(st));
+    if (steps_done) *steps_done = h.steps_done;
+    if (sat_step) *sat_step = h.sat_step;
+    if (frozen) *frozen = h.frozen;
+    return ODESAT_OK;
+}

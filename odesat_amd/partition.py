@@ -1,0 +1,248 @@
+"""One very large instance across GPUs: BASELINE configs[4] ("single instance n=1M vars m=4.2M
+clauses, clause-partitioned across 8 GPUs, RCCL all-reduce on dv each step"), SURVEY.md §8e.
+
+The fixed Euler step of ONE replica (system.rs:141-154, driven like simulate, :156-239) with the
+formula split over `world` ranks, one process per GPU.  The per-rank kernels are in
+csrc/partition.hip (include/odesat.h, odesat_part_*); this module builds each rank's local topology
+on the host and runs the collective through a communicator (torch.distributed over RCCL on GPU
+boxes, gloo on CPU, or an in-process stand-in for tests).
+
+Two partitions:
+  CLAUSES    (the north star's design) rank r owns a contiguous slice of the clauses and a full v.
+             Each step it writes the partial dv of every variable (its clauses' terms, folded in
+             clause order) and its unsat count; one all-reduce (sum) of n + 1 floats, then every
+             rank applies the same update.  Reordering the fold across ranks makes this match the
+             reference within a tolerance (bit-exact at world = 1).
+  VARIABLES  rank r owns the variables [r S, (r + 1) S) and every clause touching them (a clause
+             spanning ranks is evaluated, identically, by each).  Each step it folds the complete
+             dv of its own variables in the reference's order and updates them; one all-gather of
+             S + 1 floats per rank (half an all-reduce's traffic) rebuilds v.  Bit-exact for any
+             world size.
+The replica's bookkeeping (steps done, first sat step, frozen after it) lives on the device, so the
+host polls the stop condition at any interval without changing results.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import ODESAT_PART_CLAUSES as CLAUSES
+from ._lib import ODESAT_PART_VARIABLES as VARIABLES
+from ._lib import check, lib
+
+__all__ = ["CLAUSES", "VARIABLES", "block_size", "local_topology", "default_zeta", "PartitionedSolver",
+           "TorchComm", "LocalComm"]
+
+
+def block_size(n: int, world: int) -> int:
+    """Variables per rank in the VARIABLES partition (the last block may be short)."""
+    return -(-n // world)
+
+
+def default_zeta(n: int, m: int) -> float:
+    """system.rs:164-173: the learning rate from the clause density."""
+    d = m / n
+    return 0.1 if d >= 6.0 else (0.01 if d >= 4.9 else 0.001)
+
+
+def local_topology(cp, var, neg, n: int, mode: int, rank: int, world: int) -> dict:
+    """Rank `rank`'s share of a normalised formula (clause_ptr cp[m+1], var[L], neg[L]).
+
+    Returns the local clauses (global indices, ascending = the reference's order), their CSR, the
+    variable range [v0, v1) this rank folds, and for each of those variables its local literal slots
+    in clause-then-literal order -- the order of the reference's dv accumulation (system.rs:35, :62,
+    :80)."""
+    cp = np.asarray(cp, np.int64)
+    var = np.asarray(var, np.int64)
+    neg = np.asarray(neg, np.uint8)
+    m = len(cp) - 1
+    if not (0 <= rank < world):
+        raise ValueError("bad rank / world")
+    lens_all = np.diff(cp)
+    if mode == CLAUSES:
+        c0, c1 = rank * m // world, (rank + 1) * m // world
+        local = np.arange(c0, c1, dtype=np.int64)
+        v0, v1, S = 0, n, 0
+    elif mode == VARIABLES:
+        S = block_size(n, world)
+        v0, v1 = min(n, rank * S), min(n, (rank + 1) * S)
+        owner = np.repeat(np.arange(m, dtype=np.int64), lens_all)
+        touch = np.zeros(m, bool)
+        touch[owner[(var >= v0) & (var < v1)]] = True
+        local = np.flatnonzero(touch).astype(np.int64)
+    else:
+        raise ValueError("mode must be CLAUSES or VARIABLES")
+    lens = lens_all[local]
+    lcp = np.zeros(len(local) + 1, np.int64)
+    np.cumsum(lens, out=lcp[1:])
+    L = int(lcp[-1])
+    gslot = np.repeat(cp[local], lens) + (np.arange(L, dtype=np.int64) - np.repeat(lcp[:-1], lens))
+    lvar, lneg = var[gslot], neg[gslot]
+    sel = np.flatnonzero((lvar >= v0) & (lvar < v1))
+    inc = sel[np.argsort(lvar[sel], kind="stable")]  # per variable: ascending slot = clause, literal order
+    counts = np.bincount(lvar[sel] - v0, minlength=v1 - v0)
+    vptr = np.zeros(v1 - v0 + 1, np.int64)
+    np.cumsum(counts, out=vptr[1:])
+    return {"clauses": local, "clause_ptr": lcp, "var": lvar, "neg": lneg, "v0": int(v0), "v1": int(v1),
+            "var_ptr": vptr, "inc_slot": inc.astype(np.int64), "block": int(S), "n": int(n), "m": int(m)}
+
+
+class TorchComm:
+    """The collective over a torch.distributed process group (RCCL "nccl" moves device tensors;
+    gloo stages them through host memory)."""
+
+    def __init__(self, dist):
+        self.dist = dist
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.staged = dist.get_backend() != "nccl"
+
+    def all_gather(self, out, block):
+        if self.staged:
+            o = out.cpu()
+            self.dist.all_gather_into_tensor(o, block.cpu())
+            out.copy_(o)
+        else:
+            self.dist.all_gather_into_tensor(out, block)
+
+    def all_reduce_sum(self, t):
+        if self.staged:
+            h = t.cpu()
+            self.dist.all_reduce(h)
+            t.copy_(h)
+        else:
+            self.dist.all_reduce(t)
+
+
+class LocalComm:
+    """A single rank (world = 1, no collective), or rank `rank` of `world` when a test drives the
+    exchange itself (PartitionedSolver.rhs / .post)."""
+
+    def __init__(self, rank: int = 0, world: int = 1):
+        self.rank, self.world = rank, world
+
+    def all_gather(self, out, block):
+        assert self.world == 1, "LocalComm gathers only at world = 1"
+        out.copy_(block)
+
+    def all_reduce_sum(self, t):
+        assert self.world == 1, "LocalComm reduces only at world = 1"
+
+
+class PartitionedSolver:
+    """Rank `comm.rank`'s share of one replica of a normalised formula (f32), on `device`."""
+
+    def __init__(self, cp, var, neg, n: int, mode: int = VARIABLES, comm=None, device: int = 0):
+        import torch
+        self.comm = comm or LocalComm()
+        self.mode, self.n = int(mode), int(n)
+        self.topo = t = local_topology(cp, var, neg, n, mode, self.comm.rank, self.comm.world)
+        self.m = t["m"]
+        h = C.c_void_p()
+        check(lib().odesat_part_create(int(device), self.comm.world, self.n, self.m, len(t["clauses"]),
+                                       _lib.i64ptr(t["clause_ptr"]), _lib.i64ptr(t["var"]), _lib.u8ptr(t["neg"]),
+                                       t["v0"], t["v1"], _lib.i64ptr(t["var_ptr"]), _lib.i64ptr(t["inc_slot"]),
+                                       t["block"], C.byref(h)))
+        self._h = h
+        self.dev = torch.device("cuda", device)
+        f32 = torch.float32
+        if self.mode == VARIABLES:
+            S = t["block"]
+            self.v = torch.ones(self.comm.world * (S + 1), dtype=f32, device=self.dev)  # gathered layout
+            self.out = torch.ones(S + 1, dtype=f32, device=self.dev)                      # send block
+        else:
+            self.v = torch.zeros(self.n, dtype=f32, device=self.dev)
+            self.out = torch.ones(self.n + 1, dtype=f32, device=self.dev)                 # partial dv + unsat
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().odesat_part_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def device_bytes(self) -> int:
+        return int(lib().odesat_part_device_bytes(self._h))
+
+    # -- state --------------------------------------------------------------------------------
+    def _v_index(self):
+        i = np.arange(self.n)
+        return i + i // self.topo["block"] if self.mode == VARIABLES else i
+
+    def _stream(self):
+        import torch
+        return C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def set_state(self, v, xs, xl):
+        """Full-size host arrays v[n], xs[m], xl[m] (the reference's State, system.rs:6-11); the
+        bookkeeping restarts (no step taken, no sat step)."""
+        import torch
+        loc = self.topo["clauses"]
+        xs_l = np.ascontiguousarray(np.asarray(xs, np.float64)[loc])
+        xl_l = np.ascontiguousarray(np.asarray(xl, np.float64)[loc])
+        check(lib().odesat_part_set_memories(self._h, _lib.dptr(xs_l), _lib.dptr(xl_l)))
+        host = np.ones(self.v.numel(), np.float32)  # VARIABLES flag slots read "unsat" until a step runs
+        host[self._v_index()] = np.asarray(v, np.float64).astype(np.float32)
+        self.v.copy_(torch.from_numpy(host))
+        self.out.fill_(1.0)
+        check(lib().odesat_part_reset(self._h, self._stream()))
+
+    def get_state(self):
+        """(v[n], xs_local, xl_local, local clause indices) as host f64 arrays."""
+        import torch
+        torch.cuda.synchronize(self.dev)
+        v = self.v.cpu().numpy()[self._v_index()].astype(np.float64)
+        k = len(self.topo["clauses"])
+        xs, xl = np.zeros(k), np.zeros(k)
+        check(lib().odesat_part_get_memories(self._h, _lib.dptr(xs), _lib.dptr(xl)))
+        return v, xs, xl, self.topo["clauses"]
+
+    # -- stepping -----------------------------------------------------------------------------
+    def rhs(self, dt: float, zeta: float, stop: bool = True):
+        """The rank's local part of a step: right-hand side + memory update into `out`."""
+        apply = 1 if self.mode == VARIABLES else 0
+        check(lib().odesat_part_rhs(self._h, C.c_void_p(self.v.data_ptr()), C.c_void_p(self.out.data_ptr()),
+                                    float(dt), float(zeta), apply, int(stop), self._stream()))
+
+    def post(self, dt: float):
+        """After the collective: CLAUSES applies the summed dv (VARIABLES' gather already is v)."""
+        if self.mode == CLAUSES:
+            check(lib().odesat_part_apply(self._h, C.c_void_p(self.v.data_ptr()), C.c_void_p(self.out.data_ptr()),
+                                          float(dt), self._stream()))
+
+    def step(self, dt: float, zeta: float, stop: bool = True):
+        """One fixed Euler step of the whole instance (system.rs:141-154), enqueued on torch's
+        current stream: local RHS + memory update, the collective, the voltage update.  With stop,
+        the first allsat step freezes the replica (later steps are no-ops), as simulate does."""
+        self.rhs(dt, zeta, stop)
+        if self.mode == VARIABLES:
+            self.comm.all_gather(self.v, self.out)
+        else:
+            self.comm.all_reduce_sum(self.out)
+        self.post(dt)
+
+    def status(self, stop: bool = True) -> dict:
+        """{steps_done, first_sat_step (-1 = none), frozen}; synchronises the stream."""
+        sd, ss, fr = C.c_int64(0), C.c_int64(0), C.c_int32(0)
+        apply = 1 if self.mode == VARIABLES else 0
+        check(lib().odesat_part_status(self._h, C.c_void_p(self.v.data_ptr()), C.c_void_p(self.out.data_ptr()),
+                                       apply, int(stop), self._stream(), C.byref(sd), C.byref(ss), C.byref(fr)))
+        return {"steps_done": sd.value, "first_sat_step": ss.value, "frozen": bool(fr.value)}
+
+    def simulate(self, dt: float = 0.01, steps: int = 1000, zeta: float | None = None, stop: bool = True,
+                 poll: int = 32) -> dict:
+        """simulate (system.rs:190-203, fixed step): run until the first allsat step (that step's
+        update included, :148-152) or `steps`; the stop condition is polled every `poll` steps
+        (exact regardless: a frozen replica does not step).  Returns status()."""
+        zeta = default_zeta(self.n, self.m) if zeta is None else zeta
+        for k in range(steps):
+            self.step(dt, zeta, stop)
+            if stop and (k + 1) % poll == 0 and k + 1 < steps and self.status(stop)["frozen"]:
+                break
+        return self.status(stop)

@@ -76,3 +76,13 @@ def formula_arrays(var, neg):
     m, k = var.shape
     return (np.arange(m + 1, dtype=np.int64) * k, (var - 1).reshape(-1).astype(np.int64),
             neg.reshape(-1).astype(np.uint8))
+
+
+def init_voltages(seed: int, replica0: int, count: int, n: int) -> np.ndarray:
+    """Initial voltages v ~ U[-1, 1) of replicas replica0 .. replica0+count-1 ([count, n] f64): the
+    counter RNG the device uses (kernels.hpp init_voltage; main.rs:171 maps rand's f64 the same way,
+    (u64 >> 11) * 2^-53 * 2 - 1)."""
+    r = np.arange(replica0, replica0 + count, dtype=np.uint64)[:, None]
+    i = np.arange(n, dtype=np.uint64)[None, :]
+    h = hash3(seed, r, i)
+    return (h >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0) * 2.0 - 1.0
