@@ -52,6 +52,8 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
+        from odesat_amd import device_count
+        local %= max(1, device_count())  # the one-GPU gloo rehearsal maps every rank to GPU 0
         import torch
         import torch.distributed as td
         # RCCL ("nccl") on GPU boxes; ODESAT_DIST_BACKEND=gloo rehearses N ranks on one GPU (RCCL
@@ -129,7 +131,7 @@ def main():
 
     def run_batch(batch, profile, alg_name=None):
         from odesat_amd import _lib, device_count
-        s = Solver(f, batch, args.dtype, device=local % max(1, device_count()))
+        s = Solver(f, batch, args.dtype, device=local)
         if args.chunk:
             s.set_chunk_replicas(args.chunk)
         alg_name = alg_name or args.alg

@@ -1,0 +1,272 @@
+// cli.cpp -- the `odesat` command line over libodesat_hip.so: the reference's src/main.rs:12-397
+// (clap subcommands solve / batch / inter, their flags, phase banners and output format), with the
+// integration on the MI355X through the C ABI (include/odesat.h).
+//
+//   odesat solve -f FILE [-o OUT] [-t TOL] [-n STEPS] [-s DT] [-l ZETA] [-r RATIO]
+//   odesat batch -f FILE -n STEPS -b BATCH [-o OUT] [-t TOL] [-s DT] [-l ZETA]
+//   odesat inter -f FILE -b BATCH [-o OUT] [-t TOL] [-n STEPS] [-s DT] [-l ZETA]
+//   extra flags: --seed S (initial voltages, counter RNG), --device D, --dtype f64|f32
+//
+// Semantics (main.rs):
+//   batch (:254-323)  replicas run until their own allsat (all B at once on the device); the first
+//                     replica, in index order, whose assignment satisfies the ORIGINAL formula is
+//                     reported (the reference's sequential loop breaks there); if none does, the
+//                     last replica's assignment is printed with `false`.
+//   inter (:326-386)  all replicas stop at the first step any is allsat (simulate_inter); the first
+//                     allsat replica of that step, else replica 0 (system.rs:353-358).
+//   solve (:143-204)  one replica until allsat (unbounded without -n: launched in chunks).
+// Declared deviations: initial voltages come from the reproducible counter RNG (--seed) instead of
+// thread_rng; the assignment is rendered in ascending variable order (the reference iterates a
+// HashMap); solve's preprocessing (BVE/BCE, cnf.rs:317-840) is not built yet, so solve integrates
+// the parsed formula itself; stoch (stoch.rs) is out of scope.
+#include <algorithm>
+#include <cerrno>
+#include <cinttypes>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/odesat.h"
+
+namespace {
+
+const char *USAGE =
+    "Usage: odesat <COMMAND>\n\n"
+    "Commands:\n"
+    "  solve  Run a single simulation\n"
+    "  stoch  Run a stochastic search search (not built: out of scope)\n"
+    "  batch  Run a batch of simulations, sequentially\n"
+    "  inter  Run a batch of simulations with their executions interlaced\n\n"
+    "Options (per command, main.rs:31-141):\n"
+    "  -f, --input <FILE>          Input file containing the CNF formula\n"
+    "  -o, --output <FILE>         Optional output file\n"
+    "  -t, --tolerance <TOL>       Error tolerance\n"
+    "  -n, --step-number <N>       Step number (required by batch)\n"
+    "  -s, --step-size <DT>        Step size (overrides tolerance)\n"
+    "  -b, --batch-size <B>        Batch size (batch, inter; required)\n"
+    "  -l, --learning-rate <ZETA>  Learning rate\n"
+    "  -r, --ctv-ratio <R>         Clause-to-Variable Ratio (solve; preprocessing not built)\n"
+    "      --seed <S>              Initial-voltage seed (default 42)\n"
+    "      --device <D>            GPU index (default 0)\n"
+    "      --dtype <f64|f32>       Integration precision (default f64, the reference's)\n";
+
+struct Opts {
+    std::string cmd, input, output;
+    bool has_tol = false, has_steps = false, has_dt = false, has_batch = false, has_zeta = false;
+    double tol = 1e-3, dt = 0.01, zeta = -1.0, ratio = 7.0;
+    int64_t steps = 0, batch = 0;
+    uint64_t seed = 42;
+    int device = 0, dtype = ODESAT_F64;
+};
+
+[[noreturn]] void usage_error(const std::string &msg) {
+    std::fprintf(stderr, "error: %s\n\n%s", msg.c_str(), USAGE);
+    std::exit(2);
+}
+
+bool parse_f64(const char *s, double *out) {
+    char *end = nullptr;
+    errno = 0;
+    const double x = std::strtod(s, &end);
+    if (errno || !end || *end || end == s) return false;
+    *out = x;
+    return true;
+}
+
+bool parse_i64(const char *s, int64_t *out) {
+    char *end = nullptr;
+    errno = 0;
+    const long long x = std::strtoll(s, &end, 10);
+    if (errno || !end || *end || end == s || x < 0) return false;
+    *out = (int64_t)x;
+    return true;
+}
+
+Opts parse_args(int argc, char **argv) {
+    Opts o;
+    if (argc < 2) usage_error("a subcommand is required");
+    o.cmd = argv[1];
+    if (o.cmd == "-h" || o.cmd == "--help" || o.cmd == "help") {
+        std::printf("%s", USAGE);
+        std::exit(0);
+    }
+    if (o.cmd != "solve" && o.cmd != "batch" && o.cmd != "inter" && o.cmd != "stoch")
+        usage_error("unrecognized subcommand '" + o.cmd + "'");
+    for (int i = 2; i < argc; ++i) {
+        const std::string a = argv[i];
+        if (a == "-h" || a == "--help") {
+            std::printf("%s", USAGE);
+            std::exit(0);
+        }
+        if (i + 1 >= argc) usage_error("a value is required for '" + a + "'");
+        const char *val = argv[++i];
+        auto f64 = [&](double *dst, bool *has) {
+            if (!parse_f64(val, dst)) usage_error("invalid value '" + std::string(val) + "' for '" + a + "'");
+            if (has) *has = true;
+        };
+        auto i64 = [&](int64_t *dst, bool *has) {
+            if (!parse_i64(val, dst)) usage_error("invalid value '" + std::string(val) + "' for '" + a + "'");
+            if (has) *has = true;
+        };
+        if (a == "-f" || a == "--input") o.input = val;
+        else if (a == "-o" || a == "--output") o.output = val;
+        else if (a == "-t" || a == "--tolerance") f64(&o.tol, &o.has_tol);
+        else if (a == "-s" || a == "--step-size") f64(&o.dt, &o.has_dt);
+        else if (a == "-l" || a == "--learning-rate") f64(&o.zeta, &o.has_zeta);
+        else if (a == "-r" || a == "--ctv-ratio") f64(&o.ratio, nullptr);
+        else if (a == "-n" || a == "--step-number") i64(&o.steps, &o.has_steps);
+        else if (a == "-b" || a == "--batch-size") i64(&o.batch, &o.has_batch);
+        else if (a == "--seed") {
+            int64_t s = 0;
+            i64(&s, nullptr);
+            o.seed = (uint64_t)s;
+        } else if (a == "--device") {
+            int64_t d = 0;
+            i64(&d, nullptr);
+            o.device = (int)d;
+        } else if (a == "--dtype") {
+            if (std::string(val) == "f64") o.dtype = ODESAT_F64;
+            else if (std::string(val) == "f32") o.dtype = ODESAT_F32;
+            else usage_error("--dtype must be f64 or f32");
+        } else {
+            usage_error("unexpected argument '" + a + "'");
+        }
+    }
+    if (o.input.empty()) usage_error("the following required arguments were not provided: --input <INPUT>");
+    if (o.cmd == "batch" && !o.has_steps)
+        usage_error("the following required arguments were not provided: --step-number <STEP_NUMBER>");
+    if ((o.cmd == "batch" || o.cmd == "inter") && !o.has_batch)
+        usage_error("the following required arguments were not provided: --batch-size <BATCH_SIZE>");
+    if (o.cmd == "solve") o.batch = 1;
+    if (o.batch <= 0 && o.cmd != "stoch") usage_error("--batch-size must be > 0");
+    return o;
+}
+
+int die(const char *what) {
+    std::fprintf(stderr, "Error: %s: %s\n", what, odesat_last_error());
+    return 1;
+}
+
+// cnf.rs:289-298 render_variable_map ("{var} {0|1}\n"; ascending, see the header)
+std::string render(const std::vector<std::pair<int64_t, bool>> &vals) {
+    std::string s;
+    for (const auto &kv : vals) s += std::to_string(kv.first) + (kv.second ? " 1\n" : " 0\n");
+    return s;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    const Opts o = parse_args(argc, argv);
+    if (o.cmd == "stoch") {
+        std::fprintf(stderr, "Error: stoch (the discrete stochastic search, stoch.rs) is not built: it is a "
+                             "different algorithm outside the integrator path (SURVEY.md §2 row 16)\n");
+        return 2;
+    }
+    std::printf("Reading CNF formula from file...\n");
+    std::ifstream in(o.input, std::ios::binary);
+    if (!in) {
+        std::fprintf(stderr, "Error: cannot read %s\n", o.input.c_str());
+        return 1;
+    }
+    std::stringstream ss;
+    ss << in.rdbuf();
+    const std::string text = ss.str();
+
+    std::printf("Parsing CNF formula...\n");
+    odesat_cnf *formula = nullptr;
+    if (odesat_cnf_parse(text.data(), text.size(), &formula)) return die("parse");
+    if (o.cmd == "solve")
+        std::printf("Preprocessing CNF formula... (not built: integrating the parsed formula)\n");
+    std::printf("Normalizing CNF formula...\n");
+    const int64_t L = odesat_cnf_nliterals(formula);
+    std::vector<int64_t> names((size_t)std::max<int64_t>(L, 1));
+    int64_t k = 0;
+    odesat_cnf *norm = nullptr;
+    if (odesat_cnf_normalize(formula, &norm, names.data(), &k)) return die("normalize");
+    const int64_t n = odesat_cnf_varnum(norm);
+
+    std::printf("Simulating...\n");
+    std::fflush(stdout);
+    odesat_solver *s = nullptr;
+    if (odesat_solver_create(o.device, norm, o.batch, o.dtype, &s)) return die("solver");
+    if (odesat_init_state(s, o.seed, 0)) return die("init");
+    odesat_params p{};
+    p.adaptive = o.has_dt ? 0 : 1;  // step_size overrides tolerance (main.rs:49)
+    p.stop = o.cmd == "inter" ? ODESAT_STOP_ANY : ODESAT_STOP_EACH;
+    p.tol = o.tol;
+    p.dt = o.dt;
+    p.zeta = o.has_zeta ? o.zeta : -1.0;
+    std::vector<int64_t> sat((size_t)o.batch, -1), done((size_t)o.batch, 0);
+    if (o.has_steps || o.cmd == "batch") {
+        p.max_steps = o.steps;
+        if (p.max_steps > 0 && odesat_simulate(s, &p, sat.data(), done.data(), nullptr, nullptr))
+            return die("simulate");
+    } else {  // steps = None: until some replica is allsat (system.rs:198, :221, :296, :333)
+        p.max_steps = 1 << 20;
+        for (;;) {
+            if (odesat_simulate(s, &p, sat.data(), done.data(), nullptr, nullptr)) return die("simulate");
+            bool any = false;
+            for (int64_t r = 0; r < o.batch; ++r) any = any || sat[r] >= 0;
+            if (any) break;
+        }
+    }
+    // the replica to report and its assignment mapped back to the file's variable names
+    auto mapped = [&](int64_t r, std::vector<std::pair<int64_t, bool>> &vals) -> int {
+        std::vector<uint8_t> a((size_t)std::max<int64_t>(n, 1));
+        if (odesat_get_assignment(s, r, a.data())) return 1;
+        vals.clear();
+        for (int64_t i = 0; i < k; ++i) vals.emplace_back(names[i], a[i] != 0);  // map_values_by_indices
+        return 0;
+    };
+    auto evaluate = [&](const std::vector<std::pair<int64_t, bool>> &vals) -> bool {  // evaluate_cnf
+        int64_t top = 0;
+        for (const auto &kv : vals) top = std::max(top, kv.first + 1);
+        std::vector<uint8_t> arr((size_t)std::max<int64_t>(top, 1), 0);
+        for (const auto &kv : vals) arr[kv.first] = kv.second ? 1 : 0;
+        return odesat_cnf_evaluate(formula, arr.data(), top) == 1;
+    };
+    std::vector<std::pair<int64_t, bool>> vals;
+    bool satisfied = false;
+    if (o.cmd == "inter") {
+        int64_t win = 0, best = INT64_MAX;
+        for (int64_t r = 0; r < o.batch; ++r)
+            if (sat[r] >= 0 && sat[r] < best) {
+                best = sat[r];
+                win = r;
+            }
+        if (mapped(win, vals)) return die("assignment");
+        satisfied = evaluate(vals);
+    } else {
+        for (int64_t r = 0; r < o.batch && !satisfied; ++r) {
+            if (mapped(r, vals)) return die("assignment");
+            satisfied = evaluate(vals);
+        }
+    }
+    if (o.cmd == "solve") std::printf("Mapping values...\nEvaluating CNF formula...\n");
+    std::printf(o.cmd == "solve" ? "Checking if solution vector satisfies formula: %s\n"
+                                 : "\nChecking if solution vector satisfies formula: %s\n",
+                satisfied ? "true" : "false");
+    std::printf("Rendering variable assignments...\n");
+    const std::string out = render(vals);
+    if (!o.output.empty()) {
+        std::printf("Writing results to file...\n");
+        std::ofstream f(o.output, std::ios::binary);
+        f << out;
+        if (!f) {
+            std::fprintf(stderr, "Error: cannot write %s\n", o.output.c_str());
+            return 1;
+        }
+    } else {
+        std::printf("Variable assignments:\n%s\n", out.c_str());
+    }
+    odesat_solver_destroy(s);
+    odesat_cnf_free(norm);
+    odesat_cnf_free(formula);
+    return 0;
+}
