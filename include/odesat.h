@@ -80,6 +80,40 @@ int odesat_cnf_evaluate(const odesat_cnf *cnf, const uint8_t *values, int64_t nv
 /* system.rs:361-372 init_short_term_memory: xs[c] = +1 if clause c has a negated literal, else -1 */
 int odesat_cnf_init_short_term_memory(const odesat_cnf *cnf, double *xs);
 
+/* ------------------------------------------------------- preprocessing (cnf.rs:317-840) ----- */
+
+/* The `solve` command's preprocessing: repeatedly_resolve_and_update (cnf.rs:833-840) on the set
+ * form of the formula (convert_to_cnf_formula_set, cnf.rs:348-361): blocked-clause elimination,
+ * bounded variable elimination while the clause/variable ratio stays <= target_ratio, subsumption.
+ * out: the reduced formula in set order (convert_to_cnf_formula, cnf.rs:364-379), varnum = input
+ * varnum - eliminated variables.  trace: the SimplificationTrace (cnf.rs:560-578).
+ * Declared deviation: ties of min_ratio_resolvant (cnf.rs:728-745, a HashSet scan) go to the
+ * smallest variable. */
+typedef struct odesat_trace odesat_trace;
+#define ODESAT_STEP_VARIABLE_ELIMINATION 0 /* cnf.rs:555 (var, positive clauses without +var) */
+#define ODESAT_STEP_BLOCKED_CLAUSE 1       /* cnf.rs:556 (var, the removed clause) */
+#define ODESAT_UNSET 2                     /* tri-state assignment: no value yet */
+int odesat_preprocess(const odesat_cnf *cnf, float target_ratio, odesat_cnf **out,
+                      odesat_trace **trace);
+void odesat_trace_free(odesat_trace *t);
+int64_t odesat_trace_nsteps(const odesat_trace *t);
+/* step i: kind, variable, clause and literal counts (any pointer may be NULL) */
+int odesat_trace_step(const odesat_trace *t, int64_t i, int32_t *kind, int64_t *var,
+                      int64_t *nclauses, int64_t *nliterals);
+/* step i's clauses as a CSR: clause_ptr[nclauses+1], var[nliterals], neg[nliterals] (NULL ok) */
+int odesat_trace_step_clauses(const odesat_trace *t, int64_t i, int64_t *clause_ptr, int64_t *var,
+                              uint8_t *neg);
+/* cnf.rs:501-519 calculate_trace on a tri-state assignment values[var] in {0, 1, ODESAT_UNSET}
+ * (the reference's HashMap; a variable read while unset becomes 0, as its entry API does).
+ * nvalues must exceed every variable of the trace. */
+int odesat_trace_apply(const odesat_trace *t, uint8_t *values, int64_t nvalues);
+/* cnf.rs:246-264 evaluate_cnf on the tri-state assignment, with its side effect: every variable
+ * read (all literals of the clauses up to the first unsatisfied one) that is unset becomes 0.
+ * Returns 1 / 0 or a negative error. */
+int odesat_cnf_evaluate_assign(const odesat_cnf *cnf, uint8_t *values, int64_t nvalues);
+/* the largest variable name in the formula, -1 if it has no literals */
+int64_t odesat_cnf_max_variable(const odesat_cnf *cnf);
+
 /* ------------------------------------------------------------- integrator (system.rs) -------- */
 
 /* Upload a NORMALISED formula (every variable < varnum) for `batch` replicas on `device`.

@@ -18,6 +18,7 @@ ODESAT_STOP_EACH, ODESAT_STOP_ANY, ODESAT_STOP_NONE = 0, 1, 2
 ODESAT_SCHED_AUTO, ODESAT_SCHED_STEP_MAJOR, ODESAT_SCHED_CHUNK_MAJOR = 0, 1, 2
 ODESAT_ALG_FUSED, ODESAT_ALG_TWOPASS, ODESAT_ALG_RESIDENT, ODESAT_ALG_ONCHIP = 0, 1, 2, 3
 ODESAT_PART_CLAUSES, ODESAT_PART_VARIABLES = 0, 1
+ODESAT_STEP_VARIABLE_ELIMINATION, ODESAT_STEP_BLOCKED_CLAUSE, ODESAT_UNSET = 0, 1, 2
 
 
 class OdesatError(RuntimeError):
@@ -53,6 +54,14 @@ SIGNATURES = {
     "odesat_cnf_normalize": (C.c_int, [_P, C.POINTER(_P), _i64p, _i64p]),
     "odesat_cnf_evaluate": (C.c_int, [_P, _u8p, _i64]),
     "odesat_cnf_init_short_term_memory": (C.c_int, [_P, _dp]),
+    "odesat_preprocess": (C.c_int, [_P, C.c_float, C.POINTER(_P), C.POINTER(_P)]),
+    "odesat_trace_free": (None, [_P]),
+    "odesat_trace_nsteps": (_i64, [_P]),
+    "odesat_trace_step": (C.c_int, [_P, _i64, C.POINTER(C.c_int32), _i64p, _i64p, _i64p]),
+    "odesat_trace_step_clauses": (C.c_int, [_P, _i64, _i64p, _i64p, _u8p]),
+    "odesat_trace_apply": (C.c_int, [_P, _u8p, _i64]),
+    "odesat_cnf_evaluate_assign": (C.c_int, [_P, _u8p, _i64]),
+    "odesat_cnf_max_variable": (_i64, [_P]),
     "odesat_solver_create": (C.c_int, [C.c_int, _P, _i64, C.c_int, C.POINTER(_P)]),
     "odesat_solver_destroy": (None, [_P]),
     "odesat_solver_batch": (_i64, [_P]),

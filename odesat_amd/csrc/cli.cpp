@@ -14,11 +14,12 @@
 //                     last replica's assignment is printed with `false`.
 //   inter (:326-386)  all replicas stop at the first step any is allsat (simulate_inter); the first
 //                     allsat replica of that step, else replica 0 (system.rs:353-358).
-//   solve (:143-204)  one replica until allsat (unbounded without -n: launched in chunks).
+//   solve (:143-204)  preprocessing (cnf.rs:317-840, preprocess.cpp) to the -r ratio, one replica
+//                     until allsat (unbounded without -n: launched in chunks), calculate_trace.
 // Declared deviations: initial voltages come from the reproducible counter RNG (--seed) instead of
 // thread_rng; the assignment is rendered in ascending variable order (the reference iterates a
-// HashMap); solve's preprocessing (BVE/BCE, cnf.rs:317-840) is not built yet, so solve integrates
-// the parsed formula itself; stoch (stoch.rs) is out of scope.
+// HashMap); preprocessing ties go to the smallest variable (preprocess.cpp); stoch (stoch.rs) is out
+// of scope.
 #include <algorithm>
 #include <cerrno>
 #include <cinttypes>
@@ -50,7 +51,7 @@ const char *USAGE =
     "  -s, --step-size <DT>        Step size (overrides tolerance)\n"
     "  -b, --batch-size <B>        Batch size (batch, inter; required)\n"
     "  -l, --learning-rate <ZETA>  Learning rate\n"
-    "  -r, --ctv-ratio <R>         Clause-to-Variable Ratio (solve; preprocessing not built)\n"
+    "  -r, --ctv-ratio <R>         Clause-to-Variable Ratio (solve; default 7)\n"
     "      --seed <S>              Initial-voltage seed (default 42)\n"
     "      --device <D>            GPU index (default 0)\n"
     "      --dtype <f64|f32>       Integration precision (default f64, the reference's)\n";
@@ -181,29 +182,42 @@ int main(int argc, char **argv) {
     std::printf("Parsing CNF formula...\n");
     odesat_cnf *formula = nullptr;
     if (odesat_cnf_parse(text.data(), text.size(), &formula)) return die("parse");
-    if (o.cmd == "solve")
-        std::printf("Preprocessing CNF formula... (not built: integrating the parsed formula)\n");
-    std::printf("Normalizing CNF formula...\n");
-    const int64_t L = odesat_cnf_nliterals(formula);
+    // solve: preprocessing (main.rs:162-166, cnf.rs:833-840); batch / inter integrate the parsed formula
+    odesat_cnf *reduced = nullptr;
+    odesat_trace *trace = nullptr;
+    const odesat_cnf *work = formula;
+    if (o.cmd == "solve") {
+        std::printf("Preprocessing CNF formula...\n");
+        if (odesat_preprocess(formula, (float)o.ratio, &reduced, &trace)) return die("preprocess");
+        std::printf("Clauses: %" PRId64 " | Vars: %" PRId64 "\n", odesat_cnf_nclauses(reduced),
+                    odesat_cnf_varnum(reduced));  // cnf.rs:824-828
+        work = reduced;
+    } else {
+        std::printf("Normalizing CNF formula...\n");
+    }
+    const int64_t L = odesat_cnf_nliterals(work);
     std::vector<int64_t> names((size_t)std::max<int64_t>(L, 1));
     int64_t k = 0;
     odesat_cnf *norm = nullptr;
-    if (odesat_cnf_normalize(formula, &norm, names.data(), &k)) return die("normalize");
+    if (odesat_cnf_normalize(work, &norm, names.data(), &k)) return die("normalize");
     const int64_t n = odesat_cnf_varnum(norm);
 
     std::printf("Simulating...\n");
     std::fflush(stdout);
+    // a formula with no variables left (everything eliminated) has an empty state: nothing to
+    // integrate, the reference's simulate returns an empty vector at once
     odesat_solver *s = nullptr;
-    if (odesat_solver_create(o.device, norm, o.batch, o.dtype, &s)) return die("solver");
-    if (odesat_init_state(s, o.seed, 0)) return die("init");
+    if (n > 0 && odesat_solver_create(o.device, norm, o.batch, o.dtype, &s)) return die("solver");
+    if (s && odesat_init_state(s, o.seed, 0)) return die("init");
     odesat_params p{};
     p.adaptive = o.has_dt ? 0 : 1;  // step_size overrides tolerance (main.rs:49)
     p.stop = o.cmd == "inter" ? ODESAT_STOP_ANY : ODESAT_STOP_EACH;
     p.tol = o.tol;
     p.dt = o.dt;
     p.zeta = o.has_zeta ? o.zeta : -1.0;
-    std::vector<int64_t> sat((size_t)o.batch, -1), done((size_t)o.batch, 0);
-    if (o.has_steps || o.cmd == "batch") {
+    std::vector<int64_t> sat((size_t)o.batch, s ? -1 : 0), done((size_t)o.batch, 0);
+    if (!s) {
+    } else if (o.has_steps || o.cmd == "batch") {
         p.max_steps = o.steps;
         if (p.max_steps > 0 && odesat_simulate(s, &p, sat.data(), done.data(), nullptr, nullptr))
             return die("simulate");
@@ -216,22 +230,22 @@ int main(int argc, char **argv) {
             if (any) break;
         }
     }
-    // the replica to report and its assignment mapped back to the file's variable names
-    auto mapped = [&](int64_t r, std::vector<std::pair<int64_t, bool>> &vals) -> int {
-        std::vector<uint8_t> a((size_t)std::max<int64_t>(n, 1));
-        if (odesat_get_assignment(s, r, a.data())) return 1;
-        vals.clear();
-        for (int64_t i = 0; i < k; ++i) vals.emplace_back(names[i], a[i] != 0);  // map_values_by_indices
+    // the reference's HashMap<usize, bool> as a tri-state array over the file's variable names
+    const int64_t top = std::max<int64_t>(odesat_cnf_max_variable(formula), 0) + 1;
+    std::vector<uint8_t> vals((size_t)top, ODESAT_UNSET);
+    std::vector<uint8_t> a((size_t)std::max<int64_t>(n, 1));
+    auto mapped = [&](int64_t r) -> int {  // map_values_by_indices (cnf.rs:301-315)
+        if (s && odesat_get_assignment(s, r, a.data())) return 1;
+        std::fill(vals.begin(), vals.end(), (uint8_t)ODESAT_UNSET);
+        if (!s) return 0;
+        for (int64_t i = 0; i < k && i < n; ++i) vals[(size_t)names[i]] = a[i];
         return 0;
     };
-    auto evaluate = [&](const std::vector<std::pair<int64_t, bool>> &vals) -> bool {  // evaluate_cnf
-        int64_t top = 0;
-        for (const auto &kv : vals) top = std::max(top, kv.first + 1);
-        std::vector<uint8_t> arr((size_t)std::max<int64_t>(top, 1), 0);
-        for (const auto &kv : vals) arr[kv.first] = kv.second ? 1 : 0;
-        return odesat_cnf_evaluate(formula, arr.data(), top) == 1;
+    auto evaluate = [&]() -> bool {  // evaluate_cnf against the ORIGINAL formula (inserts unset reads)
+        const int rc = odesat_cnf_evaluate_assign(formula, vals.data(), top);
+        if (rc < 0) std::exit(die("evaluate"));
+        return rc == 1;
     };
-    std::vector<std::pair<int64_t, bool>> vals;
     bool satisfied = false;
     if (o.cmd == "inter") {
         int64_t win = 0, best = INT64_MAX;
@@ -240,20 +254,28 @@ int main(int argc, char **argv) {
                 best = sat[r];
                 win = r;
             }
-        if (mapped(win, vals)) return die("assignment");
-        satisfied = evaluate(vals);
+        if (mapped(win)) return die("assignment");
+        satisfied = evaluate();
+    } else if (o.cmd == "solve") {
+        std::printf("Mapping values...\n");
+        if (mapped(0)) return die("assignment");
+        if (odesat_trace_apply(trace, vals.data(), top)) return die("trace");  // calculate_trace
+        std::printf("Evaluating CNF formula...\n");
+        satisfied = evaluate();
     } else {
         for (int64_t r = 0; r < o.batch && !satisfied; ++r) {
-            if (mapped(r, vals)) return die("assignment");
-            satisfied = evaluate(vals);
+            if (mapped(r)) return die("assignment");
+            satisfied = evaluate();
         }
     }
-    if (o.cmd == "solve") std::printf("Mapping values...\nEvaluating CNF formula...\n");
     std::printf(o.cmd == "solve" ? "Checking if solution vector satisfies formula: %s\n"
                                  : "\nChecking if solution vector satisfies formula: %s\n",
                 satisfied ? "true" : "false");
     std::printf("Rendering variable assignments...\n");
-    const std::string out = render(vals);
+    std::vector<std::pair<int64_t, bool>> listed;
+    for (int64_t v = 0; v < top; ++v)
+        if (vals[(size_t)v] != ODESAT_UNSET) listed.emplace_back(v, vals[(size_t)v] != 0);
+    const std::string out = render(listed);
     if (!o.output.empty()) {
         std::printf("Writing results to file...\n");
         std::ofstream f(o.output, std::ios::binary);
@@ -265,8 +287,10 @@ int main(int argc, char **argv) {
     } else {
         std::printf("Variable assignments:\n%s\n", out.c_str());
     }
-    odesat_solver_destroy(s);
+    if (s) odesat_solver_destroy(s);
     odesat_cnf_free(norm);
+    odesat_cnf_free(reduced);
+    odesat_trace_free(trace);
     odesat_cnf_free(formula);
     return 0;
 }

@@ -134,3 +134,20 @@ def test_batch_and_inter_planted(tmp_path):
         assert r.returncode == 0, r.stderr
         assert "satisfies formula: true" in r.stdout, r.stdout
         assert satisfies(parse_render(out.read_text()), clauses)
+
+
+@pytest.mark.gpu
+def test_solve_preprocesses_then_rebuilds_eliminated_variables(golden_dir, tmp_path):
+    """easy.cnf ("Edited to be Satisfiable"): preprocessing to ratio 7 leaves 267 clauses over 43
+    variables (tests/golden/preprocess_golden.json); the trace restores the other 57."""
+    out = tmp_path / "easy.txt"
+    path = os.path.join(golden_dir, "easy.cnf")
+    r = run("solve", "-f", path, "-s", "0.1", "-o", str(out))
+    assert r.returncode == 0, r.stderr
+    assert "Clauses: 267 | Vars: 43" in r.stdout
+    assert "Mapping values..." in r.stdout and "satisfies formula: true" in r.stdout
+    assign = parse_render(out.read_text())
+    assert sorted(assign) == list(range(1, 101))
+    with open(path) as fh:
+        clauses = [ln for ln in fh.read().splitlines() if ln and ln[0] not in "cp%"]
+    assert satisfies(assign, clauses)
