@@ -142,6 +142,12 @@ int odesat_get_state(odesat_solver *s, int64_t r0, int64_t count, double *v, dou
                      double *xl);
 /* system.rs:238 / :355: assignment[i] = v[i] > 0 for replica r. */
 int odesat_get_assignment(odesat_solver *s, int64_t r, uint8_t *assignment);
+/* cnf.rs:246-264 evaluate_cnf of every replica's assignment (v > 0, system.rs:238) against the
+ * solver's formula, on the device.  satisfied[B] (may be NULL);
+ * first_satisfied = the lowest replica index whose assignment satisfies the formula, -1 if none
+ * (batch's pick, main.rs:302-307; may be NULL).  The formula is the normalised one the solver was
+ * built from, which without preprocessing is the input with variables renamed. */
+int odesat_evaluate(odesat_solver *s, uint8_t *satisfied, int64_t *first_satisfied);
 
 /* system.rs:25-91 compute_derivatives on every replica's current state (no state change).
  * dv[B][n], dxs[B][m], dxl[B][m] (may be NULL), allsat[B] (may be NULL). */

@@ -72,6 +72,7 @@ SIGNATURES = {
     "odesat_init_state": (C.c_int, [_P, C.c_uint64, _i64]),
     "odesat_get_state": (C.c_int, [_P, _i64, _i64, _dp, _dp, _dp]),
     "odesat_get_assignment": (C.c_int, [_P, _i64, _u8p]),
+    "odesat_evaluate": (C.c_int, [_P, _u8p, _i64p]),
     "odesat_compute_derivatives": (C.c_int, [_P, C.c_double, _dp, _dp, _dp, _u8p]),
     "odesat_euler_step_fixed": (C.c_int, [_P, C.c_double, C.c_double, _u8p]),
     "odesat_euler_step": (C.c_int, [_P, C.c_double, _dp, C.c_double, _u8p]),

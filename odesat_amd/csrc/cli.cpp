@@ -262,11 +262,12 @@ int main(int argc, char **argv) {
         if (odesat_trace_apply(trace, vals.data(), top)) return die("trace");  // calculate_trace
         std::printf("Evaluating CNF formula...\n");
         satisfied = evaluate();
-    } else {
-        for (int64_t r = 0; r < o.batch && !satisfied; ++r) {
-            if (mapped(r)) return die("assignment");
-            satisfied = evaluate();
-        }
+    } else {  // batch: the device checks every replica at once (odesat_evaluate), then the host
+              // re-checks the pick against the input: the first satisfying replica, else the last
+        int64_t first = -1;
+        if (s && odesat_evaluate(s, nullptr, &first)) return die("evaluate");
+        if (mapped(first >= 0 ? first : o.batch - 1)) return die("assignment");
+        satisfied = evaluate();
     }
     std::printf(o.cmd == "solve" ? "Checking if solution vector satisfies formula: %s\n"
                                  : "\nChecking if solution vector satisfies formula: %s\n",

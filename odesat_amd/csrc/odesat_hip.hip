@@ -1327,6 +1327,90 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
     return s->profile ? ODESAT_OK : drain_profile(s);
 }
 
+// ---- batched evaluate_cnf ----------------------------------------------
+namespace {
+
+// cnf.rs:246-264 on every replica's assignment (v > 0, system.rs:238): thread (clause c, replica r),
+// replicas fastest so a group's W lanes read one voltage row.  unsat[r] = 1 if some clause fails.
+template <typename T>
+__global__ void k_evaluate(const T *b0, const T *b1, const uint8_t *par, const int32_t *cptr, const int32_t *lits,
+                           int64_t n, int64_t m, int W, int64_t B, uint32_t *unsat) {
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= (size_t)m * (size_t)B) return;
+    const int64_t r = (int64_t)(tid % (size_t)B), c = (int64_t)(tid / (size_t)B);
+    const int64_t g = r / W;
+    const T *v = (par[g] ? b1 : b0) + (size_t)g * n * W + (r % W);
+    bool sat = false;
+    for (int32_t k = cptr[c]; k < cptr[c + 1]; ++k) {
+        const int32_t l = lits[k];
+        sat = sat || ((v[(size_t)(l >> 1) * W] > (T)0) != ((l & 1) != 0));
+    }
+    if (!sat) unsat[r] = 1u;
+}
+
+// the lowest replica whose assignment satisfies the formula (main.rs:302-307), -1 if none
+__global__ void k_first_satisfied(const uint32_t *unsat, int64_t B, int64_t *first) {
+    __shared__ int64_t best[256];
+    int64_t b = INT64_MAX;
+    for (int64_t r = threadIdx.x; r < B; r += blockDim.x)
+        if (!unsat[r]) {
+            b = r;
+            break;
+        }
+    best[threadIdx.x] = b;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) best[threadIdx.x] = min(best[threadIdx.x], best[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *first = best[0] == INT64_MAX ? -1 : best[0];
+}
+
+template <typename T> int evaluate_t(odesat_solver *s, uint32_t *flags, int64_t *first) {
+    HIP_TRY(hipMemsetAsync(flags, 0, (size_t)s->B * 4, s->stream));
+    const size_t total = (size_t)s->m * (size_t)s->B;
+    if (total) {
+        const int threads = 256;
+        hipLaunchKernelGGL((k_evaluate<T>), dim3((unsigned)((total + threads - 1) / threads)), dim3(threads), 0,
+                           s->stream, (const T *)s->v[0], (const T *)s->v[1], s->par, s->cptr, s->lits, s->n, s->m,
+                           s->W, s->B, flags);
+        HIP_TRY(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_first_satisfied, dim3(1), dim3(256), 0, s->stream, flags, s->B, first);
+    HIP_TRY(hipGetLastError());
+    return ODESAT_OK;
+}
+
+}  // namespace
+
+extern "C" int odesat_evaluate(odesat_solver *s, uint8_t *satisfied, int64_t *first_satisfied) {
+    int rc;
+    if ((rc = check_solver(s))) return rc;
+    uint32_t *flags = nullptr;
+    int64_t *first = nullptr;
+    HIP_TRY(hipMalloc(&flags, (size_t)s->B * 4 + 8));
+    first = reinterpret_cast<int64_t *>(flags + ((s->B + 1) & ~int64_t(1)));
+    rc = s->dtype == ODESAT_F64 ? evaluate_t<double>(s, flags, first) : evaluate_t<float>(s, flags, first);
+    std::vector<uint32_t> u;
+    int64_t f = -1;
+    hipError_t e = hipSuccess;
+    if (!rc) {
+        if (satisfied) {
+            u.resize((size_t)s->B);
+            e = hipMemcpyAsync(u.data(), flags, (size_t)s->B * 4, hipMemcpyDeviceToHost, s->stream);
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(&f, first, 8, hipMemcpyDeviceToHost, s->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    }
+    (void)hipFree(flags);
+    if (rc) return rc;
+    HIP_TRY(e);
+    if (satisfied)
+        for (int64_t r = 0; r < s->B; ++r) satisfied[r] = u[(size_t)r] ? 0 : 1;
+    if (first_satisfied) *first_satisfied = f;
+    return ODESAT_OK;
+}
+
 extern "C" int odesat_synchronize(odesat_solver *s) {
     int rc;
     if ((rc = check_solver(s))) return rc;

@@ -94,6 +94,10 @@ __device__ __forceinline__ void gather(const Slot &S, Gath &G) {
 //   the clamps are med3 (finite arguments: the host requires a finite dt).
 // Scalings by 0.5 / 2 / 2.5 / +-1 are exact here (no subnormals: |A| >= 0.02, |mn - c| >= 2^-26 or 0,
 // |xl xs sel| >= 6e-11 or 0).
+#ifndef ONCHIP_ORDER
+#define ONCHIP_ORDER 0
+#endif
+
 struct Front {  // first half: literal values and their min / second min
     uint32_t a0, a1, a2, hi;
     float val0, val1, val2, mn, sec;
@@ -146,6 +150,7 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
 __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &slot3, float2 &mem1, Pend &P, Front &Fn,
                                           Gath &Gn, int t, float h, float hh, uint32_t &cmax) {
     const float o0 = lds_f(P.a0 + DVC), o1 = lds_f(P.a1 + DVC), o2 = lds_f(P.a2 + DVC);
+#if ONCHIP_ORDER == 0
     lds_st(P.a0 + DVC, o0 + P.d0);
     lds_st(P.a1 + DVC, o1 + P.d1);
     lds_st(P.a2 + DVC, o2 + P.d2);
@@ -156,6 +161,35 @@ __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &sl
     __builtin_amdgcn_sched_barrier(0);
     back(a, Fn, mem1, h, hh, P, cmax);  // P <- tile t+1's terms (tile t's were written above)
     front(Gn, Fn);                      // Fn <- tile t+2's first half
+#elif ONCHIP_ORDER == 1
+    __builtin_amdgcn_sched_barrier(0);
+    Gath G3;
+    gather(slot3, G3);
+    slot3 = load_rec(R, t + 7);
+    __builtin_amdgcn_sched_barrier(0);
+    const Front F1 = Fn;
+    front(Gn, Fn);                      // Fn <- tile t+2's first half, under the dv reads
+    __builtin_amdgcn_sched_barrier(0);
+    lds_st(P.a0 + DVC, o0 + P.d0);
+    lds_st(P.a1 + DVC, o1 + P.d1);
+    lds_st(P.a2 + DVC, o2 + P.d2);
+    __builtin_amdgcn_sched_barrier(0);
+    back(a, F1, mem1, h, hh, P, cmax);  // P <- tile t+1's terms, under the dv writes
+#else
+    __builtin_amdgcn_sched_barrier(0);
+    Gath G3;
+    gather(slot3, G3);
+    slot3 = load_rec(R, t + 7);
+    __builtin_amdgcn_sched_barrier(0);
+    const Pend Q = P;
+    back(a, Fn, mem1, h, hh, P, cmax);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_st(Q.a0 + DVC, o0 + Q.d0);
+    lds_st(Q.a1 + DVC, o1 + Q.d1);
+    lds_st(Q.a2 + DVC, o2 + Q.d2);
+    __builtin_amdgcn_sched_barrier(0);
+    front(Gn, Fn);
+#endif
     __builtin_amdgcn_sched_barrier(0);  // a tile's work stays between its barriers
     __syncthreads();
     __builtin_amdgcn_sched_barrier(0);

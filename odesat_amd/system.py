@@ -103,6 +103,14 @@ class Solver:
         check(lib().odesat_get_assignment(self._h, r, _lib.u8ptr(out)))
         return out.astype(bool)
 
+    def evaluate(self):
+        """evaluate_cnf (cnf.rs:246-264) of every replica's assignment on the device.  Returns
+        (satisfied bool[B], the lowest satisfying replica or -1)."""
+        sat = np.zeros(self.batch, np.uint8)
+        first = C.c_int64(-1)
+        check(lib().odesat_evaluate(self._h, _lib.u8ptr(sat), C.byref(first)))
+        return sat.astype(bool), int(first.value)
+
     # -- single operations (system.rs:25, 111, 141) -----------------------------------------------
     def compute_derivatives(self, zeta: float):
         B = self.batch
