@@ -80,6 +80,31 @@ int odesat_cnf_evaluate(const odesat_cnf *cnf, const uint8_t *values, int64_t nv
 /* system.rs:361-372 init_short_term_memory: xs[c] = +1 if clause c has a negated literal, else -1 */
 int odesat_cnf_init_short_term_memory(const odesat_cnf *cnf, double *xs);
 
+/* ------------------------------------------------ stochastic search (stoch.rs:20-110) ------- */
+
+/* The `stoch` command's discrete search (stoch.rs; main.rs:206-251) for `batch` independent
+ * replicas of a NORMALISED formula on one GPU.  State per replica: v[n] booleans (bytes 0/1) and
+ * xl[m] u64; create / reset start every replica from search()'s v = false, xl = 1 (stoch.rs:88-91).
+ * Declared deviation: the reference's draw gen_range(1..=tot) uses thread_rng; here
+ * r = 1 + mulhi64(h, tot) with h a counter RNG of (seed, replica0 + r, step, var), step = the
+ * replica's steps since its state was set.  A variable in no clause (the reference panics at
+ * gen_range(1..=0), stoch.rs:70) makes create fail with ODESAT_EINVAL. */
+typedef struct odesat_stoch odesat_stoch;
+int odesat_stoch_create(int device, const odesat_cnf *normalized, int64_t batch, odesat_stoch **out);
+void odesat_stoch_destroy(odesat_stoch *s);
+/* v = false, xl = 1, step counter 0 for replicas [r0, r0+count) */
+int odesat_stoch_reset(odesat_stoch *s, int64_t r0, int64_t count);
+/* replica-major host arrays v[count][n] (0/1), xl[count][m]; either may be NULL (that part is
+ * reset); the step counter restarts */
+int odesat_stoch_set_state(odesat_stoch *s, int64_t r0, int64_t count, const uint8_t *v, const uint64_t *xl);
+int odesat_stoch_get_state(odesat_stoch *s, int64_t r0, int64_t count, uint8_t *v, uint64_t *xl);
+/* search (stoch.rs:83-110) on every replica: up to max_steps (> 0) steps; stop = ODESAT_STOP_EACH
+ * (a replica stops after its first step that finds every clause satisfied) or ODESAT_STOP_NONE.
+ * first_sat_step[B] (0-based step of this call, -1 none) and steps_done[B] may be NULL;
+ * poll_interval = steps between host checks of "all stopped" (0 = 64). */
+int odesat_stoch_search(odesat_stoch *s, uint64_t seed, int64_t replica0, int64_t max_steps, int stop,
+                        int32_t poll_interval, int64_t *first_sat_step, int64_t *steps_done);
+
 /* ------------------------------------------------------- preprocessing (cnf.rs:317-840) ----- */
 
 /* The `solve` command's preprocessing: repeatedly_resolve_and_update (cnf.rs:833-840) on the set

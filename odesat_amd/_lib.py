@@ -54,6 +54,12 @@ SIGNATURES = {
     "odesat_cnf_normalize": (C.c_int, [_P, C.POINTER(_P), _i64p, _i64p]),
     "odesat_cnf_evaluate": (C.c_int, [_P, _u8p, _i64]),
     "odesat_cnf_init_short_term_memory": (C.c_int, [_P, _dp]),
+    "odesat_stoch_create": (C.c_int, [C.c_int, _P, _i64, C.POINTER(_P)]),
+    "odesat_stoch_destroy": (None, [_P]),
+    "odesat_stoch_reset": (C.c_int, [_P, _i64, _i64]),
+    "odesat_stoch_set_state": (C.c_int, [_P, _i64, _i64, _u8p, C.POINTER(C.c_uint64)]),
+    "odesat_stoch_get_state": (C.c_int, [_P, _i64, _i64, _u8p, C.POINTER(C.c_uint64)]),
+    "odesat_stoch_search": (C.c_int, [_P, C.c_uint64, _i64, _i64, C.c_int, C.c_int32, _i64p, _i64p]),
     "odesat_preprocess": (C.c_int, [_P, C.c_float, C.POINTER(_P), C.POINTER(_P)]),
     "odesat_trace_free": (None, [_P]),
     "odesat_trace_nsteps": (_i64, [_P]),

@@ -18,8 +18,10 @@
 //                     until allsat (unbounded without -n: launched in chunks), calculate_trace.
 // Declared deviations: initial voltages come from the reproducible counter RNG (--seed) instead of
 // thread_rng; the assignment is rendered in ascending variable order (the reference iterates a
-// HashMap); preprocessing ties go to the smallest variable (preprocess.cpp); stoch (stoch.rs) is out
-// of scope.
+// HashMap); preprocessing ties go to the smallest variable (preprocess.cpp); stoch draws from a
+// counter RNG (stoch.hip).
+//   stoch (:206-251)  preprocessing, then the discrete search (stoch.rs) of one replica from
+//                     v = false, xl = 1 until every clause is satisfied (or -n steps).
 #include <algorithm>
 #include <cerrno>
 #include <cinttypes>
@@ -40,7 +42,7 @@ const char *USAGE =
     "Usage: odesat <COMMAND>\n\n"
     "Commands:\n"
     "  solve  Run a single simulation\n"
-    "  stoch  Run a stochastic search search (not built: out of scope)\n"
+    "  stoch  Run a stochastic search search\n"
     "  batch  Run a batch of simulations, sequentially\n"
     "  inter  Run a batch of simulations with their executions interlaced\n\n"
     "Options (per command, main.rs:31-141):\n"
@@ -51,7 +53,7 @@ const char *USAGE =
     "  -s, --step-size <DT>        Step size (overrides tolerance)\n"
     "  -b, --batch-size <B>        Batch size (batch, inter; required)\n"
     "  -l, --learning-rate <ZETA>  Learning rate\n"
-    "  -r, --ctv-ratio <R>         Clause-to-Variable Ratio (solve; default 7)\n"
+    "  -r, --ctv-ratio <R>         Clause-to-Variable Ratio (solve, stoch; default 7)\n"
     "      --seed <S>              Initial-voltage seed (default 42)\n"
     "      --device <D>            GPU index (default 0)\n"
     "      --dtype <f64|f32>       Integration precision (default f64, the reference's)\n";
@@ -143,8 +145,10 @@ Opts parse_args(int argc, char **argv) {
         usage_error("the following required arguments were not provided: --step-number <STEP_NUMBER>");
     if ((o.cmd == "batch" || o.cmd == "inter") && !o.has_batch)
         usage_error("the following required arguments were not provided: --batch-size <BATCH_SIZE>");
-    if (o.cmd == "solve") o.batch = 1;
-    if (o.batch <= 0 && o.cmd != "stoch") usage_error("--batch-size must be > 0");
+    if (o.cmd == "stoch" && (o.has_tol || o.has_dt || o.has_zeta || o.has_batch))  // StochOpts, main.rs:63-79
+        usage_error("stoch takes only --input, --output, --step-number and --ctv-ratio");
+    if (o.cmd == "solve" || o.cmd == "stoch") o.batch = 1;
+    if (o.batch <= 0) usage_error("--batch-size must be > 0");
     return o;
 }
 
@@ -164,11 +168,6 @@ std::string render(const std::vector<std::pair<int64_t, bool>> &vals) {
 
 int main(int argc, char **argv) {
     const Opts o = parse_args(argc, argv);
-    if (o.cmd == "stoch") {
-        std::fprintf(stderr, "Error: stoch (the discrete stochastic search, stoch.rs) is not built: it is a "
-                             "different algorithm outside the integrator path (SURVEY.md §2 row 16)\n");
-        return 2;
-    }
     std::printf("Reading CNF formula from file...\n");
     std::ifstream in(o.input, std::ios::binary);
     if (!in) {
@@ -186,7 +185,8 @@ int main(int argc, char **argv) {
     odesat_cnf *reduced = nullptr;
     odesat_trace *trace = nullptr;
     const odesat_cnf *work = formula;
-    if (o.cmd == "solve") {
+    const bool preprocess = o.cmd == "solve" || o.cmd == "stoch";
+    if (preprocess) {
         std::printf("Preprocessing CNF formula...\n");
         if (odesat_preprocess(formula, (float)o.ratio, &reduced, &trace)) return die("preprocess");
         std::printf("Clauses: %" PRId64 " | Vars: %" PRId64 "\n", odesat_cnf_nclauses(reduced),
@@ -207,27 +207,36 @@ int main(int argc, char **argv) {
     // a formula with no variables left (everything eliminated) has an empty state: nothing to
     // integrate, the reference's simulate returns an empty vector at once
     odesat_solver *s = nullptr;
-    if (n > 0 && odesat_solver_create(o.device, norm, o.batch, o.dtype, &s)) return die("solver");
-    if (s && odesat_init_state(s, o.seed, 0)) return die("init");
-    odesat_params p{};
-    p.adaptive = o.has_dt ? 0 : 1;  // step_size overrides tolerance (main.rs:49)
-    p.stop = o.cmd == "inter" ? ODESAT_STOP_ANY : ODESAT_STOP_EACH;
-    p.tol = o.tol;
-    p.dt = o.dt;
-    p.zeta = o.has_zeta ? o.zeta : -1.0;
-    std::vector<int64_t> sat((size_t)o.batch, s ? -1 : 0), done((size_t)o.batch, 0);
-    if (!s) {
-    } else if (o.has_steps || o.cmd == "batch") {
-        p.max_steps = o.steps;
-        if (p.max_steps > 0 && odesat_simulate(s, &p, sat.data(), done.data(), nullptr, nullptr))
-            return die("simulate");
-    } else {  // steps = None: until some replica is allsat (system.rs:198, :221, :296, :333)
-        p.max_steps = 1 << 20;
-        for (;;) {
-            if (odesat_simulate(s, &p, sat.data(), done.data(), nullptr, nullptr)) return die("simulate");
-            bool any = false;
-            for (int64_t r = 0; r < o.batch; ++r) any = any || sat[r] >= 0;
-            if (any) break;
+    odesat_stoch *st = nullptr;
+    std::vector<int64_t> sat((size_t)o.batch, n > 0 ? -1 : 0), done((size_t)o.batch, 0);
+    if (n > 0 && o.cmd == "stoch") {  // stoch.rs:83-110 search
+        if (odesat_stoch_create(o.device, norm, 1, &st)) return die("stoch");
+        const int64_t chunk = o.has_steps ? o.steps : (int64_t)1 << 16;
+        do {
+            if (chunk > 0 && odesat_stoch_search(st, o.seed, 0, chunk, ODESAT_STOP_EACH, 0, sat.data(), done.data()))
+                return die("search");
+        } while (!o.has_steps && sat[0] < 0);
+    } else if (n > 0) {
+        if (odesat_solver_create(o.device, norm, o.batch, o.dtype, &s)) return die("solver");
+        if (odesat_init_state(s, o.seed, 0)) return die("init");
+        odesat_params p{};
+        p.adaptive = o.has_dt ? 0 : 1;  // step_size overrides tolerance (main.rs:49)
+        p.stop = o.cmd == "inter" ? ODESAT_STOP_ANY : ODESAT_STOP_EACH;
+        p.tol = o.tol;
+        p.dt = o.dt;
+        p.zeta = o.has_zeta ? o.zeta : -1.0;
+        if (o.has_steps || o.cmd == "batch") {
+            p.max_steps = o.steps;
+            if (p.max_steps > 0 && odesat_simulate(s, &p, sat.data(), done.data(), nullptr, nullptr))
+                return die("simulate");
+        } else {  // steps = None: until some replica is allsat (system.rs:198, :221, :296, :333)
+            p.max_steps = 1 << 20;
+            for (;;) {
+                if (odesat_simulate(s, &p, sat.data(), done.data(), nullptr, nullptr)) return die("simulate");
+                bool any = false;
+                for (int64_t r = 0; r < o.batch; ++r) any = any || sat[r] >= 0;
+                if (any) break;
+            }
         }
     }
     // the reference's HashMap<usize, bool> as a tri-state array over the file's variable names
@@ -236,8 +245,9 @@ int main(int argc, char **argv) {
     std::vector<uint8_t> a((size_t)std::max<int64_t>(n, 1));
     auto mapped = [&](int64_t r) -> int {  // map_values_by_indices (cnf.rs:301-315)
         if (s && odesat_get_assignment(s, r, a.data())) return 1;
+        if (st && odesat_stoch_get_state(st, r, 1, a.data(), nullptr)) return 1;
         std::fill(vals.begin(), vals.end(), (uint8_t)ODESAT_UNSET);
-        if (!s) return 0;
+        if (!s && !st) return 0;
         for (int64_t i = 0; i < k && i < n; ++i) vals[(size_t)names[i]] = a[i];
         return 0;
     };
@@ -256,7 +266,7 @@ int main(int argc, char **argv) {
             }
         if (mapped(win)) return die("assignment");
         satisfied = evaluate();
-    } else if (o.cmd == "solve") {
+    } else if (preprocess) {  // solve, stoch
         std::printf("Mapping values...\n");
         if (mapped(0)) return die("assignment");
         if (odesat_trace_apply(trace, vals.data(), top)) return die("trace");  // calculate_trace
@@ -269,7 +279,7 @@ int main(int argc, char **argv) {
         if (mapped(first >= 0 ? first : o.batch - 1)) return die("assignment");
         satisfied = evaluate();
     }
-    std::printf(o.cmd == "solve" ? "Checking if solution vector satisfies formula: %s\n"
+    std::printf(preprocess ? "Checking if solution vector satisfies formula: %s\n"
                                  : "\nChecking if solution vector satisfies formula: %s\n",
                 satisfied ? "true" : "false");
     std::printf("Rendering variable assignments...\n");
@@ -289,6 +299,7 @@ int main(int argc, char **argv) {
         std::printf("Variable assignments:\n%s\n", out.c_str());
     }
     if (s) odesat_solver_destroy(s);
+    if (st) odesat_stoch_destroy(st);
     odesat_cnf_free(norm);
     odesat_cnf_free(reduced);
     odesat_trace_free(trace);

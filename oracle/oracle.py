@@ -71,6 +71,14 @@ def lib():
         L.oc_init_voltages.restype = None
         L.oc_hash3.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
         L.oc_hash3.restype = C.c_uint64
+        _u64p = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
+        L.oc_stoch_hash.argtypes = [C.c_uint64] * 4
+        L.oc_stoch_hash.restype = C.c_uint64
+        L.oc_stoch_step.argtypes = [C.POINTER(_Formula), _u8p, _u64p, C.c_uint64, C.c_uint64, C.c_uint64, _u64p, _u64p]
+        L.oc_stoch_step.restype = C.c_int
+        L.oc_stoch_search.argtypes = [C.POINTER(_Formula), _u8p, _u64p, C.c_uint64, C.c_uint64, C.c_int64, _u64p,
+                                      C.POINTER(C.c_int)]
+        L.oc_stoch_search.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -150,6 +158,27 @@ class Oracle:
         xs = np.empty(self.m, self.T)
         self._fn("init_short_term_memory")(C.byref(self._f), xs)
         return xs
+
+    # -- stoch.rs (stoch_oracle.c) --------------------------------------------------------------
+    def stoch_step(self, v, xl, seed, replica, step):
+        """One step in place on v (uint8[n]) and xl (uint64[m]); returns all-satisfied (or raises
+        where the reference panics)."""
+        tot = np.zeros(max(self.n, 1), np.uint64)
+        uns = np.zeros(max(self.n, 1), np.uint64)
+        r = self.L.oc_stoch_step(C.byref(self._f), v, xl, seed, replica, step, tot, uns)
+        if r < 0:
+            raise ValueError("a variable occurs in no clause (stoch.rs:70 panics)")
+        return bool(r)
+
+    def stoch_search(self, v, xl, seed, replica, steps):
+        """search (stoch.rs:83-110) from (v, xl) in place, at most `steps` steps.
+        Returns (steps_taken, sat)."""
+        scratch = np.zeros(2 * max(self.n, 1), np.uint64)
+        sat = C.c_int(0)
+        t = self.L.oc_stoch_search(C.byref(self._f), v, xl, seed, replica, steps, scratch, C.byref(sat))
+        if t < 0:
+            raise ValueError("a variable occurs in no clause (stoch.rs:70 panics)")
+        return int(t), bool(sat.value)
 
     def batch_run(self, v, xs, xl, adaptive, tol, dt, steps, zeta, nthreads=1):
         """Independent replicas, replica-major [B, n] / [B, m], in place."""

@@ -1,7 +1,7 @@
 """The `odesat` command line (odesat_amd/csrc/cli.cpp; the reference's src/main.rs:12-397).
 
 CPU: argument handling (clap's required flags, bad values, the out-of-scope stoch command) -- no
-solver is created on those paths.  GPU: solve / batch / inter end to end on small formulas, the
+solver is created on those paths.  GPU: solve / batch / inter / stoch end to end on small formulas, the
 reported assignment re-checked on the host against the file's clauses."""
 import os
 import subprocess
@@ -67,6 +67,7 @@ def test_help():
     (("solve", "-f", "x.cnf", "-s", "abc"), "invalid value"),
     (("batch", "-f", "x.cnf", "-n", "-5", "-b", "2"), "invalid value"),
     (("solve", "-f", "x.cnf", "--bogus", "1"), "unexpected argument"),
+    (("stoch", "-f", "x.cnf", "-s", "0.1"), "stoch takes only"),
     (("solve", "-f"), "value is required"),
     (("inter", "-f", "x.cnf", "-b", "0"), "batch-size"),
 ])
@@ -74,11 +75,6 @@ def test_usage_errors(argv, needle):
     r = run(*argv)
     assert r.returncode == 2
     assert needle in r.stderr
-
-
-def test_stoch_is_declared_out_of_scope(golden_dir):
-    r = run("stoch", "-f", os.path.join(golden_dir, "small.cnf"))
-    assert r.returncode == 2 and "stoch" in r.stderr
 
 
 def test_missing_file():
@@ -151,3 +147,24 @@ def test_solve_preprocesses_then_rebuilds_eliminated_variables(golden_dir, tmp_p
     with open(path) as fh:
         clauses = [ln for ln in fh.read().splitlines() if ln and ln[0] not in "cp%"]
     assert satisfies(assign, clauses)
+
+
+@pytest.mark.gpu
+def test_stoch_solves_easy(golden_dir, tmp_path):
+    """main.rs:206-251: preprocessing, the discrete search from v = false, trace, check."""
+    out = tmp_path / "stoch.txt"
+    path = os.path.join(golden_dir, "easy.cnf")
+    r = run("stoch", "-f", path, "-o", str(out), "--seed", "3")
+    assert r.returncode == 0, r.stderr
+    assert "Clauses: 267 | Vars: 43" in r.stdout and "satisfies formula: true" in r.stdout
+    assign = parse_render(out.read_text())
+    with open(path) as fh:
+        clauses = [ln for ln in fh.read().splitlines() if ln and ln[0] not in "cp%"]
+    assert satisfies(assign, clauses)
+
+
+@pytest.mark.gpu
+def test_stoch_bounded_on_unsat(golden_dir):
+    r = run("stoch", "-f", os.path.join(golden_dir, "hard.cnf"), "-n", "300")
+    assert r.returncode == 0, r.stderr
+    assert "Checking if solution vector satisfies formula: false" in r.stdout
