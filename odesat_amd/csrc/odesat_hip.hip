@@ -368,7 +368,16 @@ bool res_fits(int64_t n, int R, size_t tsize, bool adaptive) {
     return n < (1ll << 24) && res_lds_bytes(n, R, tsize, adaptive) <= RES_LDS_MAX;
 }
 
-int res_capacity(int R) { return R == 1 ? ResShape<1>::NL : (R == 2 ? ResShape<2>::NL : ResShape<4>::NL); }
+int res_capacity(int R) {
+    switch (R) {
+        case 1: return ResShape<1>::NL;
+        case 2: return ResShape<2>::NL;
+        case 4: return ResShape<4>::NL;
+        case 8: return ResShape<8>::NL;
+        case 16: return ResShape<16>::NL;
+        default: return ResShape<32>::NL;
+    }
+}
 
 // Var-disjoint clause tiles (resident.hpp): clause c, in the reference's order, goes to the first
 // tile after the last tile holding any of its variables that still has room.  Returns the
@@ -384,7 +393,7 @@ constexpr int kP3[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}
 // G/R terms do not depend on the order of 3 distinct variables) so that each of the 3 gather
 // instructions sees distinct keys.  The dv read-modify-write uses the same addresses + a constant.
 void bank_layout(const odesat_cnf *f, int R, std::vector<int32_t> &cl, std::vector<uint8_t> &code) {
-    const int GS = 32 / R;
+    const int GS = std::max(1, 32 / R);
     const int64_t s = (int64_t)cl.size();
     if (s == 0) return;
     const int64_t G = (s + GS - 1) / GS;
@@ -445,6 +454,42 @@ void bank_layout(const odesat_cnf *f, int R, std::vector<int32_t> &cl, std::vect
             code[grp[g][i]] = (uint8_t)pc[i];
         }
     }
+}
+
+// Tile depth of the var-disjoint tiling (build_tiles' greedy, capacity cap) -- its number of tiles.
+int64_t tile_count(const odesat_cnf *f, int64_t n, int cap) {
+    const int64_t m = f->nclauses();
+    std::vector<int32_t> last((size_t)n, -1), fill;
+    int32_t first_open = 0;
+    for (int64_t c = 0; c < m; ++c) {
+        int32_t t = first_open;
+        for (int64_t sl = f->clause_ptr[c]; sl < f->clause_ptr[c + 1]; ++sl) t = std::max(t, last[f->var[sl]] + 1);
+        while (t < (int32_t)fill.size() && fill[t] >= cap) ++t;
+        if (t == (int32_t)fill.size()) fill.push_back(0);
+        fill[t] += 1;
+        while (first_open < (int32_t)fill.size() && fill[first_open] >= cap) ++first_open;
+        for (int64_t sl = f->clause_ptr[c]; sl < f->clause_ptr[c + 1]; ++sl) last[f->var[sl]] = t;
+    }
+    return (int64_t)fill.size();
+}
+
+// RESIDENT replicas per workgroup.  A tile's depth is set by the clause-order chains, not by its
+// capacity, so a small instance leaves most of a 512-clause tile empty (config 3, n = 250: ~35
+// clauses per tile) and one replica per workgroup wastes the CU.  Then R > 1 replicas share a
+// workgroup (tile capacity 1024 / R): the largest R <= 32 that still gives every CU a workgroup and
+// whose state (with the adaptive full-step clone) fits in LDS.  Measured on config 3 (adaptive,
+// MI355X): B = 1024 R = 1 / 4: 7.2 / 13.9 M replica-steps/s; B = 4096 R = 4 / 16: 14.1 / 48.7 M.
+// Instances whose tiles are at least half full keep R = 1 (ONCHIP / RESIDENT at one replica).
+int small_instance_width(const odesat_cnf *f, int64_t n, int64_t batch, int device, size_t tsize) {
+    const int64_t m = f->nclauses();
+    if (m == 0 || std::getenv("ODESAT_GROUP_WIDTH")) return 1;
+    const int64_t nt = tile_count(f, n, ResShape<1>::NL);
+    if (2 * m >= nt * (int64_t)ResShape<1>::NL) return 1;
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+    int R = 1;
+    while (R < 32 && (batch + 2 * R - 1) / (2 * R) >= cus && res_fits(n, 2 * R, tsize, true)) R *= 2;
+    return R;
 }
 
 bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, std::vector<int32_t> &perm,
@@ -588,6 +633,9 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
         case 1: return go(IC<1>{});
         case 2: return go(IC<2>{});
         case 4: return go(IC<4>{});
+        case 8: return go(IC<8>{});
+        case 16: return go(IC<16>{});
+        case 32: return go(IC<32>{});
         default: return fail(ODESAT_EINVAL, "resident layout not available");
     }
 }
@@ -868,8 +916,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     // ODESAT_GROUP_WIDTH overrides (tuning; RESIDENT only if that width admits it).
     int lw = 1, res_r = 0;
     if (res_fits(n, 1, s->tsize, false)) {  // measured (config 2, B = 1024): R = 1 beats R = 2 by 1.13x
-        res_r = 1;
-        lw = 1;
+        res_r = lw = small_instance_width(f, n, batch, device, s->tsize);
     } else {
         while (lw < batch && lw < 64) lw <<= 1;
     }
@@ -877,7 +924,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         const int want = std::atoi(ev);
         if (want == 1 || want == 2 || want == 4 || want == 8 || want == 16 || want == 32 || want == 64) {
             lw = want;
-            res_r = (want <= 4 && res_fits(n, want, s->tsize, false)) ? want : 0;
+            res_r = (want <= 32 && res_fits(n, want, s->tsize, false)) ? want : 0;
         }
     }
     // the internal clause order: var-disjoint tiles for RESIDENT, else the file order

@@ -98,6 +98,8 @@ __device__ __forceinline__ void gather(const Slot &S, Gath &G) {
 #define ONCHIP_ORDER 0
 #endif
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 struct Front {  // first half: literal values and their min / second min
     uint32_t a0, a1, a2, hi;
     float val0, val1, val2, mn, sec;
@@ -109,8 +111,15 @@ __device__ __forceinline__ void front(const Gath &G, Front &F) {
     F.a2 = G.a2;
     F.hi = G.hi;
     const uint32_t s0 = G.hi & 0x80000000u, s1 = (G.hi << 1) & 0x80000000u, s2 = (G.hi << 2) & 0x80000000u;
+#ifdef ONCHIP_PK
+    const f2 v01 = {__uint_as_float(__float_as_uint(G.v0) ^ s0), __uint_as_float(__float_as_uint(G.v1) ^ s1)};
+    const f2 val01 = f2{1.0f, 1.0f} - v01;  // one packed subtract for two literals
+    F.val0 = val01.x;
+    F.val1 = val01.y;
+#else
     F.val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
     F.val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
+#endif
     F.val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
     F.mn = fminf(fminf(F.val0, F.val1), F.val2);                  // min (:49-55)
     F.sec = __builtin_amdgcn_fmed3f(F.val0, F.val1, F.val2);       // second min, ties -> min
@@ -124,7 +133,12 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
     const float mn = F.mn;
     const float xs = mem.x, xl = mem.y;
     const float tt = xl * xs;
+#ifdef ONCHIP_PK
+    const f2 tms = f2{tt, tt} * f2{mn, F.sec};
+    const float tm = tms.x, ts = tms.y;
+#else
     const float tm = tt * mn, ts = tt * F.sec;
+#endif
     Q.a0 = F.a0;
     Q.a1 = F.a1;
     Q.a2 = F.a2;
@@ -133,10 +147,20 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
     Q.d2 = __uint_as_float(__float_as_uint(F.val2 != mn ? tm : ts) ^ s2);
     cmax = max(cmax, __float_as_uint(mn));  // :88 -- unsat iff max mn >= 0.5
     asm volatile("" : "+v"(cmax));          // fold now: deferred, it would keep every tile's mn live
+#ifdef ONCHIP_PK
+    // the same operations two at a time: {mn - 0.5, mn - 0.1}, {2 dxs, dxl}, {h/2 2dxs, h dxl},
+    // {xs, xl} + that (a - b is a + (-b) exactly; products commute)
+    const f2 c = f2{mn, mn} + f2{-0.5f, -0.1f};
+    const f2 dd = f2{20.0f * (xs + 0.001f), 2.5f} * c;
+    const f2 nm = f2{xs, xl} + f2{hh, h} * dd;
+    mem.x = __builtin_amdgcn_fmed3f(nm.x, 0.001f, 1.0f - 0.001f);  // :94
+    mem.y = __builtin_amdgcn_fmed3f(nm.y, 1.0f, a.xl_max);         // :95
+#else
     const float dxs2 = (20.0f * (xs + 0.001f)) * (mn - 0.5f);  // 2 dxs (:84)
     const float dxl = 2.5f * (mn - 0.1f);                       // :85
     mem.x = __builtin_amdgcn_fmed3f(xs + hh * dxs2, 0.001f, 1.0f - 0.001f);  // :94
     mem.y = __builtin_amdgcn_fmed3f(xl + h * dxl, 1.0f, a.xl_max);           // :95
+#endif
     asm volatile("" : "+v"(mem.x), "+v"(mem.y));  // update now: sunk into later tiles it keeps mn live
 }
 

@@ -407,10 +407,10 @@ def _run_layout(monkeypatch, f, B, prec, width, **kw):
 
 @pytest.mark.parametrize("name", ["rand200", "small", "hard"])
 @pytest.mark.parametrize("prec", ["f64", "f32"])
-@pytest.mark.parametrize("width", [1, 2, 4])
+@pytest.mark.parametrize("width", [1, 2, 4, 8, 16, 32])
 @pytest.mark.parametrize("mode", ["fixed-each", "fixed-any", "fixed-none", "adaptive-each", "adaptive-any"])
 def test_resident_widths_match_fused_w64(monkeypatch, name, prec, width, mode):
-    """RESIDENT with R = 1, 2, 4 replicas per workgroup (LDS-resident voltages, tiled clause pass +
+    """RESIDENT with R = 1 .. 32 replicas per workgroup (LDS-resident voltages, tiled clause pass +
     ordered fold) == FUSED at group width 64: every stop policy, fixed and adaptive steps."""
     from odesat_amd import _lib
     f = product_formula(name)
@@ -428,6 +428,31 @@ def test_resident_widths_match_fused_w64(monkeypatch, name, prec, width, mode):
     assert same(r1["dt"], r2["dt"])
     for x, y in zip(s1, s2):
         assert same(x, y)
+
+
+def test_small_instance_width_config3():
+    """Config 3 (n = 250): tiles ~35 clauses deep-chained, so the solver packs R replicas per
+    workgroup (the largest R that still gives every CU a workgroup): B = 1024 -> R = 4, B = 4096 ->
+    R = 16; the trajectories equal FUSED's bit for bit on a replica subset."""
+    from odesat_amd import _lib
+    c = wl.CONFIGS["config3"]
+    var, neg = wl.random_ksat(c["n"], c["m"], 3, c["seed"])
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
+    for B, R in ((1024, 4), (4096, 16)):
+        with Solver(f, B, "f32") as s:
+            assert (s.algorithm, s.group_width) == (_lib.ODESAT_ALG_RESIDENT, R)
+            s.init_state(42)
+            r1 = s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=40, stop=ODESAT_STOP_EACH, poll_interval=8)
+            st1 = s.get_state(0, 70)
+        with Solver(f, B, "f32") as s:
+            s.set_algorithm(_lib.ODESAT_ALG_FUSED)
+            s.init_state(42)
+            r2 = s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=40, stop=ODESAT_STOP_EACH, poll_interval=8)
+            st2 = s.get_state(0, 70)
+        assert np.array_equal(r1["first_sat_step"], r2["first_sat_step"]) and same(r1["dt"], r2["dt"])
+        for x, y in zip(st1, st2):
+            assert same(x, y)
 
 
 def test_default_layout_is_resident_for_config2():
