@@ -94,12 +94,6 @@ __device__ __forceinline__ void gather(const Slot &S, Gath &G) {
 //   the clamps are med3 (finite arguments: the host requires a finite dt).
 // Scalings by 0.5 / 2 / 2.5 / +-1 are exact here (no subnormals: |A| >= 0.02, |mn - c| >= 2^-26 or 0,
 // |xl xs sel| >= 6e-11 or 0).
-#ifndef ONCHIP_ORDER
-#define ONCHIP_ORDER 0
-#endif
-
-typedef float f2 __attribute__((ext_vector_type(2)));
-
 struct Front {  // first half: literal values and their min / second min
     uint32_t a0, a1, a2, hi;
     float val0, val1, val2, mn, sec;
@@ -111,15 +105,8 @@ __device__ __forceinline__ void front(const Gath &G, Front &F) {
     F.a2 = G.a2;
     F.hi = G.hi;
     const uint32_t s0 = G.hi & 0x80000000u, s1 = (G.hi << 1) & 0x80000000u, s2 = (G.hi << 2) & 0x80000000u;
-#ifdef ONCHIP_PK
-    const f2 v01 = {__uint_as_float(__float_as_uint(G.v0) ^ s0), __uint_as_float(__float_as_uint(G.v1) ^ s1)};
-    const f2 val01 = f2{1.0f, 1.0f} - v01;  // one packed subtract for two literals
-    F.val0 = val01.x;
-    F.val1 = val01.y;
-#else
     F.val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
     F.val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
-#endif
     F.val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
     F.mn = fminf(fminf(F.val0, F.val1), F.val2);                  // min (:49-55)
     F.sec = __builtin_amdgcn_fmed3f(F.val0, F.val1, F.val2);       // second min, ties -> min
@@ -133,12 +120,7 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
     const float mn = F.mn;
     const float xs = mem.x, xl = mem.y;
     const float tt = xl * xs;
-#ifdef ONCHIP_PK
-    const f2 tms = f2{tt, tt} * f2{mn, F.sec};
-    const float tm = tms.x, ts = tms.y;
-#else
     const float tm = tt * mn, ts = tt * F.sec;
-#endif
     Q.a0 = F.a0;
     Q.a1 = F.a1;
     Q.a2 = F.a2;
@@ -147,20 +129,10 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
     Q.d2 = __uint_as_float(__float_as_uint(F.val2 != mn ? tm : ts) ^ s2);
     cmax = max(cmax, __float_as_uint(mn));  // :88 -- unsat iff max mn >= 0.5
     asm volatile("" : "+v"(cmax));          // fold now: deferred, it would keep every tile's mn live
-#ifdef ONCHIP_PK
-    // the same operations two at a time: {mn - 0.5, mn - 0.1}, {2 dxs, dxl}, {h/2 2dxs, h dxl},
-    // {xs, xl} + that (a - b is a + (-b) exactly; products commute)
-    const f2 c = f2{mn, mn} + f2{-0.5f, -0.1f};
-    const f2 dd = f2{20.0f * (xs + 0.001f), 2.5f} * c;
-    const f2 nm = f2{xs, xl} + f2{hh, h} * dd;
-    mem.x = __builtin_amdgcn_fmed3f(nm.x, 0.001f, 1.0f - 0.001f);  // :94
-    mem.y = __builtin_amdgcn_fmed3f(nm.y, 1.0f, a.xl_max);         // :95
-#else
     const float dxs2 = (20.0f * (xs + 0.001f)) * (mn - 0.5f);  // 2 dxs (:84)
     const float dxl = 2.5f * (mn - 0.1f);                       // :85
     mem.x = __builtin_amdgcn_fmed3f(xs + hh * dxs2, 0.001f, 1.0f - 0.001f);  // :94
     mem.y = __builtin_amdgcn_fmed3f(xl + h * dxl, 1.0f, a.xl_max);           // :95
-#endif
     asm volatile("" : "+v"(mem.x), "+v"(mem.y));  // update now: sunk into later tiles it keeps mn live
 }
 
@@ -174,7 +146,6 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
 __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &slot3, float2 &mem1, Pend &P, Front &Fn,
                                           Gath &Gn, int t, float h, float hh, uint32_t &cmax) {
     const float o0 = lds_f(P.a0 + DVC), o1 = lds_f(P.a1 + DVC), o2 = lds_f(P.a2 + DVC);
-#if ONCHIP_ORDER == 0
     lds_st(P.a0 + DVC, o0 + P.d0);
     lds_st(P.a1 + DVC, o1 + P.d1);
     lds_st(P.a2 + DVC, o2 + P.d2);
@@ -185,35 +156,6 @@ __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &sl
     __builtin_amdgcn_sched_barrier(0);
     back(a, Fn, mem1, h, hh, P, cmax);  // P <- tile t+1's terms (tile t's were written above)
     front(Gn, Fn);                      // Fn <- tile t+2's first half
-#elif ONCHIP_ORDER == 1
-    __builtin_amdgcn_sched_barrier(0);
-    Gath G3;
-    gather(slot3, G3);
-    slot3 = load_rec(R, t + 7);
-    __builtin_amdgcn_sched_barrier(0);
-    const Front F1 = Fn;
-    front(Gn, Fn);                      // Fn <- tile t+2's first half, under the dv reads
-    __builtin_amdgcn_sched_barrier(0);
-    lds_st(P.a0 + DVC, o0 + P.d0);
-    lds_st(P.a1 + DVC, o1 + P.d1);
-    lds_st(P.a2 + DVC, o2 + P.d2);
-    __builtin_amdgcn_sched_barrier(0);
-    back(a, F1, mem1, h, hh, P, cmax);  // P <- tile t+1's terms, under the dv writes
-#else
-    __builtin_amdgcn_sched_barrier(0);
-    Gath G3;
-    gather(slot3, G3);
-    slot3 = load_rec(R, t + 7);
-    __builtin_amdgcn_sched_barrier(0);
-    const Pend Q = P;
-    back(a, Fn, mem1, h, hh, P, cmax);
-    __builtin_amdgcn_sched_barrier(0);
-    lds_st(Q.a0 + DVC, o0 + Q.d0);
-    lds_st(Q.a1 + DVC, o1 + Q.d1);
-    lds_st(Q.a2 + DVC, o2 + Q.d2);
-    __builtin_amdgcn_sched_barrier(0);
-    front(Gn, Fn);
-#endif
     __builtin_amdgcn_sched_barrier(0);  // a tile's work stays between its barriers
     __syncthreads();
     __builtin_amdgcn_sched_barrier(0);
