@@ -193,8 +193,12 @@ typedef struct {
     int64_t max_steps;     /* > 0 (the reference's None = unbounded is refused) */
     int32_t poll_interval; /* steps between host polls of the stop condition (0 = default 32); with
                               ODESAT_ALG_RESIDENT also the steps per kernel launch (STOP_ANY: 1) */
-    int32_t reserved;
+    int32_t dt_policy;     /* ODESAT_DT_PER_REPLICA (0, the device's) | ODESAT_DT_SHARED_SERIAL (1: the
+                              reference's one dt threaded through the replicas, system.rs:314-326; the
+                              CPU oracle's policy, refused by the device) */
 } odesat_params;
+#define ODESAT_DT_PER_REPLICA 0
+#define ODESAT_DT_SHARED_SERIAL 1
 
 /* system.rs:156-239 (simulate) applied to every replica at once, or :241-359 (simulate_inter)
  * with stop = ODESAT_STOP_ANY.  Replicas continue from their current state.
@@ -209,6 +213,25 @@ int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t *first_sat
 
 /* Block until all work queued by the solver is done. */
 int odesat_synchronize(odesat_solver *s);
+
+/* ------------------------------------------- one-call boundary --------------- */
+
+/* The drop-in for simulate / simulate_inter (system.rs:156-163, :241-248) in one call.
+ * odesat_create: a normalised formula as CSR (clause_ptr[m+1], lits = var << 1 | negated, every
+ * var < n) for `device`; NULL on error with the message in err[errlen] (and odesat_last_error()).
+ * odesat_run: B replicas' f32 states, replica-innermost (v0[n][B], xs0[m][B], xl0[m][B]), are
+ * integrated per *p: adaptive 0/1 (FIXED/ADAPTIVE), dt, tol, zeta (< 0: density heuristic),
+ * max_steps (0 = the reference's None: until every replica (STOP_EACH) / some replica (STOP_ANY)
+ * is allsat), stop, dt_policy (the device runs ODESAT_DT_PER_REPLICA only).  The final states go to
+ * v_out / xs_out / xl_out (same layout; any may be NULL), first_sat_step[B] (-1 = never) and
+ * steps_done[B].  Host buffers stay the caller's; device memory is the context's. */
+typedef struct odesat_ctx odesat_ctx;
+odesat_ctx *odesat_create(int device, int32_t n, int32_t m, const int32_t *clause_ptr, const int32_t *lits,
+                          char *err, size_t errlen);
+int odesat_run(odesat_ctx *ctx, const odesat_params *p, int32_t B, const float *v0, const float *xs0,
+               const float *xl0, float *v_out, float *xs_out, float *xl_out, int64_t *first_sat_step,
+               int64_t *steps_done);
+void odesat_destroy(odesat_ctx *ctx);
 
 /* --------------------------------------------------------------- measurement ----------------- */
 

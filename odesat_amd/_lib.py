@@ -30,7 +30,7 @@ class OdesatError(RuntimeError):
 class Params(C.Structure):
     _fields_ = [("adaptive", C.c_int32), ("stop", C.c_int32), ("tol", C.c_double), ("dt", C.c_double),
                 ("zeta", C.c_double), ("max_steps", C.c_int64), ("poll_interval", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("dt_policy", C.c_int32)]
 
 
 _P = C.c_void_p
@@ -38,6 +38,7 @@ _i64 = C.c_int64
 _dp = C.POINTER(C.c_double)
 _u8p = C.POINTER(C.c_uint8)
 _i64p = C.POINTER(C.c_int64)
+_fp = C.POINTER(C.c_float)
 
 # name -> (restype, argtypes); kept in sync with include/odesat.h (tests/test_abi.py checks)
 SIGNATURES = {
@@ -54,6 +55,10 @@ SIGNATURES = {
     "odesat_cnf_normalize": (C.c_int, [_P, C.POINTER(_P), _i64p, _i64p]),
     "odesat_cnf_evaluate": (C.c_int, [_P, _u8p, _i64]),
     "odesat_cnf_init_short_term_memory": (C.c_int, [_P, _dp]),
+    "odesat_create": (_P, [C.c_int, C.c_int32, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.c_char_p,
+                           C.c_size_t]),
+    "odesat_run": (C.c_int, [_P, C.POINTER(Params), C.c_int32, _fp, _fp, _fp, _fp, _fp, _fp, _i64p, _i64p]),
+    "odesat_destroy": (None, [_P]),
     "odesat_stoch_create": (C.c_int, [C.c_int, _P, _i64, C.POINTER(_P)]),
     "odesat_stoch_destroy": (None, [_P]),
     "odesat_stoch_reset": (C.c_int, [_P, _i64, _i64]),

@@ -1293,6 +1293,8 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
     int rc;
     if ((rc = check_solver(s))) return rc;
     if (!p) return fail(ODESAT_EINVAL, "null params");
+    if (p->dt_policy != ODESAT_DT_PER_REPLICA)
+        return fail(ODESAT_EINVAL, "the device runs every replica with its own dt (ODESAT_DT_PER_REPLICA)");
     if (p->max_steps <= 0 || p->max_steps > INT_MAX - 1)
         return fail(ODESAT_EINVAL, "max_steps must be in [1, 2^31-2] (unbounded runs are refused)");
     if (p->stop != ODESAT_STOP_EACH && p->stop != ODESAT_STOP_ANY && p->stop != ODESAT_STOP_NONE)

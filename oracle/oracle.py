@@ -71,6 +71,10 @@ def lib():
         L.oc_init_voltages.restype = None
         L.oc_hash3.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
         L.oc_hash3.restype = C.c_uint64
+        for p, Rp in (("oc64_", _f64p), ("oc32_", _f32p)):
+            getattr(L, p + "run").argtypes = [C.c_int32, C.c_int32, _i32p, _i32p, C.c_void_p, C.c_int32, Rp, Rp, Rp,
+                                              Rp, Rp, Rp, _i64p, _i64p]
+            getattr(L, p + "run").restype = C.c_int
         _u64p = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
         L.oc_stoch_hash.argtypes = [C.c_uint64] * 4
         L.oc_stoch_hash.restype = C.c_uint64
@@ -189,6 +193,23 @@ class Oracle:
         total = self._fn("batch_run")(C.byref(self._f), B, v, xs, xl, 1 if adaptive else 0, tol, dt, steps,
                                       zeta, nthreads, sat, done, dts)
         return total, sat, done, dts
+
+
+def run(n, clause_ptr, lits, params, v0, xs0, xl0, precision="f32"):
+    """SURVEY 8(b) one-call boundary on the CPU (oc64_run / oc32_run): states replica-innermost
+    [n][B] / [m][B]; params = a ctypes struct with odesat_params' layout.  Returns
+    (v, xs, xl, first_sat_step[B], steps_done[B])."""
+    T = np.float64 if precision == "f64" else np.float32
+    cp = np.ascontiguousarray(clause_ptr, np.int32)
+    lt = np.ascontiguousarray(lits, np.int32) if len(lits) else np.zeros(1, np.int32)
+    v0, xs0, xl0 = (np.ascontiguousarray(a, T) for a in (v0, xs0, xl0))
+    m, B = len(cp) - 1, v0.shape[1]
+    v, xs, xl = np.empty_like(v0), np.empty_like(xs0), np.empty_like(xl0)
+    sat, done = np.zeros(B, np.int64), np.zeros(B, np.int64)
+    fn = getattr(lib(), ("oc64_" if precision == "f64" else "oc32_") + "run")
+    if fn(n, m, cp, lt, C.cast(C.byref(params), C.c_void_p), B, v0, xs0, xl0, v, xs, xl, sat, done) != 0:
+        raise ValueError("oracle run failed")
+    return v, xs, xl, sat, done
 
 
 def init_voltages(seed, r0, B, n):
