@@ -95,7 +95,16 @@ def time_gpu(solver, steps, warmup, dist, local, profile):
     return t1 - t0, ms, launches
 
 
-def cpu_baseline(cp, var, neg, n, m, replicas, steps):
+def cpu_threads():
+    """The host cores this job may use: OMP_NUM_THREADS (16 on the GPU box: its share of a larger
+    machine, whose os.cpu_count() would overstate it), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(cp, var, neg, n, m, replicas, steps, threads=1):
     """Bounded sample of the same workload on the host: the f64 line-by-line oracle (the reference's
     own precision and algorithm), 1 thread, `replicas` x `steps` fixed steps."""
     import numpy as np
@@ -106,11 +115,12 @@ def cpu_baseline(cp, var, neg, n, m, replicas, steps):
     xs = np.tile(o.init_short_term_memory(), (replicas, 1))
     xl = np.ones((replicas, m))
     t0 = time.perf_counter()
-    o.batch_run(v, xs, xl, False, 1e-3, 0.01, steps, 0.001, nthreads=1)
+    o.batch_run(v, xs, xl, False, 1e-3, 0.01, steps, 0.001, nthreads=threads)
     dt = time.perf_counter() - t0
-    return {"value": replicas * steps / dt, "unit": "replica-steps/s", "cores": 1, "kind": "port",
-            "sample": f"C f64 oracle (line-by-line restatement of system.rs), 1 thread, {replicas} replicas x "
-                      f"{steps} fixed steps of the same n=10k m=42k instance ({dt:.1f} s)"}
+    return {"value": replicas * steps / dt, "unit": "replica-steps/s", "cores": threads, "kind": "port",
+            "sample": f"C f64 oracle (line-by-line restatement of system.rs), {threads} thread(s) (OpenMP over "
+                      f"replicas), {replicas} replicas x {steps} fixed steps of the same n=10k m=42k instance "
+                      f"({dt:.1f} s)"}
 
 
 def main():
@@ -204,9 +214,12 @@ def main():
                  "value": args.extra_batch * world * args.steps / w2,
                  "ms_per_step": w2 * 1e3 / args.steps}
 
-    cpu = None
+    cpu = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(cp, v_, n_, n, m, args.cpu_replicas, args.cpu_steps)
+        t = cpu_threads()
+        if t > 1:  # the same oracle on every host core this job has, beside the 1-core line
+            cpu_all = cpu_baseline(cp, v_, n_, n, m, args.cpu_replicas * t, args.cpu_steps, threads=t)
 
     if rank == 0:
         out = {
@@ -230,6 +243,7 @@ def main():
             "step_kernels_ms": {"clause": ms[0], "variable": ms[1], "status": ms[2]},
             "step_algorithmic_GBps": step_bytes * args.steps / wall / 1e9,
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
             "extra_batch": extra,
             "ab_hbm_streaming": ab,
         }

@@ -19,6 +19,7 @@
 #include "cnf.hpp"
 #include "kernels.hpp"
 #include "resident.hpp"
+#include "wave.hpp"
 #include "onchip.hpp"
 
 using odesat::fail;
@@ -59,6 +60,10 @@ struct odesat_solver {
     // RESIDENT (resident.hpp): group width W == res_R replicas per workgroup; clauses are stored
     // in the internal (tile) order, cmap[original clause] = internal clause
     int res_R = 0;        // 0 = the layout does not admit the resident kernel
+    bool res_narrow = false;  // RESIDENT with one wave per workgroup (R = 1, 64-clause tiles)
+    bool res_wave = false;    // RESIDENT as k_wave (wave.hpp): small 3-SAT, one wave per replica, variable fold
+    int4 *wv_tp4 = nullptr;   // [m] k_wave: variable-major term position of each literal
+    int32_t *wv_vst = nullptr;  // [n+1] k_wave: first term position of each variable
     bool res_ada = false; // adaptive steps fit in LDS too (else they run FUSED on the same layout)
     int res_ntiles = 0;
     int32_t *res_tc = nullptr, *cmap = nullptr;
@@ -535,7 +540,8 @@ bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, std::v
 // ONCHIP eligibility and slot-major records (onchip.hpp).  tiles = the padded tile starts, lits =
 // the internal-order literals (var << 1 | neg).
 int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std::vector<int32_t> &lits) {
-    if (s->res_R != 1 || s->dtype != ODESAT_F32 || s->uniform_k != 3 || s->n > onchip::MAX_N) return ODESAT_OK;
+    if (s->res_R != 1 || s->res_narrow || s->res_wave || s->dtype != ODESAT_F32 || s->uniform_k != 3 || s->n > onchip::MAX_N)
+        return ODESAT_OK;
     if (const char *ev = std::getenv("ODESAT_ONCHIP"))
         if (std::atoi(ev) == 0) return ODESAT_OK;
     const int nt = (int)tiles.size() - 1;
@@ -577,25 +583,73 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
     return ODESAT_OK;
 }
 
-template <typename T, int R, bool ADA, bool K3> int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
+template <typename T, int R, bool ADA, bool K3, int NTHR = ResShape<R>::NTH>
+int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     static bool attr_set = false;  // per instantiation
     const size_t lds = res_lds_bytes(s->n, R, sizeof(T), ADA);
     if (!attr_set) {
-        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3>),
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)RES_LDS_MAX));
         attr_set = true;
     }
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_resident<T, R, ADA, K3>), dim3(s->G), dim3(ResShape<R>::NTH), lds, s->stream, a);
+        hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR>), dim3(s->G), dim3(NTHR), lds, s->stream, a);
+    }
+    HIP_TRY(hipGetLastError());
+    return ODESAT_OK;
+}
+
+template <typename T, bool ADA> int launch_wave_k(odesat_solver *s, const WArgs<T> &a) {
+    static bool attr_set = false;  // per instantiation
+    const size_t lds = wave_lds_bytes(s->n, s->m, s->L, sizeof(T), ADA);
+    if (!attr_set) {
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wave<T, ADA>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)RES_LDS_MAX));
+        attr_set = true;
+    }
+    {
+        Timed tm(s, 0);
+        hipLaunchKernelGGL((k_wave<T, ADA>), dim3(s->G), dim3(WAVE_NTH), lds, s->stream, a);
     }
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
 }
 
 template <typename T>
+int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
+                int stop_mode) {
+    WArgs<T> a{};
+    a.cl4 = s->res_cl4;
+    a.tp4 = s->wv_tp4;
+    a.vst = s->wv_vst;
+    a.v0 = (T *)s->v[0];
+    a.v1 = (T *)s->v[1];
+    a.c0 = (T *)s->c[0];
+    a.c1 = (T *)s->c[1];
+    a.par = s->par;
+    a.dtr = (T *)s->dtr;
+    a.act = s->act;
+    a.sat_step = s->sat_step;
+    a.steps_done = s->steps_done;
+    a.stop = s->stop;
+    a.n = (int32_t)s->n;
+    a.m = (int32_t)s->m;
+    a.L = (int32_t)s->L;
+    a.step0 = step0;
+    a.nsteps = nsteps;
+    a.stop_mode = stop_mode;
+    a.dt = (T)dt;
+    a.zeta = (T)zeta;
+    a.xl_max = (T)1e4 * (T)s->m;  // system.rs:95
+    a.tol = tol;
+    return adaptive ? launch_wave_k<T, true>(s, a) : launch_wave_k<T, false>(s, a);
+}
+
+template <typename T>
 int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
                     int stop_mode) {
+    if (s->res_wave) return launch_wave<T>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode);
     RArgs<T> a{};
     a.cl4 = s->res_cl4;
     a.cptr = s->cptr;
@@ -624,6 +678,13 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
     a.xl_max = (T)1e4 * (T)s->m;  // system.rs:95
     a.tol = tol;
     const bool k3 = s->uniform_k == 3;
+    if (s->res_narrow) {
+        if (adaptive)
+            return k3 ? launch_resident_k<T, 1, true, true, RES_NARROW>(s, a)
+                      : launch_resident_k<T, 1, true, false, RES_NARROW>(s, a);
+        return k3 ? launch_resident_k<T, 1, false, true, RES_NARROW>(s, a)
+                  : launch_resident_k<T, 1, false, false, RES_NARROW>(s, a);
+    }
     auto go = [&](auto rr) -> int {
         constexpr int R = decltype(rr)::value;
         if (adaptive) return k3 ? launch_resident_k<T, R, true, true>(s, a) : launch_resident_k<T, R, true, false>(s, a);
@@ -864,7 +925,7 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     for (auto e : s->pool) (void)hipEventDestroy(e);
     void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->pc, s->ps, s->empty, s->inc, s->v[0], s->v[1], s->c[0],
                     s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
-                    s->sat_step, s->steps_done, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec};
+                    s->sat_step, s->steps_done, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec, s->wv_tp4, s->wv_vst};
     for (void *p : ptrs) dfree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
@@ -915,7 +976,17 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     // for FUSED (measured on MI355X, config 2: W = 64 beats 32 / 16 by 1.5-1.7x).
     // ODESAT_GROUP_WIDTH overrides (tuning; RESIDENT only if that width admits it).
     int lw = 1, res_r = 0;
-    if (res_fits(n, 1, s->tsize, false)) {  // measured (config 2, B = 1024): R = 1 beats R = 2 by 1.13x
+    // k_wave (wave.hpp) for small 3-SAT instances whose replica -- with the adaptive clones --
+    // fits in 64 KiB of LDS (two or more waves per CU); ODESAT_WAVE=0/1 overrides, an explicit
+    // ODESAT_GROUP_WIDTH selects the tile kernels
+    if (s->uniform_k == 3 && m > 0 && !std::getenv("ODESAT_GROUP_WIDTH")) {
+        const char *ev = std::getenv("ODESAT_WAVE");
+        const size_t wl = wave_lds_bytes(n, m, L, s->tsize, true);
+        s->res_wave = ev ? (std::atoi(ev) != 0 && wl <= RES_LDS_MAX) : wl <= 64 * 1024;
+    }
+    if (s->res_wave) {
+        res_r = lw = 1;
+    } else if (res_fits(n, 1, s->tsize, false)) {  // measured (config 2, B = 1024): R = 1 beats R = 2 by 1.13x
         res_r = lw = small_instance_width(f, n, batch, device, s->tsize);
     } else {
         while (lw < batch && lw < 64) lw <<= 1;
@@ -927,10 +998,28 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             res_r = (want <= 32 && res_fits(n, want, s->tsize, false)) ? want : 0;
         }
     }
+    // One replica per wave (RES_NARROW) when the tile chain is deep and narrow: 64-clause tiles
+    // then need barely more tiles than 512-clause ones, and a replica's step costs one wave instead
+    // of eight (hard.cnf at B = 1: a step is a chain of ~20 tiles of ~8 clauses).
+    // ODESAT_RES_NARROW=0/1 overrides.
+    if (res_r == 1 && m > 0 && !s->res_wave) {
+        const char *ev = std::getenv("ODESAT_RES_NARROW");
+        if (ev) s->res_narrow = std::atoi(ev) != 0;
+        else s->res_narrow = 4 * tile_count(f, n, RES_NARROW) <= 5 * tile_count(f, n, ResShape<1>::NL);
+    }
     // the internal clause order: var-disjoint tiles for RESIDENT, else the file order
     std::vector<int32_t> perm, tiles;
     std::vector<uint8_t> lorder;  // per internal clause: literal order code (kP3), 0 = file order
-    if (res_r > 0 && !build_tiles(f, n, res_capacity(res_r), res_r, s->uniform_k == 3, perm, tiles, lorder)) res_r = 0;
+    const int cap = s->res_narrow ? RES_NARROW : res_capacity(res_r);
+    if (s->res_wave) {  // no tiles: the file order, one pseudo-tile
+        perm.resize(m);
+        for (int64_t c = 0; c < m; ++c) perm[c] = (int32_t)c;
+        tiles = {0, (int32_t)m};
+        lorder.assign(m, 0);
+    } else if (res_r > 0 && !build_tiles(f, n, cap, res_r, s->uniform_k == 3, perm, tiles, lorder)) {
+        res_r = 0;
+    }
+    if (res_r != 1) s->res_narrow = false;
     if (res_r == 0 && !std::getenv("ODESAT_GROUP_WIDTH")) {
         lw = 1;
         while (lw < batch && lw < 64) lw <<= 1;
@@ -1035,6 +1124,26 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         s->res_ada = res_fits(n, res_r, s->tsize, true);
         s->res_ntiles = (int)tiles.size() - 1;
         s->alg = ODESAT_ALG_RESIDENT;
+        if (s->res_wave) {  // k_wave: variable-major term positions, incidences sorted by (clause, literal)
+            std::vector<int32_t> vst((size_t)n + 1, 0), fillc((size_t)n, 0);
+            for (int64_t k = 0; k < L; ++k) vst[(lits[k] >> 1) + 1] += 1;
+            for (int64_t i = 0; i < n; ++i) vst[i + 1] += vst[i];
+            std::vector<int4> tp4((size_t)m);
+            for (int64_t c = 0; c < m; ++c) {
+                int q[3];
+                for (int j = 0; j < 3; ++j) {
+                    const int32_t v = lits[3 * c + j] >> 1;
+                    q[j] = vst[v] + fillc[v]++;
+                }
+                tp4[c] = make_int4(q[0], q[1], q[2], 0);
+            }
+            if ((rc = dmalloc(s, (void **)&s->wv_tp4, (size_t)m * 16)) || (rc = dmalloc(s, (void **)&s->wv_vst, (n + 1) * 4)))
+                return bail(rc);
+            if (hipMemcpy(s->wv_tp4, tp4.data(), (size_t)m * 16, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(s->wv_vst, vst.data(), (n + 1) * 4, hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
+            s->res_ada = true;  // wave_lds_bytes(adaptive) fits by selection
+        }
         if ((rc = onchip_setup(s, tiles, lits))) return bail(rc);
         if (s->oc_tr > 0) s->alg = ODESAT_ALG_ONCHIP;
     }

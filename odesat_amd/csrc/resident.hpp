@@ -276,11 +276,14 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
     if (!K3 && NT_ == 0) __syncthreads();
 }
 
-template <typename T, int R, bool ADAPTIVE, bool K3>
-__global__ __launch_bounds__(ResShape<R>::NTH) void k_resident(RArgs<T> a) {
+// NTHR threads per workgroup: ResShape<R>::NTH, or one wave (RES_NARROW) for instances whose tile
+// chains are deep and narrow (a few dozen clauses per tile): one replica per wave, no idle waves.
+constexpr int RES_NARROW = 64;
+template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR>
+__global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char res_smem[];
     using U = typename Bits<T>::U;
-    constexpr int NTH = ResShape<R>::NTH, NL = ResShape<R>::NL;
+    constexpr int NTH = NTHR, NL = NTHR / R;
     __shared__ uint32_t unsL[R];
     __shared__ U errL[R];
     __shared__ T dtL[R];

@@ -1,0 +1,193 @@
+// wave.hpp -- ALG_RESIDENT for small 3-SAT instances: one wave per replica, the dv fold variable by
+// variable instead of clause tile by clause tile (included by odesat_hip.hip).
+//
+// The tile kernels fold every dv[i] in the reference's order by running var-disjoint clause tiles
+// one after another, so a step costs the depth of the clause-order chains -- 34 tiles of ~5 clauses
+// for tests/hard.cnf, 30 of ~35 for config 3 -- whatever the instance's size.  On a small instance
+// the whole replica fits in one wave's share of LDS, and the step splits into two phases with no
+// order between clauses at all:
+//   1. every clause (lane l takes clauses l, l + 64, ...) computes C, its memory update and its
+//      three dv terms (system.rs:43-88), and stores each term at its variable-major position:
+//      the incidences of variable i, sorted by (clause, literal), occupy [vstart[i], vstart[i+1]);
+//   2. every variable (lane l takes l, l + 64, ...) folds its terms in that order from +0 -- the
+//      reference's dv[i] += ... sequence exactly (:33, :80) -- and applies :96.
+// A single wave needs no barrier between the phases (its LDS operations complete in order; the
+// __syncthreads below are a compiler ordering fence costing nothing for one wave).  The state
+// (v, the clause memories, the adaptive clones) stays in LDS for the whole launch; per step the
+// only memory reads are the L2-resident literal and position records.
+// Arithmetic: the tile kernel's (res_clause3 / res_mem_update) expression for expression, so every
+// result is bit-identical to it and to the oracle.
+#pragma once
+
+#include "kernels.hpp"
+
+namespace odk {
+
+constexpr int WAVE_NTH = 64;
+
+template <typename T> struct WArgs {
+    const int4 *__restrict__ cl4;     // [m] the clause's literals (var << 1 | neg), file order
+    const int4 *__restrict__ tp4;     // [m] variable-major position of each literal's term
+    const int32_t *__restrict__ vst;  // [n+1] variable -> first term position
+    T *v0, *v1, *c0, *c1;             // state buffers, group width 1
+    const uint8_t *par;
+    T *dtr;
+    uint8_t *act;
+    int64_t *sat_step, *steps_done;
+    int32_t *stop;
+    int32_t n, m, L;
+    int32_t step0, nsteps, stop_mode;
+    T dt, zeta, xl_max;
+    double tol;
+};
+
+// LDS bytes of one replica: v, its full-step clone (adaptive), the terms, the memories and their
+// full-step and first-half clones (adaptive)
+inline size_t wave_lds_bytes(int64_t n, int64_t m, int64_t L, size_t tsize, bool adaptive) {
+    return ((adaptive ? 2 : 1) * (size_t)n + (size_t)L + (adaptive ? 6 : 2) * (size_t)m) * tsize;
+}
+
+enum WPass : int { W_FIXED = 0, W_ADA1 = 1, W_ADA2 = 2 };
+
+// Phase 1 over the replica's clauses.  Returns (wave-uniform) whether some clause is unsat (:88,
+// W_FIXED / W_ADA1) and raises e to the memories' max_error terms (W_ADA2).
+template <typename T, int PK>
+__device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const T *vL, T *tL, T *cmL, T *cfL, T *chL, T h,
+                                             T &e) {
+    const T one = (T)1.0, halfc = (T)0.5, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
+    bool uns = false;
+    for (int c = threadIdx.x; c < a.m; c += WAVE_NTH) {
+        const int4 l4 = a.cl4[c], p4 = a.tp4[c];
+        const int lit[3] = {l4.x, l4.y, l4.z}, pos[3] = {p4.x, p4.y, p4.z};
+        T v[3], q[3], val[3], d[3];
+        T mn = inf_v<T>(), sec = inf_v<T>();
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {  // :43-57
+            q[j] = (lit[j] & 1) ? (T)-1.0 : (T)1.0;
+            v[j] = vL[lit[j] >> 1];
+            val[j] = one - q[j] * v[j];
+            minsec(val[j], mn, sec);
+        }
+        const T C = halfc * mn;  // :60
+        const T *mem = (PK == W_ADA2 ? chL : cmL) + 2 * c;
+        const T xs_m = mem[0], xl_m = mem[1];
+        const T tt = xl_m * xs_m;
+        const T tr = (one + a.zeta * xl_m) * (one - xs_m);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) d[j] = tt * (halfc * q[j] * (val[j] != mn ? mn : sec));  // :64-70
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {  // :73-80 (zero unless C == val_j; adding it keeps the sum exact)
+            const T r_ = (C == one - q[j] * v[j]) ? halfc * (q[j] - v[j]) : (T)0.0;
+            d[j] = d[j] + tr * r_;
+            tL[pos[j]] = d[j];
+        }
+        if (PK != W_ADA2) uns = uns || !(C < (T)0.25);  // :88
+        const T dxs = (T)20.0 * (xs_m + eps) * (C - (T)0.25);  // :84
+        const T dxl = (T)5.0 * (C - (T)0.05);                  // :85
+        if (PK == W_FIXED) {
+            cmL[2 * c] = dmin(dmax(xs_m + h * dxs, eps), xs_hi);  // :94-95
+            cmL[2 * c + 1] = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
+        } else if (PK == W_ADA1) {
+            const T half = (T)0.5 * h;
+            cfL[2 * c] = dmin(dmax(xs_m + h * dxs, eps), xs_hi);  // full-step clone (:124-125)
+            cfL[2 * c + 1] = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
+            chL[2 * c] = dmin(dmax(xs_m + half * dxs, eps), xs_hi);  // first half step (:128)
+            chL[2 * c + 1] = dmin(dmax(xl_m + half * dxl, one), a.xl_max);
+        } else {
+            const T half = (T)0.5 * h;  // second half step (:130), max_error terms (:132)
+            const T xs_n = dmin(dmax(xs_m + half * dxs, eps), xs_hi);
+            const T xl_n = dmin(dmax(xl_m + half * dxl, one), a.xl_max);
+            e = dmax(e, dmax(dabs(cfL[2 * c] - xs_n), dabs(cfL[2 * c + 1] - xl_n)));
+            cmL[2 * c] = xs_n;
+            cmL[2 * c + 1] = xl_n;
+        }
+    }
+    return __any(uns);
+}
+
+// Phase 2 for variable i: dv[i] as the reference's left fold of its terms (:33, :80).
+template <typename T> __device__ __forceinline__ T wave_fold(const WArgs<T> &a, const T *tL, int i) {
+    T dv = (T)0.0;
+    for (int k = a.vst[i]; k < a.vst[i + 1]; ++k) dv += tL[k];
+    return dv;
+}
+
+template <typename T, bool ADAPTIVE>
+__global__ __launch_bounds__(WAVE_NTH) void k_wave(WArgs<T> a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char wave_smem[];
+    using U = typename Bits<T>::U;
+    __shared__ U errL;
+    const int g = blockIdx.x, l = threadIdx.x;
+    int act = a.act[g];
+    if (!act) return;  // uniform
+    if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
+    int64_t sat = a.sat_step[g], done = a.steps_done[g];
+    T dtr = ADAPTIVE ? a.dtr[g] : a.dt;
+    T *vL = reinterpret_cast<T *>(wave_smem);
+    T *vfL = vL + (ADAPTIVE ? a.n : 0);
+    T *tL = vfL + a.n;
+    T *cmL = tL + a.L;
+    T *cfL = cmL + 2 * a.m;
+    T *chL = cfL + 2 * a.m;
+    const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
+    T *V = (p ? a.v1 : a.v0) + (size_t)g * a.n;
+    T *CM = (p ? a.c1 : a.c0) + (size_t)g * a.m * 2;
+    for (int i = l; i < a.n; i += WAVE_NTH) vL[i] = V[i];
+    for (int i = l; i < 2 * a.m; i += WAVE_NTH) cmL[i] = CM[i];
+    __syncthreads();
+    for (int k = 0; k < a.nsteps; ++k) {
+        const int step = a.step0 + k;
+        const T h = dtr;
+        T e = (T)0.0;
+        bool uns;
+        if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
+            uns = wave_clauses<T, W_FIXED>(a, vL, tL, cmL, cfL, chL, h, e);
+            __syncthreads();
+            for (int i = l; i < a.n; i += WAVE_NTH) vL[i] = dmin(dmax(vL[i] + h * wave_fold(a, tL, i), (T)-1.0), (T)1.0);
+            __syncthreads();
+        } else {  // euler_step (:111-139)
+            uns = wave_clauses<T, W_ADA1>(a, vL, tL, cmL, cfL, chL, h, e);
+            __syncthreads();
+            if (uns) {  // an allsat replica takes no step (:122)
+                const T half = (T)0.5 * h;
+                for (int i = l; i < a.n; i += WAVE_NTH) {
+                    const T d = wave_fold(a, tL, i), v = vL[i];
+                    vfL[i] = dmin(dmax(v + h * d, (T)-1.0), (T)1.0);    // full-step clone
+                    vL[i] = dmin(dmax(v + half * d, (T)-1.0), (T)1.0);  // first half step
+                }
+                __syncthreads();
+                wave_clauses<T, W_ADA2>(a, vL, tL, cmL, cfL, chL, h, e);
+                __syncthreads();
+                for (int i = l; i < a.n; i += WAVE_NTH) {
+                    const T vn = dmin(dmax(vL[i] + half * wave_fold(a, tL, i), (T)-1.0), (T)1.0);  // second half
+                    e = dmax(e, dabs(vfL[i] - vn));  // :101-108
+                    vL[i] = vn;
+                }
+                if (l == 0) errL = 0;
+                __syncthreads();
+                atomicMax(&errL, tobits(e));
+                __syncthreads();
+                const T error = frombits(errL);  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
+                dtr = dmax(dmin(dtr * dsqrt((T)a.tol / error), (T)1e3), (T)0.0078125);
+            }
+        }
+        done += 1;
+        if (!uns) {  // allsat: the fixed step was still taken (:148-152); adaptive took none
+            if (sat < 0) sat = step;
+            if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                            // simulate() breaks (:193)
+            if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
+        }
+        if (!act) break;  // uniform
+    }
+    __syncthreads();
+    for (int i = l; i < a.n; i += WAVE_NTH) V[i] = vL[i];
+    for (int i = l; i < 2 * a.m; i += WAVE_NTH) CM[i] = cmL[i];
+    if (l == 0) {
+        a.act[g] = (uint8_t)act;
+        a.sat_step[g] = sat;
+        a.steps_done[g] = done;
+        if (ADAPTIVE) a.dtr[g] = dtr;
+    }
+}
+
+}  // namespace odk

@@ -370,19 +370,26 @@ def test_algorithms_identical(name, prec, B):
     f = product_formula(name)
     with Solver(f, B, prec) as s:
         default = s.algorithm
-    # these formulas fit in LDS; f32 3-SAT ones fit on chip (ONCHIP, fixed steps; adaptive -> RESIDENT)
-    assert default == (_lib.ODESAT_ALG_ONCHIP if prec == "f32" and name == "rand200" else _lib.ODESAT_ALG_RESIDENT)
-    algs = [_lib.ODESAT_ALG_RESIDENT, _lib.ODESAT_ALG_FUSED, _lib.ODESAT_ALG_TWOPASS]
-    if default == _lib.ODESAT_ALG_ONCHIP:
-        algs.append(_lib.ODESAT_ALG_ONCHIP)
+    # these formulas are small: RESIDENT as k_wave (one wave per replica, variable fold)
+    assert default == _lib.ODESAT_ALG_RESIDENT
+    # k_wave, the tile kernels (ODESAT_WAVE=0: RESIDENT, and ONCHIP for f32 3-SAT), FUSED, TWOPASS
+    algs = [(_lib.ODESAT_ALG_RESIDENT, "1"), (_lib.ODESAT_ALG_RESIDENT, "0"), (_lib.ODESAT_ALG_FUSED, "1"),
+            (_lib.ODESAT_ALG_TWOPASS, "1")]
+    if prec == "f32" and name == "rand200":
+        algs.append((_lib.ODESAT_ALG_ONCHIP, "0"))
+    import os
     for adaptive in (False, True):
         out = []
-        for alg in algs:
+        for alg, wave in algs:
+            os.environ["ODESAT_WAVE"] = wave
+            os.environ["ODESAT_RES_NARROW"] = "0" if alg == _lib.ODESAT_ALG_ONCHIP else "1"  # ONCHIP: 512-lane tiles
             with Solver(f, B, prec) as s:
                 s.set_algorithm(alg)
                 s.init_state(21)
                 r = s.simulate(adaptive=adaptive, dt=0.05, max_steps=80, stop=ODESAT_STOP_EACH, poll_interval=3)
                 out.append((r["first_sat_step"], r["steps_done"], r["dt"], s.get_state()))
+        os.environ.pop("ODESAT_WAVE", None)
+        os.environ.pop("ODESAT_RES_NARROW", None)
         for o in out[1:]:
             assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1])
             assert same(out[0][2], o[2])
@@ -420,8 +427,8 @@ def test_resident_widths_match_fused_w64(monkeypatch, name, prec, width, mode):
     B = 37
     a1, w1, r1, s1 = _run_layout(monkeypatch, f, B, prec, width, **kw)
     a2, w2, r2, s2 = _run_layout(monkeypatch, f, B, prec, 64, **kw)
-    onchip = width == 1 and prec == "f32" and name != "small"  # f32 3-SAT at R = 1: ONCHIP by default
-    assert (a1, w1) == (_lib.ODESAT_ALG_ONCHIP if onchip else _lib.ODESAT_ALG_RESIDENT, width)
+    # f32 3-SAT at R = 1: ONCHIP, unless the tile chain is narrow enough for one-wave tiles
+    assert w1 == width and a1 in (_lib.ODESAT_ALG_RESIDENT, _lib.ODESAT_ALG_ONCHIP)
     assert (a2, w2) == (_lib.ODESAT_ALG_FUSED, 64)
     assert np.array_equal(r1["first_sat_step"], r2["first_sat_step"])
     assert np.array_equal(r1["steps_done"], r2["steps_done"]) and r1["steps_run"] == r2["steps_run"]
@@ -431,16 +438,19 @@ def test_resident_widths_match_fused_w64(monkeypatch, name, prec, width, mode):
 
 
 def test_small_instance_width_config3():
-    """Config 3 (n = 250): tiles ~35 clauses deep-chained, so the solver packs R replicas per
-    workgroup (the largest R that still gives every CU a workgroup): B = 1024 -> R = 4, B = 4096 ->
-    R = 16; the trajectories equal FUSED's bit for bit on a replica subset."""
+    """Config 3 (n = 250): by default k_wave (one replica per wave); with the tile kernel the solver
+    packs R replicas per workgroup (the largest R that still gives every CU a workgroup): B = 1024
+    -> R = 4, B = 4096 -> R = 16.  Every trajectory equals FUSED's bit for bit on a replica subset."""
     from odesat_amd import _lib
     c = wl.CONFIGS["config3"]
     var, neg = wl.random_ksat(c["n"], c["m"], 3, c["seed"])
     cp, v_, n_ = wl.formula_arrays(var, neg)
     f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
-    for B, R in ((1024, 4), (4096, 16)):
+    import os
+    for B, R, wave in ((1024, 1, "1"), (1024, 4, "0"), (4096, 16, "0")):
+        os.environ["ODESAT_WAVE"] = wave  # 1: k_wave (one replica per wave); 0: the tile kernel at width R
         with Solver(f, B, "f32") as s:
+            os.environ.pop("ODESAT_WAVE")
             assert (s.algorithm, s.group_width) == (_lib.ODESAT_ALG_RESIDENT, R)
             s.init_state(42)
             r1 = s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=40, stop=ODESAT_STOP_EACH, poll_interval=8)
@@ -518,19 +528,22 @@ def test_onchip_lds_tiles_match_resident_and_oracle(stop):
     assert same(v[0], ov) and same(xs[0], oxs) and same(xl[0], oxl)
 
 
-def test_onchip_long_launches_sat_and_freeze():
+def test_onchip_long_launches_sat_and_freeze(monkeypatch):
     """STOP_EACH over launches of many steps: replicas that satisfy easy.cnf freeze at their own
-    step inside a launch (ONCHIP == FUSED, states and sat steps)."""
+    step inside a launch (ONCHIP == k_wave == FUSED, states and sat steps)."""
     from odesat_amd import _lib
     f = product_formula("easy")
     out = []
-    for alg in (_lib.ODESAT_ALG_ONCHIP, _lib.ODESAT_ALG_FUSED):
+    for alg, wave in ((_lib.ODESAT_ALG_ONCHIP, "0"), (_lib.ODESAT_ALG_RESIDENT, "1"), (_lib.ODESAT_ALG_FUSED, "1")):
+        monkeypatch.setenv("ODESAT_WAVE", wave)
+        monkeypatch.setenv("ODESAT_RES_NARROW", "0")
         with Solver(f, 40, "f32") as s:
             s.set_algorithm(alg)
             s.init_state(4)
             r = s.simulate(dt=0.1, max_steps=3000, stop=ODESAT_STOP_EACH, poll_interval=500)
             out.append((r["first_sat_step"], r["steps_done"], s.get_state()))
     assert (out[0][0] >= 0).any()
-    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
-    for x, y in zip(out[0][2], out[1][2]):
-        assert same(x, y)
+    for o in out[1:]:
+        assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1])
+        for x, y in zip(out[0][2], o[2]):
+            assert same(x, y)
