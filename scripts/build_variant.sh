@@ -1,12 +1,17 @@
 #!/bin/bash
-# Build an experimental variant of libodesat_hip.so with extra flags for onchip.hip:
-#   scripts/build_variant.sh NAME "-DONCHIP_ORDER=1"   ->  expt/libNAME.so
-# Run it with ODESAT_LIB=$PWD/expt/libNAME.so (scripts/expt.sh).  The product build is untouched.
+# Build an experimental variant of libodesat_hip.so: SRC (default onchip) is recompiled with extra
+# flags from the working tree, every other object comes from the product build (make first):
+#   scripts/build_variant.sh NAME "-DFLAG" [SRC]   ->  expt/libNAME.so
+# Run it with ODESAT_LIB=$PWD/expt/libNAME.so (scripts/expt.sh, scripts/expt_small.sh).
 set -eu
 cd "$(dirname "$0")/.."
-name=$1; flags=$2
+name=$1; flags=$2; src=${3:-onchip}
 mkdir -p build/vobj/$name expt
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -Wall -Wno-unused-function"
-$H -fno-slp-vectorize $flags -c -o build/vobj/$name/onchip.o odesat_amd/csrc/onchip.hip
-$H --offload-arch=gfx950 -shared -fPIC -o expt/lib$name.so build/vobj/$name/onchip.o build/obj/odesat_hip.o \
-   build/obj/partition.o build/obj/cnf.o build/obj/preprocess.o build/obj/stoch.o
+extra=""; [ "$src" = onchip ] && extra="-fno-slp-vectorize"
+$H $extra $flags -c -o build/vobj/$name/$src.o odesat_amd/csrc/$src.hip
+objs=""
+for o in odesat_hip onchip partition cnf preprocess stoch run_abi; do
+  if [ "$o" = "$src" ]; then objs="$objs build/vobj/$name/$o.o"; else objs="$objs build/obj/$o.o"; fi
+done
+$H -shared -fPIC -o expt/lib$name.so $objs
