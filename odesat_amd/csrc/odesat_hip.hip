@@ -64,6 +64,7 @@ struct odesat_solver {
     bool res_wave = false;    // RESIDENT as k_wave (wave.hpp): small 3-SAT, one wave per replica, variable fold
     int4 *wv_tp4 = nullptr;   // [m] k_wave: variable-major term position of each literal
     int32_t *wv_vst = nullptr;  // [n+1] k_wave: first term position of each variable
+    int wv_wpw = 1;             // k_wave: replicas (waves) per workgroup sharing the LDS topology
     bool res_ada = false; // adaptive steps fit in LDS too (else they run FUSED on the same layout)
     int res_ntiles = 0;
     int32_t *res_tc = nullptr, *cmap = nullptr;
@@ -600,17 +601,20 @@ int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     return ODESAT_OK;
 }
 
-template <typename T, bool ADA> int launch_wave_k(odesat_solver *s, const WArgs<T> &a) {
+template <typename T, bool ADA, int WPW> int launch_wave_k(odesat_solver *s, WArgs<T> a) {
     static bool attr_set = false;  // per instantiation
-    const size_t lds = wave_lds_bytes(s->n, s->m, s->L, sizeof(T), ADA);
+    a.topo_bytes = (uint32_t)wave_topo_bytes(s->n, s->m);
+    a.rep_bytes = (uint32_t)wave_lds_bytes(s->n, s->m, s->L, sizeof(T), ADA);
+    const size_t lds = a.topo_bytes + (size_t)WPW * a.rep_bytes;
     if (!attr_set) {
-        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wave<T, ADA>),
+        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wave<T, ADA, WPW>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)RES_LDS_MAX));
         attr_set = true;
     }
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_wave<T, ADA>), dim3(s->G), dim3(WAVE_NTH), lds, s->stream, a);
+        hipLaunchKernelGGL((k_wave<T, ADA, WPW>), dim3((unsigned)((s->G + WPW - 1) / WPW)), dim3(WAVE_NTH * WPW), lds,
+                           s->stream, a);
     }
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
@@ -643,7 +647,16 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     a.zeta = (T)zeta;
     a.xl_max = (T)1e4 * (T)s->m;  // system.rs:95
     a.tol = tol;
-    return adaptive ? launch_wave_k<T, true>(s, a) : launch_wave_k<T, false>(s, a);
+    a.G = s->G;
+    auto go = [&](auto ww) -> int {
+        constexpr int WPW = decltype(ww)::value;
+        return adaptive ? launch_wave_k<T, true, WPW>(s, a) : launch_wave_k<T, false, WPW>(s, a);
+    };
+    switch (s->wv_wpw) {
+        case 4: return go(IC<4>{});
+        case 2: return go(IC<2>{});
+        default: return go(IC<1>{});
+    }
 }
 
 template <typename T>
@@ -979,10 +992,11 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     // k_wave (wave.hpp) for small 3-SAT instances whose replica -- with the adaptive clones --
     // fits in 64 KiB of LDS (two or more waves per CU); ODESAT_WAVE=0/1 overrides, an explicit
     // ODESAT_GROUP_WIDTH selects the tile kernels
-    if (s->uniform_k == 3 && m > 0 && !std::getenv("ODESAT_GROUP_WIDTH")) {
+    if (s->uniform_k == 3 && m > 0 && !std::getenv("ODESAT_GROUP_WIDTH") && m < (1 << 26) && L < (1 << 26)) {
         const char *ev = std::getenv("ODESAT_WAVE");
-        const size_t wl = wave_lds_bytes(n, m, L, s->tsize, true);
-        s->res_wave = ev ? (std::atoi(ev) != 0 && wl <= RES_LDS_MAX) : wl <= 64 * 1024;
+        const size_t topo = wave_topo_bytes(n, m), rep = wave_lds_bytes(n, m, L, s->tsize, true);
+        s->wv_wpw = topo + 4 * rep <= RES_LDS_MAX ? 4 : (topo + 2 * rep <= RES_LDS_MAX ? 2 : 1);
+        s->res_wave = ev ? (std::atoi(ev) != 0 && topo + rep <= RES_LDS_MAX) : topo + 2 * rep <= RES_LDS_MAX;
     }
     if (s->res_wave) {
         res_r = lw = 1;

@@ -11,10 +11,11 @@
 //      the incidences of variable i, sorted by (clause, literal), occupy [vstart[i], vstart[i+1]);
 //   2. every variable (lane l takes l, l + 64, ...) folds its terms in that order from +0 -- the
 //      reference's dv[i] += ... sequence exactly (:33, :80) -- and applies :96.
-// A single wave needs no barrier between the phases (its LDS operations complete in order; the
-// __syncthreads below are a compiler ordering fence costing nothing for one wave).  The state
-// (v, the clause memories, the adaptive clones) stays in LDS for the whole launch; per step the
-// only memory reads are the L2-resident literal and position records.
+// A single wave needs no barrier between the phases: its LDS operations complete in issue order,
+// and wave_sync only keeps the compiler from moving LDS accesses across them.  The state (v, the
+// clause memories, the adaptive clone of v and the first pass's C) stays in LDS for a launch, and
+// the topology (literal and position records, variable starts) is copied into LDS once per launch
+// and shared by the workgroup's WPW waves, so a step reads nothing from the memory hierarchy.
 // Arithmetic: the tile kernel's (res_clause3 / res_mem_update) expression for expression, so every
 // result is bit-identical to it and to the oracle.
 #pragma once
@@ -35,29 +36,34 @@ template <typename T> struct WArgs {
     uint8_t *act;
     int64_t *sat_step, *steps_done;
     int32_t *stop;
-    int32_t n, m, L;
+    int32_t n, m, L, G;                 // G: replicas (groups of width 1)
+    uint32_t topo_bytes, rep_bytes;     // LDS: the shared topology, then WPW replicas of rep_bytes
     int32_t step0, nsteps, stop_mode;
     T dt, zeta, xl_max;
     double tol;
 };
 
-// LDS bytes of one replica: v, its full-step clone (adaptive), the terms, the memories and their
-// full-step and first-half clones (adaptive)
+// LDS bytes of one replica: v, its full-step clone (adaptive), the terms, the memories and (adaptive)
+// each clause's C of the first pass, from which the second pass recomputes the full-step and
+// first-half memories with the first pass's expressions -- bit-identical, and 16 bytes per clause
+// less than storing them
 inline size_t wave_lds_bytes(int64_t n, int64_t m, int64_t L, size_t tsize, bool adaptive) {
-    return ((adaptive ? 2 : 1) * (size_t)n + (size_t)L + (adaptive ? 6 : 2) * (size_t)m) * tsize;
+    return (((adaptive ? 2 : 1) * (size_t)n + (size_t)L + (adaptive ? 3 : 2) * (size_t)m) * tsize + 15) / 16 * 16;
 }
+// the topology every wave of a workgroup reads: literal and position records, variable starts
+inline size_t wave_topo_bytes(int64_t n, int64_t m) { return ((size_t)m * 32 + (size_t)(n + 1) * 4 + 15) / 16 * 16; }
 
 enum WPass : int { W_FIXED = 0, W_ADA1 = 1, W_ADA2 = 2 };
 
 // Phase 1 over the replica's clauses.  Returns (wave-uniform) whether some clause is unsat (:88,
 // W_FIXED / W_ADA1) and raises e to the memories' max_error terms (W_ADA2).
 template <typename T, int PK>
-__device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const T *vL, T *tL, T *cmL, T *cfL, T *chL, T h,
-                                             T &e) {
+__device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *cl4, const int4 *tp4, const T *vL, T *tL,
+                                             T *cmL, T *cL, int l, T h, T &e) {
     const T one = (T)1.0, halfc = (T)0.5, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
     bool uns = false;
-    for (int c = threadIdx.x; c < a.m; c += WAVE_NTH) {
-        const int4 l4 = a.cl4[c], p4 = a.tp4[c];
+    for (int c = l; c < a.m; c += WAVE_NTH) {
+        const int4 l4 = cl4[c], p4 = tp4[c];
         const int lit[3] = {l4.x, l4.y, l4.z}, pos[3] = {p4.x, p4.y, p4.z};
         T v[3], q[3], val[3], d[3];
         T mn = inf_v<T>(), sec = inf_v<T>();
@@ -69,8 +75,19 @@ __device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const T *vL, T *
             minsec(val[j], mn, sec);
         }
         const T C = halfc * mn;  // :60
-        const T *mem = (PK == W_ADA2 ? chL : cmL) + 2 * c;
-        const T xs_m = mem[0], xl_m = mem[1];
+        T xs_m = cmL[2 * c], xl_m = cmL[2 * c + 1];
+        T xs_f = xs_m, xl_f = xl_m;
+        if (PK == W_ADA2) {  // y's memories -> the full-step clone and the first half step (:124-128)
+            const T C1 = cL[c], half = (T)0.5 * h;
+            const T dxs1 = (T)20.0 * (xs_m + eps) * (C1 - (T)0.25);  // :84
+            const T dxl1 = (T)5.0 * (C1 - (T)0.05);                  // :85
+            xs_f = dmin(dmax(xs_m + h * dxs1, eps), xs_hi);
+            xl_f = dmin(dmax(xl_m + h * dxl1, one), a.xl_max);
+            const T xs_h = dmin(dmax(xs_m + half * dxs1, eps), xs_hi);
+            const T xl_h = dmin(dmax(xl_m + half * dxl1, one), a.xl_max);
+            xs_m = xs_h;
+            xl_m = xl_h;
+        }
         const T tt = xl_m * xs_m;
         const T tr = (one + a.zeta * xl_m) * (one - xs_m);
 #pragma unroll
@@ -88,16 +105,12 @@ __device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const T *vL, T *
             cmL[2 * c] = dmin(dmax(xs_m + h * dxs, eps), xs_hi);  // :94-95
             cmL[2 * c + 1] = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
         } else if (PK == W_ADA1) {
-            const T half = (T)0.5 * h;
-            cfL[2 * c] = dmin(dmax(xs_m + h * dxs, eps), xs_hi);  // full-step clone (:124-125)
-            cfL[2 * c + 1] = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
-            chL[2 * c] = dmin(dmax(xs_m + half * dxs, eps), xs_hi);  // first half step (:128)
-            chL[2 * c + 1] = dmin(dmax(xl_m + half * dxl, one), a.xl_max);
+            cL[c] = C;  // the memories stay y until the second pass (an allsat replica takes no step)
         } else {
             const T half = (T)0.5 * h;  // second half step (:130), max_error terms (:132)
             const T xs_n = dmin(dmax(xs_m + half * dxs, eps), xs_hi);
             const T xl_n = dmin(dmax(xl_m + half * dxl, one), a.xl_max);
-            e = dmax(e, dmax(dabs(cfL[2 * c] - xs_n), dabs(cfL[2 * c + 1] - xl_n)));
+            e = dmax(e, dmax(dabs(xs_f - xs_n), dabs(xl_f - xl_n)));
             cmL[2 * c] = xs_n;
             cmL[2 * c + 1] = xl_n;
         }
@@ -105,69 +118,97 @@ __device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const T *vL, T *
     return __any(uns);
 }
 
-// Phase 2 for variable i: dv[i] as the reference's left fold of its terms (:33, :80).
-template <typename T> __device__ __forceinline__ T wave_fold(const WArgs<T> &a, const T *tL, int i) {
+// Phase 2 for variable i: dv[i] as the reference's left fold of its terms (:33, :80).  The term
+// reads go out four at a time; the adds stay in order.
+template <typename T> __device__ __forceinline__ T wave_fold(const int32_t *vst, const T *tL, int i) {
     T dv = (T)0.0;
-    for (int k = a.vst[i]; k < a.vst[i + 1]; ++k) dv += tL[k];
+    const int k1 = vst[i + 1];
+    for (int k = vst[i]; k < k1; k += 4) {
+        T t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t[u] = tL[min(k + u, k1 - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k + u < k1) dv += t[u];
+    }
     return dv;
 }
 
-template <typename T, bool ADAPTIVE>
-__global__ __launch_bounds__(WAVE_NTH) void k_wave(WArgs<T> a) {
+// Orders one wave's LDS accesses across the phases: a wave's LDS operations complete in issue
+// order, so only the compiler must not move accesses across this point.
+__device__ __forceinline__ void wave_sync() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// WPW replicas (one per wave) per workgroup share one LDS copy of the topology.
+template <typename T, bool ADAPTIVE, int WPW>
+__global__ __launch_bounds__(WAVE_NTH * WPW) void k_wave(WArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char wave_smem[];
     using U = typename Bits<T>::U;
-    __shared__ U errL;
-    const int g = blockIdx.x, l = threadIdx.x;
+    __shared__ U errL[WPW];
+    const int w = threadIdx.x / WAVE_NTH, l = threadIdx.x % WAVE_NTH;
+    const int g = blockIdx.x * WPW + w;  // this wave's replica (group width 1)
+    int4 *cl4 = reinterpret_cast<int4 *>(wave_smem);
+    int4 *tp4 = cl4 + a.m;
+    int32_t *vst = reinterpret_cast<int32_t *>(tp4 + a.m);
+    for (int i = threadIdx.x; i < a.m; i += WAVE_NTH * WPW) {
+        cl4[i] = a.cl4[i];
+        tp4[i] = a.tp4[i];
+    }
+    for (int i = threadIdx.x; i <= a.n; i += WAVE_NTH * WPW) vst[i] = a.vst[i];
+    __syncthreads();  // the workgroup's only barrier: from here on every wave is on its own
+    if (g >= a.G) return;
     int act = a.act[g];
-    if (!act) return;  // uniform
+    if (!act) return;  // uniform per wave
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
     int64_t sat = a.sat_step[g], done = a.steps_done[g];
     T dtr = ADAPTIVE ? a.dtr[g] : a.dt;
-    T *vL = reinterpret_cast<T *>(wave_smem);
+    T *vL = reinterpret_cast<T *>(wave_smem + a.topo_bytes + (size_t)w * a.rep_bytes);
     T *vfL = vL + (ADAPTIVE ? a.n : 0);
     T *tL = vfL + a.n;
     T *cmL = tL + a.L;
-    T *cfL = cmL + 2 * a.m;
-    T *chL = cfL + 2 * a.m;
+    T *cL = cmL + 2 * a.m;
     const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
     T *V = (p ? a.v1 : a.v0) + (size_t)g * a.n;
     T *CM = (p ? a.c1 : a.c0) + (size_t)g * a.m * 2;
     for (int i = l; i < a.n; i += WAVE_NTH) vL[i] = V[i];
     for (int i = l; i < 2 * a.m; i += WAVE_NTH) cmL[i] = CM[i];
-    __syncthreads();
+    wave_sync();
     for (int k = 0; k < a.nsteps; ++k) {
         const int step = a.step0 + k;
         const T h = dtr;
         T e = (T)0.0;
         bool uns;
         if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
-            uns = wave_clauses<T, W_FIXED>(a, vL, tL, cmL, cfL, chL, h, e);
-            __syncthreads();
-            for (int i = l; i < a.n; i += WAVE_NTH) vL[i] = dmin(dmax(vL[i] + h * wave_fold(a, tL, i), (T)-1.0), (T)1.0);
-            __syncthreads();
+            uns = wave_clauses<T, W_FIXED>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
+            wave_sync();
+            for (int i = l; i < a.n; i += WAVE_NTH) vL[i] = dmin(dmax(vL[i] + h * wave_fold(vst, tL, i), (T)-1.0), (T)1.0);
+            wave_sync();
         } else {  // euler_step (:111-139)
-            uns = wave_clauses<T, W_ADA1>(a, vL, tL, cmL, cfL, chL, h, e);
-            __syncthreads();
+            uns = wave_clauses<T, W_ADA1>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
+            wave_sync();
             if (uns) {  // an allsat replica takes no step (:122)
                 const T half = (T)0.5 * h;
                 for (int i = l; i < a.n; i += WAVE_NTH) {
-                    const T d = wave_fold(a, tL, i), v = vL[i];
+                    const T d = wave_fold(vst, tL, i), v = vL[i];
                     vfL[i] = dmin(dmax(v + h * d, (T)-1.0), (T)1.0);    // full-step clone
                     vL[i] = dmin(dmax(v + half * d, (T)-1.0), (T)1.0);  // first half step
                 }
-                __syncthreads();
-                wave_clauses<T, W_ADA2>(a, vL, tL, cmL, cfL, chL, h, e);
-                __syncthreads();
+                wave_sync();
+                wave_clauses<T, W_ADA2>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
+                wave_sync();
                 for (int i = l; i < a.n; i += WAVE_NTH) {
-                    const T vn = dmin(dmax(vL[i] + half * wave_fold(a, tL, i), (T)-1.0), (T)1.0);  // second half
+                    const T vn = dmin(dmax(vL[i] + half * wave_fold(vst, tL, i), (T)-1.0), (T)1.0);  // second half
                     e = dmax(e, dabs(vfL[i] - vn));  // :101-108
                     vL[i] = vn;
                 }
-                if (l == 0) errL = 0;
-                __syncthreads();
-                atomicMax(&errL, tobits(e));
-                __syncthreads();
-                const T error = frombits(errL);  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
+                if (l == 0) errL[w] = 0;
+                wave_sync();
+                atomicMax(&errL[w], tobits(e));
+                wave_sync();
+                const T error = frombits(errL[w]);  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
                 dtr = dmax(dmin(dtr * dsqrt((T)a.tol / error), (T)1e3), (T)0.0078125);
             }
         }
@@ -177,9 +218,9 @@ __global__ __launch_bounds__(WAVE_NTH) void k_wave(WArgs<T> a) {
             if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                            // simulate() breaks (:193)
             if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
         }
-        if (!act) break;  // uniform
+        if (!act) break;  // uniform per wave
     }
-    __syncthreads();
+    wave_sync();
     for (int i = l; i < a.n; i += WAVE_NTH) V[i] = vL[i];
     for (int i = l; i < 2 * a.m; i += WAVE_NTH) CM[i] = cmL[i];
     if (l == 0) {
