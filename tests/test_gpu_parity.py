@@ -547,3 +547,31 @@ def test_onchip_long_launches_sat_and_freeze(monkeypatch):
         assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1])
         for x, y in zip(out[0][2], o[2]):
             assert same(x, y)
+
+
+@pytest.mark.parametrize("n,m,prec,wave_env,wpw", [(250, 1065, "f64", None, 2), (600, 2520, "f32", "1", 1)])
+def test_wave_workgroup_widths(monkeypatch, n, m, prec, wave_env, wpw):
+    """k_wave with 2 (config 3 in f64) and 1 (a larger instance, forced) replicas per workgroup
+    equals FUSED bit for bit, fixed and adaptive."""
+    from odesat_amd import _lib
+    var, neg = wl.random_ksat(n, m, 3, 7)
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    f = cnf.CNFFormula.from_arrays(cp, v_, n_, n)
+    if wave_env is not None:
+        monkeypatch.setenv("ODESAT_WAVE", wave_env)
+    topo = m * 32 + (n + 1) * 4
+    rep = ((2 * n + 3 * m + 3 * m) * (8 if prec == "f64" else 4) + 15) // 16 * 16
+    assert (topo + 4 * rep > 159 * 1024) and (wpw == 1) == (topo + 2 * rep > 159 * 1024)
+    for adaptive in (False, True):
+        out = []
+        for alg in (_lib.ODESAT_ALG_RESIDENT, _lib.ODESAT_ALG_FUSED):
+            with Solver(f, 9, prec) as s:
+                assert s.group_width == 1
+                s.set_algorithm(alg)
+                s.init_state(11)
+                r = s.simulate(adaptive=adaptive, dt=0.05, max_steps=40, stop=ODESAT_STOP_EACH, poll_interval=7)
+                out.append((r, s.get_state()))
+        assert np.array_equal(out[0][0]["first_sat_step"], out[1][0]["first_sat_step"])
+        assert np.array_equal(out[0][0]["steps_done"], out[1][0]["steps_done"]) and same(out[0][0]["dt"], out[1][0]["dt"])
+        for x, y in zip(out[0][1], out[1][1]):
+            assert same(x, y)
