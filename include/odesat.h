@@ -104,6 +104,9 @@ int odesat_stoch_get_state(odesat_stoch *s, int64_t r0, int64_t count, uint8_t *
  * poll_interval = steps between host checks of "all stopped" (0 = 64). */
 int odesat_stoch_search(odesat_stoch *s, uint64_t seed, int64_t replica0, int64_t max_steps, int stop,
                         int32_t poll_interval, int64_t *first_sat_step, int64_t *steps_done);
+/* the kernel search runs on: replicas per workgroup of the one-wave-per-replica kernel (formulas
+ * whose topology and one replica's state fit in LDS), or 0 for the three-kernel HBM path */
+int odesat_stoch_wave_width(const odesat_stoch *s);
 
 /* ------------------------------------------------------- preprocessing (cnf.rs:317-840) ----- */
 

@@ -62,6 +62,7 @@ SIGNATURES = {
     "odesat_stoch_create": (C.c_int, [C.c_int, _P, _i64, C.POINTER(_P)]),
     "odesat_stoch_destroy": (None, [_P]),
     "odesat_stoch_reset": (C.c_int, [_P, _i64, _i64]),
+    "odesat_stoch_wave_width": (C.c_int, [_P]),
     "odesat_stoch_set_state": (C.c_int, [_P, _i64, _i64, _u8p, C.POINTER(C.c_uint64)]),
     "odesat_stoch_get_state": (C.c_int, [_P, _i64, _i64, _u8p, C.POINTER(C.c_uint64)]),
     "odesat_stoch_search": (C.c_int, [_P, C.c_uint64, _i64, _i64, C.c_int, C.c_int32, _i64p, _i64p]),

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstdint>
 #include <new>
 #include <string>
@@ -50,6 +51,10 @@ struct odesat_stoch {
     uint8_t *act = nullptr;                    // [B] still searching
     int64_t *steps = nullptr;                  // [B] steps taken since the state was set (RNG step index)
     int64_t *sat_step = nullptr, *done = nullptr;  // [B] per call
+    int32_t *topo = nullptr;                   // cptr | lits | vptr | vinc, one block for the wave kernel
+    int wpw = 0;                               // wave kernel: replicas (waves) per workgroup; 0 = 3-kernel path
+    bool k3 = false;                           // wave kernel: every clause has three literals
+    size_t topo_bytes = 0, rep_bytes = 0;      // wave kernel LDS: shared topology, per-replica state
 };
 
 namespace {
@@ -121,6 +126,216 @@ __global__ void k_stoch_status(uint32_t *unsat, uint8_t *act, int64_t *steps, in
     if (all && stop == ODESAT_STOP_EACH) act[r] = 0;  // search breaks (:96-99)
 }
 
+// ---- one wave per replica (small formulas): the whole search step in LDS -----------------------
+// The workgroup copies the topology (clause starts, literals, variable starts, incidences) into
+// LDS once; each of its WPW waves then owns one replica for `nsteps` steps with v, xl and the
+// clause flags in LDS.  Phase 1: lane l evaluates clauses l, l+64, ... and updates their memories;
+// phase 2 (skipped when every clause is satisfied: no variable can flip then) lane l sums variable
+// i's incidences (i = l, l+64, ...), draws and flips.  A wave's LDS operations complete in issue
+// order, so the phases need no barrier, only a compiler fence.  The first three stages of the
+// counter hash depend only on (seed, replica, step) and are hoisted out of the variable loop; the
+// value is the same as stoch_hash's.
+struct SArgs {
+    const int32_t *topo;
+    uint8_t *v;
+    uint64_t *xl;
+    uint8_t *act;
+    int64_t *steps, *sat_step, *done;
+    int32_t n, m, L;
+    int64_t B;
+    uint32_t topo_bytes, rep_bytes;
+    int64_t nsteps;
+    int stop;
+    uint64_t seed;
+    int64_t replica0;
+};
+
+__device__ __forceinline__ void stoch_wave_sync() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_wave_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// A step is a chain of dependent LDS round trips (literal -> value, incidence -> memory) with one
+// wave per SIMD at B = 1024, so latency, not issue, bounds it: the loops are written to put several
+// independent reads in flight at once.  K3 (every clause has three literals, as in the
+// configurations) keeps one 16-byte literal record per clause and evaluates four clauses per lane
+// iteration; the general form walks clause_ptr.
+template <bool K3>
+__device__ __forceinline__ bool stoch_clauses(const int32_t *cptr, const int4 *cl4, const int32_t *lits,
+                                              const uint8_t *v, uint64_t *xl, uint8_t *sat, uint8_t *flag,
+                                              int32_t m, int lane) {
+    bool u = false;
+    if constexpr (K3) {
+        for (int32_t base = 0; base < m; base += 256) {
+            int4 l[4];
+            bool ok[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int32_t c = base + 64 * j + lane;
+                ok[j] = c < m;
+                l[j] = cl4[ok[j] ? c : 0];
+            }
+            uint8_t x0[4], x1[4], x2[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                x0[j] = v[l[j].x >> 1];
+                x1[j] = v[l[j].y >> 1];
+                x2[j] = v[l[j].z >> 1];
+            }
+            uint64_t x[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = xl[ok[j] ? base + 64 * j + lane : 0];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!ok[j]) continue;
+                const bool sj = ((x0[j] != 0) != ((l[j].x & 1) != 0)) || ((x1[j] != 0) != ((l[j].y & 1) != 0)) ||
+                                ((x2[j] != 0) != ((l[j].z & 1) != 0));
+                uint64_t y = x[j];  // stoch.rs:47-51
+                y = sj ? (y > 1 ? y - 1 : 1) : (y > UINT64_MAX - 20 ? UINT64_MAX : y + 20);
+                const int32_t c = base + 64 * j + lane;
+                xl[c] = y;
+                sat[c] = sj ? 1 : 0;
+                if (!sj) {  // its variables may flip
+                    flag[l[j].x >> 1] = 1;
+                    flag[l[j].y >> 1] = 1;
+                    flag[l[j].z >> 1] = 1;
+                }
+                u = u || !sj;
+            }
+        }
+    } else {
+        for (int32_t c = lane; c < m; c += 64) {  // stoch.rs:43-52
+            bool sj = false;
+            for (int32_t q = cptr[c]; q < cptr[c + 1]; ++q) {
+                const int32_t l = lits[q];
+                sj = sj || ((v[l >> 1] != 0) != ((l & 1) != 0));
+            }
+            uint64_t y = xl[c];
+            y = sj ? (y > 1 ? y - 1 : 1) : (y > UINT64_MAX - 20 ? UINT64_MAX : y + 20);
+            xl[c] = y;
+            sat[c] = sj ? 1 : 0;
+            if (!sj)
+                for (int32_t q = cptr[c]; q < cptr[c + 1]; ++q) flag[lits[q] >> 1] = 1;
+            u = u || !sj;
+        }
+    }
+    return u;
+}
+
+// variable i's sums over its incidences (stoch.rs:54-59), reads issued four at a time; integer
+// sums, so the order is free
+__device__ __forceinline__ void stoch_sums(const int32_t *vinc, int32_t q, int32_t e, const uint64_t *xl,
+                                           const uint8_t *sat, uint64_t &tot, uint64_t &uns) {
+    tot = 0;
+    uns = 0;
+    for (; q + 4 <= e; q += 4) {
+        int32_t c[4];
+        uint64_t x[4];
+        uint8_t f[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = vinc[q + j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            x[j] = xl[c[j]];
+            f[j] = sat[c[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            tot += x[j];
+            if (!f[j]) uns += x[j];
+        }
+    }
+    for (; q < e; ++q) {
+        const int32_t c = vinc[q];
+        const uint64_t x = xl[c];
+        tot += x;
+        if (!sat[c]) uns += x;
+    }
+}
+
+template <int WPW, bool K3> __global__ __launch_bounds__(64 * WPW) void k_stoch_wave(SArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.topo);
+        uint4 *dst = reinterpret_cast<uint4 *>(smem);
+        for (uint32_t w = threadIdx.x; w < a.topo_bytes / 16; w += 64 * WPW) dst[w] = src[w];
+    }
+    __syncthreads();
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    const int64_t r = (int64_t)blockIdx.x * WPW + wv;
+    if (r >= a.B || !a.act[r]) return;
+    const int32_t n = a.n, m = a.m, L = a.L;
+    // topology: K3: cl4[m] | vptr[n+1] | vinc[L]; general: cptr[m+1] | lits[L] | vptr[n+1] | vinc[L]
+    const int4 *cl4 = reinterpret_cast<const int4 *>(smem);
+    const int32_t *cptr = reinterpret_cast<const int32_t *>(smem);
+    const int32_t *lits = cptr + m + 1;
+    const int32_t *vptr = K3 ? reinterpret_cast<const int32_t *>(cl4 + m) : lits + L;
+    const int32_t *vinc = vptr + n + 1;
+    uint8_t *rep = smem + a.topo_bytes + (size_t)wv * a.rep_bytes;
+    uint64_t *xl = reinterpret_cast<uint64_t *>(rep);
+    uint8_t *sat = rep + (size_t)8 * m, *v = sat + m, *flag = v + n;
+    int32_t *list = reinterpret_cast<int32_t *>(rep + (((size_t)9 * m + 2 * n + 3) & ~(size_t)3));
+    const int64_t B = a.B;
+    for (int32_t i = lane; i < n; i += 64) {
+        v[i] = a.v[(size_t)i * B + r];
+        flag[i] = 0;
+    }
+    for (int32_t c = lane; c < m; c += 64) xl[c] = a.xl[(size_t)c * B + r];
+    stoch_wave_sync();
+    int64_t st = a.steps[r], ss = a.sat_step[r], dn = a.done[r];
+    bool active = true;
+    const uint64_t h1 = mix64(mix64(a.seed + 0x9E3779B97F4A7C15ULL) ^
+                              ((uint64_t)(a.replica0 + r) * 0xD1B54A32D192ED03ULL + 0x632BE59BD9B4E019ULL));
+    for (int64_t k = 0; k < a.nsteps; ++k) {
+        const bool u = stoch_clauses<K3>(cptr, cl4, lits, v, xl, sat, flag, m, lane);
+        stoch_wave_sync();
+        const bool unsat = __ballot(u) != 0;
+        if (unsat) {  // :54-75
+            const uint64_t h3 = mix64(h1 ^ ((uint64_t)st * 0xA24BAED4963EE407ULL + 0x9FB21C651E98DF25ULL));
+            // Only a variable of an unsat clause has uns > 0, and the draw is >= 1, so no other
+            // variable can flip (its draw is a pure function of the counter, so skipping it
+            // changes nothing): compact the flagged variables, then sum, draw and flip those.
+            int32_t cnt = 0;
+            for (int32_t base = 0; base < n; base += 64) {
+                const int32_t i = base + lane;
+                const bool f = i < n && flag[i];
+                const uint64_t mask = __ballot(f);
+                if (f) {
+                    list[cnt + __popcll(mask & ((1ull << lane) - 1))] = i;
+                    flag[i] = 0;
+                }
+                cnt += __popcll(mask);
+            }
+            stoch_wave_sync();
+            for (int32_t j = lane; j < cnt; j += 64) {
+                const int32_t i = list[j];
+                uint64_t tot, uns;
+                stoch_sums(vinc, vptr[i], vptr[i + 1], xl, sat, tot, uns);
+                const uint64_t h = mix64(h3 ^ ((uint64_t)i * 0x8CB92BA72F3D8DD7ULL + 0x9E3779B97F4A7C15ULL));
+                if (1 + __umul64hi(h, tot) <= uns) v[i] ^= 1;
+            }
+            stoch_wave_sync();
+        } else if (ss < 0) {
+            ss = dn;
+        }
+        dn += 1;
+        st += 1;
+        if (!unsat && a.stop == ODESAT_STOP_EACH) {  // :96-99
+            active = false;
+            break;
+        }
+    }
+    for (int32_t i = lane; i < n; i += 64) a.v[(size_t)i * B + r] = v[i];
+    for (int32_t c = lane; c < m; c += 64) a.xl[(size_t)c * B + r] = xl[c];
+    if (lane == 0) {
+        a.steps[r] = st;
+        a.sat_step[r] = ss;
+        a.done[r] = dn;
+        if (!active) a.act[r] = 0;
+    }
+}
+
 __global__ void k_stoch_reset(uint8_t *v, uint64_t *xl, int64_t n, int64_t m, int64_t B, int64_t r0, int64_t count) {
     const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t nv = (size_t)n * count, total = nv + (size_t)m * count;
@@ -156,13 +371,59 @@ int stoch_reset(odesat_stoch *s, int64_t r0, int64_t count) {
     return ODESAT_OK;
 }
 
+
+constexpr size_t STOCH_LDS_MAX = 160 * 1024 - 1024;
+
+size_t round16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// The wave kernel's width: the widest WPW in {8, 4, 2, 1} whose LDS fits and that still gives
+// every CU (256) a workgroup; 0 (3-kernel path) when one replica's state and the topology do not
+// fit.  ODESAT_STOCH_WAVE=0 forces the 3-kernel path, ODESAT_STOCH_WPW=w forces a width that fits.
+int stoch_wave_width(int64_t B, size_t topo, size_t rep) {
+    const char *e = std::getenv("ODESAT_STOCH_WAVE");
+    if (e && e[0] == '0') return 0;
+    auto fits = [&](int w) { return topo + (size_t)w * rep <= STOCH_LDS_MAX; };
+    if (!fits(1)) return 0;
+    if (const char *f = std::getenv("ODESAT_STOCH_WPW")) {
+        const int w = std::atoi(f);
+        if ((w == 1 || w == 2 || w == 4 || w == 8) && fits(w)) return w;
+    }
+    for (int w : {8, 4, 2}) {
+        if (fits(w) && (B + w - 1) / w >= 256) return w;
+    }
+    return 1;
+}
+
+template <int WPW, bool K3> int launch_stoch_wave(odesat_stoch *s, const SArgs &a) {
+    const size_t lds = s->topo_bytes + (size_t)WPW * s->rep_bytes;
+    STOCH_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_stoch_wave<WPW, K3>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((k_stoch_wave<WPW, K3>), dim3((unsigned)((s->B + WPW - 1) / WPW)), dim3(64 * WPW), lds, s->stream,
+                       a);
+    STOCH_TRY(hipGetLastError());
+    return ODESAT_OK;
+}
+
+template <bool K3> int stoch_wave_launch_k(odesat_stoch *s, const SArgs &a) {
+    switch (s->wpw) {
+    case 8: return launch_stoch_wave<8, K3>(s, a);
+    case 4: return launch_stoch_wave<4, K3>(s, a);
+    case 2: return launch_stoch_wave<2, K3>(s, a);
+    default: return launch_stoch_wave<1, K3>(s, a);
+    }
+}
+
+int stoch_wave_launch(odesat_stoch *s, const SArgs &a) {
+    return s->k3 ? stoch_wave_launch_k<true>(s, a) : stoch_wave_launch_k<false>(s, a);
+}
+
 }  // namespace
 
 extern "C" void odesat_stoch_destroy(odesat_stoch *s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     void *ptrs[] = {s->cptr, s->lits, s->vptr, s->vinc, s->v, s->sat, s->xl, s->unsat, s->act, s->steps,
-                    s->sat_step, s->done};
+                    s->sat_step, s->done, s->topo};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -223,10 +484,39 @@ extern "C" int odesat_stoch_create(int device, const odesat_cnf *f, int64_t batc
         (L && hipMemcpy(s->vinc, vinc.data(), L * 4, hipMemcpyHostToDevice) != hipSuccess) ||
         hipMemset(s->unsat, 0, B * 4) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "hipMemcpy failed"));
+    {  // the wave kernel's topology block (K3: cl4[m] | vptr | vinc; else cptr | lits | vptr | vinc)
+        std::vector<int32_t> topo;
+        topo.reserve((size_t)(m + 1 + 2 * L + n + 1 + 4));
+        s->k3 = L == 3 * m;
+        for (int64_t c = 0; c < m && s->k3; ++c) s->k3 = cptr[c + 1] - cptr[c] == 3;
+        if (s->k3) {  // one 16-byte record per clause: three literals and a pad
+            for (int64_t c = 0; c < m; ++c) {
+                topo.insert(topo.end(), lits.begin() + 3 * c, lits.begin() + 3 * c + 3);
+                topo.push_back(0);
+            }
+        } else {
+            topo.insert(topo.end(), cptr.begin(), cptr.end());
+            topo.insert(topo.end(), lits.begin(), lits.begin() + L);
+        }
+        topo.insert(topo.end(), deg.begin(), deg.end());
+        topo.insert(topo.end(), vinc.begin(), vinc.begin() + L);
+        s->topo_bytes = round16(topo.size() * 4);
+        topo.resize(s->topo_bytes / 4, 0);
+        // xl[m] u64 | sat[m] | v[n] | flag[n] | (4-aligned) list[n] int32
+        s->rep_bytes = round16((((size_t)9 * m + 2 * n + 3) & ~(size_t)3) + (size_t)4 * n);
+        s->wpw = stoch_wave_width(batch, s->topo_bytes, s->rep_bytes);
+        if (s->wpw) {
+            if ((rc = dalloc(&s->topo, topo.size()))) return bail(rc);
+            if (hipMemcpy(s->topo, topo.data(), s->topo_bytes, hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(ODESAT_EDEVICE, "hipMemcpy failed"));
+        }
+    }
     if ((rc = stoch_reset(s, 0, batch))) return bail(rc);
     *out = s;
     return ODESAT_OK;
 }
+
+extern "C" int odesat_stoch_wave_width(const odesat_stoch *s) { return s ? s->wpw : 0; }
 
 extern "C" int odesat_stoch_reset(odesat_stoch *s, int64_t r0, int64_t count) {
     int rc;
@@ -292,8 +582,25 @@ extern "C" int odesat_stoch_search(odesat_stoch *s, uint64_t seed, int64_t repli
     STOCH_TRY(hipMemcpyAsync(s->sat_step, neg.data(), B * 8, hipMemcpyHostToDevice, s->stream));
     STOCH_TRY(hipMemsetAsync(s->done, 0, B * 8, s->stream));
     STOCH_TRY(hipMemsetAsync(s->unsat, 0, B * 4, s->stream));
-    const size_t tc = (size_t)s->m * B, tv = (size_t)s->n * B;
     std::vector<uint8_t> act(B);
+    if (s->wpw) {
+        SArgs a{s->topo, s->v, s->xl, s->act, s->steps, s->sat_step, s->done, (int32_t)s->n, (int32_t)s->m,
+                (int32_t)s->L, s->B, (uint32_t)s->topo_bytes, (uint32_t)s->rep_bytes, 0, stop, seed, replica0};
+        // one launch per poll interval (EACH) or per 4096 steps (NONE): bounded launch durations
+        const int64_t chunk = stop == ODESAT_STOP_EACH ? poll : 4096;
+        for (int64_t k = 0; k < max_steps;) {
+            a.nsteps = std::min<int64_t>(chunk, max_steps - k);
+            if ((rc = stoch_wave_launch(s, a))) return rc;
+            k += a.nsteps;
+            if (stop == ODESAT_STOP_EACH && k < max_steps) {
+                STOCH_TRY(hipMemcpyAsync(act.data(), s->act, B, hipMemcpyDeviceToHost, s->stream));
+                STOCH_TRY(hipStreamSynchronize(s->stream));
+                if (std::none_of(act.begin(), act.end(), [](uint8_t x) { return x != 0; })) break;
+            }
+        }
+        max_steps = 0;  // the 3-kernel loop below does not run
+    }
+    const size_t tc = (size_t)s->m * B, tv = (size_t)s->n * B;
     for (int64_t k = 0; k < max_steps; ++k) {
         if (tc)
             hipLaunchKernelGGL(k_stoch_clause, dim3((unsigned)((tc + 255) / 256)), dim3(256), 0, s->stream, s->cptr,

@@ -51,6 +51,11 @@ class StochSearch:
     def __exit__(self, *a):
         self.close()
 
+    @property
+    def wave_width(self) -> int:
+        """Replicas per workgroup of the one-wave-per-replica kernel, 0 on the 3-kernel path."""
+        return int(lib().odesat_stoch_wave_width(self._h))
+
     def reset(self, r0: int = 0, count: int | None = None):
         count = self.batch - r0 if count is None else count
         check(lib().odesat_stoch_reset(self._h, r0, count))

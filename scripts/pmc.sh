@@ -13,6 +13,6 @@ IFS='|' read -ra GLIST <<< "$PMC_GROUPS"
 for grp in "${GLIST[@]}"; do
     i=$((i+1))
     timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/p$i" -o run -- \
-        python3 "$ROOT/scripts/prof_step.py" > "$OUT/p$i.log" 2>&1 || { echo "pass $i ($grp) failed rc=$?"; tail -5 "$OUT/p$i.log"; exit 1; }
+        python3 "$ROOT/${PROG:-scripts/prof_step.py}" ${PROG_ARGS:-} > "$OUT/p$i.log" 2>&1 || { echo "pass $i ($grp) failed rc=$?"; tail -5 "$OUT/p$i.log"; exit 1; }
     echo "pass $i ($grp) ok"
 done

@@ -98,14 +98,31 @@ def product_formula(name):
     return g
 
 
+# the two device paths: the one-wave-per-replica LDS kernel (default for formulas that fit) and
+# the three-kernel HBM path (ODESAT_STOCH_WAVE=0, the path large formulas take)
+PATHS = {"wave": {}, "hbm": {"ODESAT_STOCH_WAVE": "0"}}
+
+
+def set_path(monkeypatch, path):
+    monkeypatch.delenv("ODESAT_STOCH_WAVE", raising=False)
+    monkeypatch.delenv("ODESAT_STOCH_WPW", raising=False)
+    for k, v in PATHS.get(path, {}).items():
+        monkeypatch.setenv(k, v)
+    if path.startswith("wpw"):
+        monkeypatch.setenv("ODESAT_STOCH_WPW", path[3:])
+
+
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["wave", "hbm"])
 @pytest.mark.parametrize("name", ["easy", "hard", "rand200"])
 @pytest.mark.parametrize("B", [1, 37, 128])
-def test_search_bitexact(name, B):
+def test_search_bitexact(name, B, path, monkeypatch):
     from odesat_amd.stoch import StochSearch
+    set_path(monkeypatch, path)
     _, o = oracle_for(name)
     steps, seed = 300, 5
     with StochSearch(product_formula(name), B) as s:
+        assert (s.wave_width > 0) == (path == "wave")
         r = s.search(seed, steps, replica0=100)
         gv, gxl = s.get_state()
     for b in range(B):
@@ -118,9 +135,11 @@ def test_search_bitexact(name, B):
 
 
 @pytest.mark.gpu
-def test_stop_none_and_chunked_calls():
+@pytest.mark.parametrize("path", ["wave", "hbm"])
+def test_stop_none_and_chunked_calls(path, monkeypatch):
     """STOP_NONE keeps stepping after a satisfying step; two calls continue one RNG stream."""
     from odesat_amd.stoch import ODESAT_STOP_NONE, StochSearch
+    set_path(monkeypatch, path)
     _, o = oracle_for("easy")
     with StochSearch(product_formula("easy"), 4) as s:
         s.search(9, 150, stop=ODESAT_STOP_NONE)
@@ -135,8 +154,10 @@ def test_stop_none_and_chunked_calls():
 
 
 @pytest.mark.gpu
-def test_set_state_roundtrip_and_errors():
+@pytest.mark.parametrize("path", ["wave", "hbm"])
+def test_set_state_roundtrip_and_errors(path, monkeypatch):
     from odesat_amd.stoch import StochSearch
+    set_path(monkeypatch, path)
     _, o = oracle_for("rand200")
     rng = np.random.default_rng(0)
     v = rng.integers(0, 2, (3, o.n)).astype(np.uint8)
@@ -156,3 +177,100 @@ def test_set_state_roundtrip_and_errors():
     from odesat_amd._lib import OdesatError
     with pytest.raises(OdesatError):
         StochSearch(unused, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["wpw1", "wpw2", "wpw4", "wpw8"])
+def test_wave_workgroup_widths(path, monkeypatch):
+    """WPW replicas share a workgroup's LDS topology; 37 replicas leave the last workgroup ragged."""
+    from odesat_amd.stoch import StochSearch
+    set_path(monkeypatch, path)
+    _, o = oracle_for("rand200")
+    B, steps, seed = 37, 200, 11
+    with StochSearch(product_formula("rand200"), B) as s:
+        assert s.wave_width == int(path[3:])
+        r = s.search(seed, steps, poll_interval=17)
+        gv, gxl = s.get_state()
+    for b in range(B):
+        v = np.zeros(o.n, np.uint8)
+        xl = np.ones(o.m, np.uint64)
+        t, sat = o.stoch_search(v, xl, seed, b, steps)
+        assert np.array_equal(gv[b], v.astype(bool)) and np.array_equal(gxl[b], xl)
+        assert r["steps_done"][b] == t
+        assert r["first_sat_step"][b] == (t - 1 if sat else -1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["wave", "hbm"])
+def test_saturating_memories(path, monkeypatch):
+    """xl at the top of u64: +20 saturates (stoch.rs:50) and the u64 sums wrap, on both paths."""
+    from odesat_amd.stoch import ODESAT_STOP_NONE, StochSearch
+    set_path(monkeypatch, path)
+    _, o = oracle_for("easy")
+    rng = np.random.default_rng(3)
+    B = 3
+    v = rng.integers(0, 2, (B, o.n)).astype(np.uint8)
+    xl = (np.uint64(U64) - rng.integers(0, 40, (B, o.m)).astype(np.uint64)).astype(np.uint64)
+    with StochSearch(product_formula("easy"), B) as s:
+        s.set_state(v, xl)
+        s.search(2, 60, stop=ODESAT_STOP_NONE)
+        gv, gxl = s.get_state()
+    for b in range(B):
+        vv, xx = v[b].copy(), xl[b].copy()
+        for k in range(60):
+            o.stoch_step(vv, xx, 2, b, k)
+        assert np.array_equal(gv[b], vv.astype(bool)) and np.array_equal(gxl[b], xx)
+
+
+@pytest.mark.gpu
+def test_large_formula_takes_the_hbm_path(monkeypatch):
+    from odesat_amd.stoch import StochSearch
+    set_path(monkeypatch, "wave")
+    n, m = 10_000, 42_000  # config 2's size: 9m + n bytes of state per replica exceed the LDS
+    var = np.arange(3 * m) % n
+    f = cnf.CNFFormula.from_arrays(np.arange(0, 3 * m + 1, 3), var, var % 2, varnum=n)
+    with StochSearch(f, 8) as s:
+        assert s.wave_width == 0
+    with StochSearch(product_formula("rand200"), 1024) as s:
+        assert s.wave_width >= 4  # 1024 replicas: four or more per workgroup still fill 256 CUs
+
+
+def mixed_width_formula():
+    """rand200 with every 5th clause cut to two literals and every 7th widened to four: the wave
+    kernel's general (clause_ptr) form rather than its three-literal records."""
+    f = oracle_formula("rand200")
+    n = f.varnum
+    cp, var, neg = [0], [], []
+    for c in range(len(f.clause_ptr) - 1):
+        lits = [(int(f.var[s]), int(f.neg[s])) for s in range(f.clause_ptr[c], f.clause_ptr[c + 1])]
+        if c % 5 == 0:
+            lits = lits[:2]
+        if c % 7 == 0:
+            extra = (lits[0][0] + 1) % n
+            if all(x != extra for x, _ in lits):
+                lits.append((extra, c % 2))
+        var += [x for x, _ in lits]
+        neg += [g for _, g in lits]
+        cp.append(len(var))
+    assert len(set(var)) == n
+    return np.array(cp), np.array(var), np.array(neg, np.uint8), n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["wave", "hbm"])
+def test_mixed_clause_widths(path, monkeypatch):
+    from odesat_amd.stoch import StochSearch
+    set_path(monkeypatch, path)
+    cp, var, neg, n = mixed_width_formula()
+    o = Oracle(cp, var, neg, n, "f64")
+    B, steps, seed = 9, 250, 21
+    with StochSearch(cnf.CNFFormula.from_arrays(cp, var, neg, varnum=n), B) as s:
+        assert (s.wave_width > 0) == (path == "wave")
+        r = s.search(seed, steps)
+        gv, gxl = s.get_state()
+    for b in range(B):
+        v = np.zeros(n, np.uint8)
+        xl = np.ones(o.m, np.uint64)
+        t, sat = o.stoch_search(v, xl, seed, b, steps)
+        assert np.array_equal(gv[b], v.astype(bool)) and np.array_equal(gxl[b], xl)
+        assert r["steps_done"][b] == t
