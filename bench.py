@@ -5,15 +5,19 @@ workload: config 2's instance (random 3-SAT n=10 000, m=42 000, generator seed 1
 GPU (the north star's roofline point), dt = 0.01, every replica forced to run all K steps
 (ODESAT_STOP_NONE).  Inputs are initialised on the device before the timed region.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per
-GPU, each steps its own B replicas (global replica index rank*B + b) with no collective in the data
-path -- weak scaling; barrier + max-over-ranks timing via torch.distributed.
+Multi-GPU: `python bench.py --gpus N` starts N ranks itself (torch.distributed.run, one process per
+GPU) when WORLD_SIZE is unset; under the driver's own `torch.distributed.run --nproc-per-node N` the
+ranks are already there.  Each rank steps its own B replicas (global replica index rank*B + b) with
+no collective in the data path -- weak scaling; barrier + max-over-ranks timing via
+torch.distributed (RCCL).
 
 Rank 0 prints ONE JSON line (see DESIGN.md §6 for every field).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -21,6 +25,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD (SIMD-32),
+# at the 2.4 GHz max clock (MI355X_MICROARCH.md, wave scheduling / chip-level parameters)
+VALU_PEAK_GINST = 1024 * 2.4e9 / 2 / 1e9
 
 
 def parse():
@@ -35,15 +42,31 @@ def parse():
     p.add_argument("--cpu-replicas", type=int, default=16)
     p.add_argument("--cpu-steps", type=int, default=300)
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--traffic-dir", default=os.path.join(ROOT, "profiles"),
-                   help="directory of traffic_<kernel>.json files: the dominant kernel's HBM bytes per launch "
-                        "from the PMC passes (scripts/make_traffic.py)")
+    p.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles"),
+                   help="directory of profile_<kernel>.json: the dominant kernel's PMC HBM bytes and VALU "
+                        "instructions as fixed-per-launch + per-step fits (scripts/make_profile_json.py)")
     p.add_argument("--alg", default="auto", choices=["auto", "onchip", "resident", "fused", "twopass"],
                    help="force an algorithm (A/B); auto = the solver's default")
     p.add_argument("--extra-batch", type=int, default=256, help="also time this B (configs[1]); 0 = off")
     p.add_argument("--no-ab", action="store_true",
                    help="skip the in-run A/B line of the HBM-streaming kernel (k_resident) on the same workload")
+    p.add_argument("--no-inter", action="store_true", help="skip the inter-mode (STOP_ANY) line")
     return p.parse_args()
+
+
+def spawn_ranks(args):
+    """`--gpus N` without a launcher: start N ranks (one per GPU) under torch.distributed.run and exit
+    with its status.  Started as a child process before this process touches the GPU."""
+    import torch
+    ndev = torch.cuda.device_count()  # counts devices without initialising HIP
+    if args.gpus > ndev:
+        sys.exit(f"bench.py: --gpus {args.gpus} but only {ndev} GPU(s) are visible")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.run(cmd).returncode)
 
 
 def dist_setup(args):
@@ -51,19 +74,28 @@ def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    devices = 1
     if world > 1:
-        from odesat_amd import device_count
-        local %= max(1, device_count())  # the one-GPU gloo rehearsal maps every rank to GPU 0
         import torch
         import torch.distributed as td
-        # RCCL ("nccl") on GPU boxes; ODESAT_DIST_BACKEND=gloo rehearses N ranks on one GPU (RCCL
-        # refuses two ranks on one device).  Only host scalars cross ranks (odesat_amd/sharding.py).
-        backend = os.environ.get("ODESAT_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        ndev = torch.cuda.device_count()
+        # RCCL ("nccl") on GPU boxes, one rank per GPU; ODESAT_DIST_BACKEND=gloo rehearses N ranks on
+        # fewer GPUs (RCCL refuses two ranks on one device): ranks then share devices round-robin.
+        # Only host scalars cross ranks (odesat_amd/sharding.py).
+        backend = os.environ.get("ODESAT_DIST_BACKEND") or ("nccl" if ndev > 0 else "gloo")
         if backend == "nccl":
+            if local >= ndev:
+                raise SystemExit(f"bench.py: rank {rank} has local rank {local} but only {ndev} GPU(s) are visible")
             torch.cuda.set_device(local)
+            devices = world
+        else:
+            devices = min(world, max(1, ndev))
+            local %= max(1, ndev)
         td.init_process_group(backend=backend)
         dist = td
-    return world, rank, local, dist
+    elif args.gpus != 1:
+        raise SystemExit("bench.py: --gpus N > 1 needs N ranks (run without a launcher to spawn them)")
+    return world, rank, local, dist, devices
 
 
 def barrier_sync(dist, solver, local):
@@ -77,22 +109,23 @@ def barrier_sync(dist, solver, local):
         dist.barrier()
 
 
-STEPS_PER_LAUNCH = 50  # persistent kernel: steps per launch (the state crosses HBM once per launch)
-
-
-def time_gpu(solver, steps, warmup, dist, local, profile):
+def time_gpu(solver, steps, warmup, dist, local, profile, stop):
+    """Warmup, then `steps` steps (one persistent launch; STOP_ANY may end earlier) between barrier +
+    sync pairs."""
     from odesat_amd.system import ODESAT_STOP_NONE
     if warmup:
-        solver.simulate(dt=0.01, max_steps=warmup, stop=ODESAT_STOP_NONE, poll_interval=STEPS_PER_LAUNCH)
+        solver.simulate(dt=0.01, max_steps=warmup, stop=stop, poll_interval=warmup)
     solver.profile(profile)
     barrier_sync(dist, solver, local)
     t0 = time.perf_counter()
-    solver.simulate(dt=0.01, max_steps=steps, stop=ODESAT_STOP_NONE, poll_interval=STEPS_PER_LAUNCH)
+    r = solver.simulate(dt=0.01, max_steps=steps, stop=stop, poll_interval=steps)
     barrier_sync(dist, solver, local)
     t1 = time.perf_counter()
     ms, launches = solver.profile_read() if profile else (None, None)
     solver.profile(False)
-    return t1 - t0, ms, launches
+    if stop == ODESAT_STOP_NONE:
+        assert r["steps_run"] == steps and (r["steps_done"] == steps).all(), "a replica did not take every step"
+    return t1 - t0, ms, launches, int(r["steps_run"])
 
 
 def cpu_threads():
@@ -123,14 +156,28 @@ def cpu_baseline(cp, var, neg, n, m, replicas, steps, threads=1):
                       f"({dt:.1f} s)"}
 
 
+def load_profile(profile_dir, short, B, dtype, config):
+    """PMC fits of one kernel on this workload (scripts/make_profile_json.py), or None."""
+    path = os.path.join(profile_dir, f"profile_{short}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        pj = json.load(fh)
+    if pj.get("batch") != B or pj.get("dtype") != dtype or pj.get("config") != config:
+        return None
+    return pj
+
+
 def main():
     args = parse()
-    world, rank, local, dist = dist_setup(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        spawn_ranks(args)
+    world, rank, local, dist, devices = dist_setup(args)
 
     from odesat_amd import cnf
     from odesat_amd import workloads as wl
     from odesat_amd.sharding import max_over_ranks, shard_range
-    from odesat_amd.system import Solver
+    from odesat_amd.system import ODESAT_STOP_ANY, ODESAT_STOP_NONE, Solver
 
     c = wl.CONFIGS[args.config]
     n, m = c["n"], c["m"]
@@ -139,8 +186,8 @@ def main():
     f = cnf.CNFFormula.from_arrays(cp, v_, n_, n)
     B = args.batch
 
-    def run_batch(batch, profile, alg_name=None):
-        from odesat_amd import _lib, device_count
+    def run_batch(batch, profile, alg_name=None, stop=ODESAT_STOP_NONE):
+        from odesat_amd import _lib
         s = Solver(f, batch, args.dtype, device=local)
         if args.chunk:
             s.set_chunk_replicas(args.chunk)
@@ -148,17 +195,19 @@ def main():
         if alg_name != "auto":
             s.set_algorithm(getattr(_lib, "ODESAT_ALG_" + alg_name.upper()))
         s.init_state(42, replica0=shard_range(rank, world, batch)[0])
-        wall, ms, launches = time_gpu(s, args.steps, args.warmup, dist, local, profile)
+        wall, ms, launches, ran = time_gpu(s, args.steps, args.warmup, dist, local, profile, stop)
         bytes_step = s.clause_kernel_bytes()
         alg = s.algorithm
         s.close()
-        return wall, ms, launches, bytes_step, alg
+        return wall, ms, launches, bytes_step, alg, ran
 
     def roofline(alg, ms, launches, clause_bytes_step):
-        """Dominant kernel: algorithmic bytes per launch ((8n + 16m) B per fp32
-        replica-step -- v, xs, xl read and written once -- x the replica-steps of one launch) / its mean
-        launch time (HIP events on the solver's stream); traffic = PMC HBM bytes per launch of the same
-        kernel and workload (profiles/traffic_<kernel>.json), or None."""
+        """Dominant kernel.  HBM side: algorithmic bytes per launch ((8n + 16m) B per
+        fp32 replica-step -- v, xs, xl read and written once -- x the replica-steps of one launch) / its
+        mean launch time (HIP events on the solver's stream), and the PMC HBM bytes of a launch of this
+        size (profile fit: fixed + per-step bytes).  k_onchip keeps the state on the CU, so HBM does not
+        bound it: its roofline is VALU issue -- PMC VALU instructions of a launch of this size / the
+        launch time, against 1024 SIMDs x one wave64 instruction per 2 cycles at 2.4 GHz."""
         from odesat_amd._lib import ODESAT_ALG_ONCHIP, ODESAT_ALG_RESIDENT
         kernel = {ODESAT_ALG_RESIDENT: "k_resident (persistent; v in LDS, clause memories streamed through HBM "
                                        "every step)",
@@ -169,27 +218,32 @@ def main():
         per_launch_s = ms[0] / 1e3 / nlaunch
         steps_per_launch = args.steps / nlaunch
         per_launch_bytes = clause_bytes_step * steps_per_launch
-        achieved = per_launch_bytes / per_launch_s / 1e9
-        traffic = None
-        tpath = os.path.join(args.traffic_dir, f"traffic_{short}.json")
-        if os.path.exists(tpath):
-            with open(tpath) as fh:
-                tj = json.load(fh)
-            if tj.get("batch") == B and tj.get("dtype") == args.dtype and tj.get("config") == args.config \
-                    and tj.get("steps_per_launch") == steps_per_launch:
-                traffic = tj["hbm_bytes_per_launch"]
-        r = {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-             "algorithmic_bytes_per_launch": per_launch_bytes, "mean_launch_us": per_launch_s * 1e6,
-             "launches": nlaunch, "steps_per_launch": steps_per_launch}
-        if alg == ODESAT_ALG_ONCHIP:
-            r["note"] = ("k_onchip keeps v, dv and the clause memories on the CU for a whole launch: HBM moves "
-                         "the state once per launch (traffic), so the algorithmic rate can exceed the HBM peak; "
-                         "the binding resources are the CU's LDS and VALU issue (DESIGN.md). ab_hbm_streaming is "
-                         "the HBM-bound kernel on the same workload.")
+        hbm_alg = per_launch_bytes / per_launch_s / 1e9
+        pj = load_profile(args.profile_dir, short, B, args.dtype, args.config)
+        traffic = valu = None
+        if pj is not None:
+            traffic = pj["hbm_bytes_fixed"] + pj["hbm_bytes_per_step"] * steps_per_launch
+            if "valu_insts_per_step" in pj:
+                valu = pj["valu_insts_fixed"] + pj["valu_insts_per_step"] * steps_per_launch
+        r = {"kernel": kernel, "traffic": traffic, "mean_launch_us": per_launch_s * 1e6, "launches": nlaunch,
+             "steps_per_launch": steps_per_launch, "algorithmic_bytes_per_launch": per_launch_bytes}
+        hbm = {"achieved": hbm_alg, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_alg / HBM_PEAK_GBS}
+        if alg == ODESAT_ALG_ONCHIP and valu is not None:
+            achieved = valu / per_launch_s / 1e9
+            r.update({"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_GINST,
+                      "unit": "G VALU wave-instructions/s", "frac": achieved / VALU_PEAK_GINST,
+                      "valu_insts_per_launch": valu, "hbm_algorithmic": hbm,
+                      "note": "k_onchip keeps v, dv and the clause memories on the CU for a whole launch: HBM "
+                              "moves the state once per launch (traffic), so the HBM-algorithmic rate exceeds "
+                              "the HBM peak and the binding resource is the CU's VALU issue (plus LDS/barrier "
+                              "latency; DESIGN.md §4.0).  ab_hbm_streaming is the HBM-bound kernel on the same "
+                              "workload."})
+        else:
+            r.update({"bound": "hbm", **hbm})
         return r
 
-    wall, ms, launches, clause_bytes_step, alg = run_batch(B, True)
+    from odesat_amd._lib import ODESAT_ALG_ONCHIP
+    wall, ms, launches, clause_bytes_step, alg, _ = run_batch(B, True)
     wall_max = max_over_ranks(dist, wall)
     total_replica_steps = B * world * args.steps
     value = total_replica_steps / wall_max
@@ -198,18 +252,23 @@ def main():
     tsize = 4 if args.dtype == "f32" else 8
     step_bytes = B * (2 * n + 4 * m) * tsize  # algorithmic per GPU-step: v, xs, xl read + written once
 
-    from odesat_amd._lib import ODESAT_ALG_ONCHIP
     ab = None
     if alg == ODESAT_ALG_ONCHIP and not args.no_ab:
-        w3, ms3, l3, b3, a3 = run_batch(B, True, "resident")
+        w3, ms3, l3, b3, a3, _ = run_batch(B, True, "resident")
         w3 = max_over_ranks(dist, w3)
         ab = {"value": B * world * args.steps / w3, "ms_per_step": w3 * 1e3 / args.steps,
               "roofline": roofline(a3, ms3, l3, b3)}
 
+    inter = None
+    if not args.no_inter:  # simulate_inter (STOP_ANY): multi-step launches with replay at the stop step
+        ri = run_batch(B, False, stop=ODESAT_STOP_ANY)
+        wi, ran = max_over_ranks(dist, ri[0]), ri[5]  # a stop before `steps` ends the run early
+        inter = {"value": B * world * ran / wi, "ms_per_step": wi * 1e3 / ran, "steps_run": ran,
+                 "vs_stop_none": (B * world * ran / wi) / value}
+
     extra = None
     if args.extra_batch and args.extra_batch != B:
-        w2 = run_batch(args.extra_batch, False)[0]
-        w2 = max_over_ranks(dist, w2)
+        w2 = max_over_ranks(dist, run_batch(args.extra_batch, False)[0])
         extra = {"batch_per_gpu": args.extra_batch,
                  "value": args.extra_batch * world * args.steps / w2,
                  "ms_per_step": w2 * 1e3 / args.steps}
@@ -226,7 +285,8 @@ def main():
             "metric": "ODE steps/s x batch on random 3-SAT n=10k m=42k (replica-steps/s)",
             "value": value,
             "unit": "replica-steps/s",
-            "n_gpus": world,
+            "n_gpus": devices,
+            "ranks": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
@@ -244,6 +304,7 @@ def main():
             "step_algorithmic_GBps": step_bytes * args.steps / wall / 1e9,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
+            "inter": inter,
             "extra_batch": extra,
             "ab_hbm_streaming": ab,
         }

@@ -195,7 +195,7 @@ typedef struct {
     double zeta;           /* learning rate; < 0 = density heuristic (system.rs:164-173) */
     int64_t max_steps;     /* > 0 (the reference's None = unbounded is refused) */
     int32_t poll_interval; /* steps between host polls of the stop condition (0 = default 32); with
-                              ODESAT_ALG_RESIDENT also the steps per kernel launch (STOP_ANY: 1) */
+                              the persistent kernels (RESIDENT / ONCHIP) also the steps per launch */
     int32_t dt_policy;     /* ODESAT_DT_PER_REPLICA (0, the device's) | ODESAT_DT_SHARED_SERIAL (1: the
                               reference's one dt threaded through the replicas, system.rs:314-326; the
                               CPU oracle's policy, refused by the device) */
@@ -208,11 +208,27 @@ typedef struct {
  *   first_sat_step[B] : 0-based step at which the replica was allsat, -1 if never (may be NULL)
  *   steps_done[B]     : euler steps applied to the replica in this call (may be NULL)
  *   dt_out[B]         : final adaptive dt per replica (may be NULL)
- *   steps_run         : steps launched (may be NULL)
+ *   steps_run         : steps run: the steps launched, or with STOP_ANY after a stop the stop step + 1
+ *                       (the reference's simulate_inter steps; may be NULL)
  * Declared deviation: adaptive STOP_ANY uses a per-replica dt; the reference threads ONE dt
  * serially through the replicas (system.rs:314-326), which cannot run in parallel. */
 int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t *first_sat_step,
                     int64_t *steps_done, double *dt_out, int64_t *steps_run);
+/* The same run continued for up to p->max_steps more steps (p as in the call that started it): no
+ * bookkeeping restarts -- adaptive dt, frozen replicas (STOP_EACH) and a reached stop step (STOP_ANY)
+ * carry over, steps are numbered from the run's start (first_sat_step is run-relative, steps_done
+ * cumulative).  This is how the reference's unbounded loops (steps = None, system.rs:198, :221,
+ * :296, :333) run in bounded calls without leaving its trajectory.  odesat_set_state /
+ * odesat_init_state end a run (the next continue numbers steps from 0). */
+int odesat_simulate_continue(odesat_solver *s, const odesat_params *p, int64_t *first_sat_step,
+                             int64_t *steps_done, double *dt_out, int64_t *steps_run);
+
+/* A device-side checkpoint of every replica's state and bookkeeping, including the position in a
+ * continued run (one slot per solver, library-owned memory); odesat_rollback restores it (ODESAT_ESTATE
+ * without one).  The sharded inter driver uses it to stop every rank at the global first allsat step
+ * (odesat_amd/sharding.py, cli.cpp --gpus). */
+int odesat_checkpoint(odesat_solver *s);
+int odesat_rollback(odesat_solver *s);
 
 /* Block until all work queued by the solver is done. */
 int odesat_synchronize(odesat_solver *s);

@@ -89,7 +89,10 @@ SIGNATURES = {
     "odesat_euler_step_fixed": (C.c_int, [_P, C.c_double, C.c_double, _u8p]),
     "odesat_euler_step": (C.c_int, [_P, C.c_double, _dp, C.c_double, _u8p]),
     "odesat_simulate": (C.c_int, [_P, C.POINTER(Params), _i64p, _i64p, _dp, _i64p]),
+    "odesat_simulate_continue": (C.c_int, [_P, C.POINTER(Params), _i64p, _i64p, _dp, _i64p]),
     "odesat_synchronize": (C.c_int, [_P]),
+    "odesat_checkpoint": (C.c_int, [_P]),
+    "odesat_rollback": (C.c_int, [_P]),
     "odesat_profile_enable": (C.c_int, [_P, C.c_int]),
     "odesat_profile_read": (C.c_int, [_P, _dp, _i64p]),
     "odesat_clause_kernel_bytes": (_i64, [_P]),

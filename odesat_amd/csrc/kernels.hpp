@@ -981,6 +981,36 @@ __global__ void k_gather(double *dst, const T *b0, const T *b1, const uint8_t *p
     dst[tid] = (double)src[(((size_t)g * items + i) * W + (r % W)) * stride + comp];
 }
 
+// Checkpoint (to_ck) or rollback of one double-buffered state array: group g's words live in buffer
+// par[g]; ck holds them group by group.
+__global__ void k_group_copy(uint32_t *ck, uint32_t *b0, uint32_t *b1, const uint8_t *par, int64_t gwords, int G,
+                             int to_ck) {
+    const int64_t total = gwords * G;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t *cur = par[i / gwords] ? b1 : b0;
+        if (to_ck) ck[i] = cur[i];
+        else cur[i] = ck[i];
+    }
+}
+
+// Per-call bookkeeping of odesat_simulate, queued on the solver's stream (no host round trip):
+// every real replica active, no sat step, no steps done, the adaptive dt restarted at 0.01
+// (system.rs:205) when reset_dt, and the stop word cleared.
+__global__ void k_begin_call(uint8_t *act, uint32_t *unsat, int64_t *sat_step, int64_t *steps_done, void *dtr,
+                             int dtype, int reset_dt, int64_t B, int64_t Bp, int32_t *stop) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r == 0) *stop = 0x7fffffff;
+    if (r >= Bp) return;
+    act[r] = r < B ? 1 : 0;
+    unsat[r] = 0;
+    sat_step[r] = -1;
+    steps_done[r] = 0;
+    if (reset_dt) {
+        if (dtype == ODESAT_F64) ((double *)dtr)[r] = 0.01;
+        else ((float *)dtr)[r] = 0.01f;
+    }
+}
+
 __global__ void k_reset_replicas(uint8_t *act, uint32_t *unsat, int64_t *sat_step, int64_t *steps_done,
                                  void *dtr, int dtype, int64_t r0, int64_t count, int64_t B, int64_t Bp) {
     const int64_t r = r0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

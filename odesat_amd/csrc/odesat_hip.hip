@@ -21,6 +21,7 @@
 #include "resident.hpp"
 #include "wave.hpp"
 #include "onchip.hpp"
+#include "devattr.hpp"
 
 using odesat::fail;
 using namespace odk;
@@ -76,6 +77,25 @@ struct odesat_solver {
     int64_t oc_rec_bytes = 0;
     bool in_range = true;        // every replica's state is in ONCHIP's range (onchip.hip header)
     int64_t bytes = 0;
+    // steps run since the last fresh odesat_simulate: odesat_simulate_continue numbers its steps from
+    // here and keeps every replica's bookkeeping (sat step, steps done, frozen, adaptive dt)
+    int64_t t_base = 0;
+    // pinned host staging for polls and results (no pageable copies on the hot path)
+    int64_t *h_sat = nullptr, *h_done = nullptr;  // [Bp]
+    double *h_dt = nullptr;                       // [Bp] (f32 dt is read into its first half)
+    int32_t *h_stop = nullptr;
+    uint8_t *h_act = nullptr;                     // [Bp]
+    // STOP_ANY replay snapshot of a launch's starting bookkeeping (lazy)
+    uint8_t *snap_par = nullptr;
+    int64_t *snap_sat = nullptr, *snap_done = nullptr;
+    void *snap_dt = nullptr;
+    // odesat_checkpoint slot (lazy): the state of every group and the bookkeeping
+    void *ck_v = nullptr, *ck_c = nullptr, *ck_dt = nullptr;
+    uint8_t *ck_par = nullptr, *ck_act = nullptr;
+    int64_t *ck_sat = nullptr, *ck_done = nullptr;
+    int32_t *ck_stop = nullptr;
+    int64_t ck_t_base = -1;  // -1: no checkpoint taken
+    bool ck_in_range = true;
     // profiling
     bool profile = false;
     struct Pending { int cls; hipEvent_t a, b; };
@@ -586,13 +606,9 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
 
 template <typename T, int R, bool ADA, bool K3, int NTHR = ResShape<R>::NTH>
 int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
-    static bool attr_set = false;  // per instantiation
     const size_t lds = res_lds_bytes(s->n, R, sizeof(T), ADA);
-    if (!attr_set) {
-        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)RES_LDS_MAX));
-        attr_set = true;
-    }
+    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR>),
+                                   (int)RES_LDS_MAX));
     {
         Timed tm(s, 0);
         hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR>), dim3(s->G), dim3(NTHR), lds, s->stream, a);
@@ -602,15 +618,10 @@ int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
 }
 
 template <typename T, bool ADA, int WPW> int launch_wave_k(odesat_solver *s, WArgs<T> a) {
-    static bool attr_set = false;  // per instantiation
     a.topo_bytes = (uint32_t)wave_topo_bytes(s->n, s->m);
     a.rep_bytes = (uint32_t)wave_lds_bytes(s->n, s->m, s->L, sizeof(T), ADA);
     const size_t lds = a.topo_bytes + (size_t)WPW * a.rep_bytes;
-    if (!attr_set) {
-        HIP_TRY(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wave<T, ADA, WPW>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)RES_LDS_MAX));
-        attr_set = true;
-    }
+    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_wave<T, ADA, WPW>), (int)RES_LDS_MAX));
     {
         Timed tm(s, 0);
         hipLaunchKernelGGL((k_wave<T, ADA, WPW>), dim3((unsigned)((s->G + WPW - 1) / WPW)), dim3(WAVE_NTH * WPW), lds,
@@ -622,8 +633,9 @@ template <typename T, bool ADA, int WPW> int launch_wave_k(odesat_solver *s, WAr
 
 template <typename T>
 int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
-                int stop_mode) {
+                int stop_mode, bool oop) {
     WArgs<T> a{};
+    a.oop = oop ? 1 : 0;
     a.cl4 = s->res_cl4;
     a.tp4 = s->wv_tp4;
     a.vst = s->wv_vst;
@@ -661,9 +673,11 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
 
 template <typename T>
 int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
-                    int stop_mode) {
-    if (s->res_wave) return launch_wave<T>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode);
+                    int stop_mode, bool oop) {
+    if (s->res_wave) return launch_wave<T>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode, oop);
+    if (oop && adaptive) return fail(ODESAT_EINVAL, "out-of-place RESIDENT launches are fixed-step only");
     RArgs<T> a{};
+    a.oop = oop ? 1 : 0;
     a.cl4 = s->res_cl4;
     a.cptr = s->cptr;
     a.lits = s->lits;
@@ -714,8 +728,9 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
     }
 }
 
-int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zeta, int stop_mode) {
+int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zeta, int stop_mode, bool oop) {
     onchip::Args a{};
+    a.oop = oop ? 1 : 0;
     a.rec = s->oc_rec;
     a.rec_bytes = (uint32_t)s->oc_rec_bytes;
     a.lds = onchip::lds_map(s->n);
@@ -746,9 +761,9 @@ int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zet
 }
 
 int dispatch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
-                      int stop_mode) {
-    return s->dtype == ODESAT_F64 ? launch_resident<double>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode)
-                                  : launch_resident<float>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode);
+                      int stop_mode, bool oop) {
+    return s->dtype == ODESAT_F64 ? launch_resident<double>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode, oop)
+                                  : launch_resident<float>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode, oop);
 }
 
 template <typename T> int deriv_t(odesat_solver *s, double zeta) {
@@ -940,6 +955,12 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
                     s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
                     s->sat_step, s->steps_done, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec, s->wv_tp4, s->wv_vst};
     for (void *p : ptrs) dfree(p);
+    void *snaps[] = {s->snap_par, s->snap_sat, s->snap_done, s->snap_dt, s->ck_v, s->ck_c, s->ck_dt, s->ck_par,
+                     s->ck_act, s->ck_sat, s->ck_done, s->ck_stop};
+    for (void *p : snaps) dfree(p);
+    void *pinned[] = {s->h_sat, s->h_done, s->h_dt, s->h_stop, s->h_act};
+    for (void *p : pinned)
+        if (p) (void)hipHostFree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
     delete s;
 }
@@ -1174,6 +1195,11 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     if ((rc = dmalloc(s, (void **)&s->sat_step, s->Bp * 8))) return bail(rc);
     if ((rc = dmalloc(s, (void **)&s->steps_done, s->Bp * 8))) return bail(rc);
     if ((rc = dmalloc(s, (void **)&s->stop, 16))) return bail(rc);
+    if (hipHostMalloc((void **)&s->h_sat, s->Bp * 8) != hipSuccess ||
+        hipHostMalloc((void **)&s->h_done, s->Bp * 8) != hipSuccess ||
+        hipHostMalloc((void **)&s->h_dt, s->Bp * 8) != hipSuccess ||
+        hipHostMalloc((void **)&s->h_stop, 16) != hipSuccess || hipHostMalloc((void **)&s->h_act, s->Bp) != hipSuccess)
+        return bail(fail(ODESAT_ENOMEM, "hipHostMalloc failed"));
     if (hipMemsetAsync(s->err, 0, s->Bp * 8, s->stream) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "memset failed"));
     // default state: v = 0, xs = init_short_term_memory, xl = 1
@@ -1249,6 +1275,7 @@ extern "C" int odesat_set_state(odesat_solver *s, int64_t r0, int64_t count, con
     };
     s->in_range = s->in_range && within(v, count * s->n, -1.0, 1.0) && within(xs, count * s->m, -1.0, 1.0) &&
                   within(xl, count * s->m, 1.0, 1e30);
+    s->t_base = 0;
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ODESAT_OK;
 }
@@ -1259,6 +1286,7 @@ extern "C" int odesat_init_state(odesat_solver *s, uint64_t seed, int64_t replic
     if ((rc = init_dispatch(s, seed, replica0, false))) return rc;
     if ((rc = reset_replicas(s, 0, s->Bp))) return rc;
     s->in_range = true;  // v in [-1, 1), xs = +-1, xl = 1
+    s->t_base = 0;
     HIP_TRY(hipStreamSynchronize(s->stream));
     return ODESAT_OK;
 }
@@ -1350,69 +1378,131 @@ extern "C" int odesat_euler_step(odesat_solver *s, double tol, double *dt, doubl
     return single_step(s, true, tol, 0.0, zeta, dt, allsat);
 }
 
-// odesat_simulate for RESIDENT: launches of many steps (STOP_ANY: one step per launch, so no
-// replica runs past the step at which another one satisfied the formula), polled every `poll`
-// steps.
+// Results of a simulate call: per-replica bookkeeping through the pinned staging buffers, one sync.
 static int finish_simulate(odesat_solver *s, const odesat_params *p, bool adaptive, int64_t t_run,
                            int64_t *first_sat_step, int64_t *steps_done, double *dt_out, int64_t *steps_run) {
-    int rc;
+    if (first_sat_step) HIP_TRY(hipMemcpyAsync(s->h_sat, s->sat_step, s->B * 8, hipMemcpyDeviceToHost, s->stream));
+    if (steps_done) HIP_TRY(hipMemcpyAsync(s->h_done, s->steps_done, s->B * 8, hipMemcpyDeviceToHost, s->stream));
+    if (dt_out && adaptive)
+        HIP_TRY(hipMemcpyAsync(s->h_dt, s->dtr, s->B * s->tsize, hipMemcpyDeviceToHost, s->stream));
+    if (p->stop == ODESAT_STOP_ANY) HIP_TRY(hipMemcpyAsync(s->h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    // simulate_inter runs T + 1 steps when step T is the first allsat one (system.rs:291): launches
+    // after it were no-ops
+    if (p->stop == ODESAT_STOP_ANY && *s->h_stop != INT_MAX)
+        t_run = std::max<int64_t>(0, std::min<int64_t>(t_run, (int64_t)*s->h_stop - s->t_base + 1));
+    s->in_range = true;  // every replica that stepped took a clamped step
+    s->t_base += t_run;
     if (steps_run) *steps_run = t_run;
-    if (first_sat_step) HIP_TRY(hipMemcpy(first_sat_step, s->sat_step, s->B * 8, hipMemcpyDeviceToHost));
-    if (steps_done) HIP_TRY(hipMemcpy(steps_done, s->steps_done, s->B * 8, hipMemcpyDeviceToHost));
+    if (first_sat_step) std::memcpy(first_sat_step, s->h_sat, s->B * 8);
+    if (steps_done) std::memcpy(steps_done, s->h_done, s->B * 8);
     if (dt_out) {
-        if (!adaptive) {
-            for (int64_t r = 0; r < s->B; ++r) dt_out[r] = p->dt;
-        } else if ((rc = get_dt(s, dt_out))) {
-            return rc;
-        }
+        for (int64_t r = 0; r < s->B; ++r)
+            dt_out[r] = !adaptive ? p->dt
+                                  : (s->dtype == ODESAT_F64 ? s->h_dt[r] : (double)reinterpret_cast<float *>(s->h_dt)[r]);
     }
     return s->profile ? ODESAT_OK : drain_profile(s);
 }
 
+// STOP_ANY replay: the bookkeeping a multi-step launch starts from (the state itself survives in the
+// other buffer of each group, the launch writing out of place).
+static int ensure_snapshot(odesat_solver *s) {
+    if (s->snap_par) return ODESAT_OK;
+    int rc;
+    if ((rc = dmalloc(s, (void **)&s->snap_par, s->G)) || (rc = dmalloc(s, (void **)&s->snap_sat, s->Bp * 8)) ||
+        (rc = dmalloc(s, (void **)&s->snap_done, s->Bp * 8)) || (rc = dmalloc(s, &s->snap_dt, s->Bp * s->tsize)))
+        return rc;
+    return ODESAT_OK;
+}
+
+static int snapshot(odesat_solver *s, bool restore) {
+    auto cp = [&](void *dst, const void *src, size_t bytes) {
+        return hipMemcpyAsync(restore ? const_cast<void *>(src) : dst, restore ? dst : src, bytes,
+                              hipMemcpyDeviceToDevice, s->stream);
+    };
+    HIP_TRY(cp(s->snap_par, s->par, s->G));
+    HIP_TRY(cp(s->snap_sat, s->sat_step, s->Bp * 8));
+    HIP_TRY(cp(s->snap_done, s->steps_done, s->Bp * 8));
+    HIP_TRY(cp(s->snap_dt, s->dtr, s->Bp * s->tsize));
+    if (restore) HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)s->stop, INT_MAX, 1, s->stream));
+    return ODESAT_OK;
+}
+
+static int read_stop(odesat_solver *s, int32_t *out) {
+    HIP_TRY(hipMemcpyAsync(s->h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    *out = *s->h_stop;
+    return ODESAT_OK;
+}
+
+// odesat_simulate for the persistent kernels (RESIDENT / k_wave / ONCHIP): launches of `poll` steps,
+// polled at the launch ends.  STOP_ANY (simulate_inter, system.rs:278-294): every replica takes the
+// step at which the first one is allsat, and none goes further.  The launches are written out of
+// place (the starting state survives in the other buffer of each group); when one finds the first
+// allsat step T inside it, the bookkeeping is restored and the launch re-runs from its start to T
+// exactly -- bit-identical, the integration being deterministic -- so the multi-step launches cost
+// nothing over STOP_NONE until the stop.  RESIDENT's adaptive pass updates in place: one step per
+// launch there.
 static int simulate_resident(odesat_solver *s, const odesat_params *p, bool adaptive, double zeta, double tol,
                              int poll, int64_t *first_sat_step, int64_t *steps_done, double *dt_out,
                              int64_t *steps_run) {
     int rc = ODESAT_OK;
-    // launches of `poll` steps (STOP_ANY: 1, so no replica runs past the stop step), aligned to the
-    // poll points.  ONCHIP needs in-range states (onchip.hip): when the caller's state may not be,
-    // the first step runs RESIDENT, whose clamps bring every state into range.
-    const int per_launch = p->stop == ODESAT_STOP_ANY ? 1 : poll;
-    // (the kernel omits the rigidity term and uses med3 clamps: both exact for finite zeta and a
-    // finite, normal dt -- onchip.hip)
+    // ONCHIP needs in-range states (onchip.hip): when the caller's state may not be, the first step
+    // runs RESIDENT, whose clamps bring every state into range.  (The kernel omits the rigidity term
+    // and uses med3 clamps: both exact for finite zeta and a finite, normal dt -- onchip.hip.)
     const double adt = std::fabs(p->dt);
     const bool oc = s->alg == ODESAT_ALG_ONCHIP && !adaptive && std::fabs(zeta) <= 1e6 && adt >= 1e-30 && adt <= 1e30;
-    int32_t h_stop = INT_MAX;
-    std::vector<uint8_t> h_act(s->Bp);
+    const bool any = p->stop == ODESAT_STOP_ANY;
+    const bool replay = any && (oc || s->res_wave || !adaptive);
+    const int per_launch = any && !replay ? 1 : poll;
+    const int64_t base = s->t_base;
+    if (replay && (rc = ensure_snapshot(s))) return rc;
+    auto launch = [&](int64_t t0, int k, bool oop) -> int {
+        const bool use_oc = oc && (t0 > 0 || s->in_range);
+        return use_oc ? launch_onchip(s, (int)(base + t0), k, p->dt, zeta, p->stop, oop)
+                      : dispatch_resident(s, (int)(base + t0), k, adaptive, p->dt, zeta, tol, p->stop, oop);
+    };
     int64_t t = 0, next_poll = poll;
     while (t < p->max_steps) {
         const bool use_oc = oc && (t > 0 || s->in_range);
         int k = (int)std::min<int64_t>(std::min<int64_t>(per_launch, next_poll - t), p->max_steps - t);
         if (oc && !use_oc) k = 1;
-        if ((rc = use_oc ? launch_onchip(s, (int)t, k, p->dt, zeta, p->stop)
-                         : dispatch_resident(s, (int)t, k, adaptive, p->dt, zeta, tol, p->stop)))
-            return rc;
+        if (replay && k > 1 && (rc = snapshot(s, false))) return rc;
+        if ((rc = launch(t, k, replay))) return rc;
+        const int64_t t0 = t;
         t += k;
-        if (t < next_poll) continue;
-        next_poll += poll;
-        if (p->stop != ODESAT_STOP_NONE && t < p->max_steps) {
-            HIP_TRY(hipMemcpyAsync(&h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream));
-            HIP_TRY(hipMemcpyAsync(h_act.data(), s->act, s->Bp, hipMemcpyDeviceToHost, s->stream));
-            HIP_TRY(hipStreamSynchronize(s->stream));
-            if (p->stop == ODESAT_STOP_ANY && h_stop != INT_MAX) break;
-            if (p->stop == ODESAT_STOP_EACH) {
-                bool any = false;
-                for (int64_t r = 0; r < s->B && !any; ++r) any = h_act[r] != 0;
-                if (!any) break;
+        const bool at_poll = t >= next_poll;
+        if (at_poll) next_poll += poll;
+        if (replay) {  // every launch is polled, the last one too: it may have run past the stop
+            int32_t h_stop = INT_MAX;
+            if ((rc = read_stop(s, &h_stop))) return rc;
+            if (h_stop == INT_MAX) continue;
+            const int64_t T = (int64_t)h_stop - base;  // this call's step index of the first allsat step
+            if (T < t - 1) {  // replicas ran past T: back to the launch's start, then exactly to T
+                if ((rc = snapshot(s, true))) return rc;
+                if ((rc = launch(t0, (int)(T - t0 + 1), true))) return rc;
+                t = T + 1;
             }
+            break;
+        }
+        if (!at_poll || p->stop == ODESAT_STOP_NONE || t >= p->max_steps) continue;
+        if (any) {
+            int32_t h_stop = INT_MAX;
+            if ((rc = read_stop(s, &h_stop))) return rc;
+            if (h_stop != INT_MAX) break;
+        } else {  // STOP_EACH: stop once every replica is frozen
+            HIP_TRY(hipMemcpyAsync(s->h_act, s->act, s->Bp, hipMemcpyDeviceToHost, s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            bool live = false;
+            for (int64_t r = 0; r < s->B && !live; ++r) live = s->h_act[r] != 0;
+            if (!live) break;
         }
     }
-    s->in_range = true;  // every replica took at least one clamped step
     return finish_simulate(s, p, adaptive, t, first_sat_step, steps_done, dt_out, steps_run);
 }
 
-extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t *first_sat_step,
-                               int64_t *steps_done, double *dt_out, int64_t *steps_run) {
+static int simulate_impl(odesat_solver *s, const odesat_params *p, bool cont, int64_t *first_sat_step,
+                         int64_t *steps_done, double *dt_out, int64_t *steps_run) {
     int rc;
     if ((rc = check_solver(s))) return rc;
     if (!p) return fail(ODESAT_EINVAL, "null params");
@@ -1427,26 +1517,27 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
     const double zeta = p->zeta < 0 ? default_zeta(s) : p->zeta;
     if ((rc = ensure_w(s))) return rc;
     if (adaptive && (rc = ensure_scratch(s))) return rc;
-    if ((rc = set_stop(s, INT_MAX))) return rc;
-    {   // per-call bookkeeping: sat step / steps done restart; adaptive dt restarts at 0.01 (:205)
-        std::vector<int64_t> minus = host_i64(s->Bp, -1), zero = host_i64(s->Bp, 0);
-        HIP_TRY(hipMemcpy(s->sat_step, minus.data(), s->Bp * 8, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(s->steps_done, zero.data(), s->Bp * 8, hipMemcpyHostToDevice));
-        if ((rc = set_all_active(s))) return rc;
-        if (adaptive && (rc = put_dt(s, nullptr, 0.01))) return rc;
+    if (!cont) {  // per-call bookkeeping restarts; adaptive dt restarts at 0.01 (:205) -- one async kernel
+        s->t_base = 0;
+        const int threads = 256;
+        hipLaunchKernelGGL(k_begin_call, dim3((unsigned)((s->Bp + threads - 1) / threads)), dim3(threads), 0,
+                           s->stream, s->act, s->unsat, s->sat_step, s->steps_done, s->dtr, s->dtype, adaptive ? 1 : 0,
+                           s->B, s->Bp, s->stop);
+        HIP_TRY(hipGetLastError());
+    } else {
+        if (s->t_base + p->max_steps > INT_MAX - 1)
+            return fail(ODESAT_EINVAL, "continued run exceeds 2^31-2 steps");
+        if (p->stop == ODESAT_STOP_ANY) {  // a run that already stopped (simulate_inter broke) stays stopped
+            int32_t h_stop = INT_MAX;
+            if ((rc = read_stop(s, &h_stop))) return rc;
+            if (h_stop != INT_MAX) return finish_simulate(s, p, adaptive, 0, first_sat_step, steps_done, dt_out, steps_run);
+        }
     }
     const int poll = p->poll_interval > 0 ? p->poll_interval : 32;
     if (s->alg == ODESAT_ALG_ONCHIP && !adaptive)
         return simulate_resident(s, p, adaptive, zeta, tol, poll, first_sat_step, steps_done, dt_out, steps_run);
-    if ((s->alg == ODESAT_ALG_RESIDENT || s->alg == ODESAT_ALG_ONCHIP) && (!adaptive || s->res_ada)) return simulate_resident(s, p, adaptive, zeta, tol, poll, first_sat_step,
-                                                                steps_done, dt_out, steps_run);
-    int32_t *h_stop = nullptr;
-    uint8_t *h_act = nullptr;
-    HIP_TRY(hipHostMalloc((void **)&h_stop, sizeof(int32_t)));
-    if (hipHostMalloc((void **)&h_act, s->Bp) != hipSuccess) {
-        (void)hipHostFree(h_stop);
-        return fail(ODESAT_ENOMEM, "hipHostMalloc failed");
-    }
+    if ((s->alg == ODESAT_ALG_RESIDENT || s->alg == ODESAT_ALG_ONCHIP) && (!adaptive || s->res_ada))
+        return simulate_resident(s, p, adaptive, zeta, tol, poll, first_sat_step, steps_done, dt_out, steps_run);
     // Schedule: replicas are independent, so with STOP_EACH / STOP_NONE the batch may be stepped
     // chunk by chunk (all steps of one chunk, then the next).  STOP_ANY needs lock-step.  FUSED has
     // no per-chunk buffer: its chunk is the whole batch unless CHUNK_MAJOR is forced.
@@ -1455,48 +1546,40 @@ extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t
                              (s->schedule == ODESAT_SCHED_CHUNK_MAJOR ||
                               (s->schedule == ODESAT_SCHED_AUTO && s->G > chunk));
     const int span = chunk_major ? chunk : s->G;
+    const int64_t base = s->t_base;
     int64_t t_run = 0;
-    rc = ODESAT_OK;
-    for (int gA = 0; gA < s->G && rc == ODESAT_OK; gA += span) {
+    for (int gA = 0; gA < s->G; gA += span) {
         const int gB = std::min(s->G, gA + span);
         const int64_t r0 = (int64_t)gA * s->W, r1 = std::min<int64_t>((int64_t)gB * s->W, s->B);
         int64_t t = 0;
         for (; t < p->max_steps; ++t) {
-            if ((rc = dispatch_step(s, (int)t, adaptive, p->dt, zeta, tol, p->stop, gA, gB))) break;
+            if ((rc = dispatch_step(s, (int)(base + t), adaptive, p->dt, zeta, tol, p->stop, gA, gB))) return rc;
             if (p->stop != ODESAT_STOP_NONE && (t + 1) % poll == 0 && t + 1 < p->max_steps) {
                 // poll the stop condition (results are exact regardless: later launches are no-ops)
-                if (hipMemcpyAsync(h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
-                    hipMemcpyAsync(h_act + r0, s->act + r0, r1 - r0, hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
-                    hipStreamSynchronize(s->stream) != hipSuccess) {
-                    rc = fail(ODESAT_EDEVICE, "poll failed");
-                    break;
-                }
-                if (p->stop == ODESAT_STOP_ANY && *h_stop != INT_MAX) { ++t; break; }
+                HIP_TRY(hipMemcpyAsync(s->h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream));
+                HIP_TRY(hipMemcpyAsync(s->h_act + r0, s->act + r0, r1 - r0, hipMemcpyDeviceToHost, s->stream));
+                HIP_TRY(hipStreamSynchronize(s->stream));
+                if (p->stop == ODESAT_STOP_ANY && *s->h_stop != INT_MAX) { ++t; break; }
                 if (p->stop == ODESAT_STOP_EACH) {
-                    bool any = false;
-                    for (int64_t r = r0; r < r1 && !any; ++r) any = h_act[r] != 0;
-                    if (!any) { ++t; break; }
+                    bool live = false;
+                    for (int64_t r = r0; r < r1 && !live; ++r) live = s->h_act[r] != 0;
+                    if (!live) { ++t; break; }
                 }
             }
         }
         t_run = std::max(t_run, t);
     }
-    (void)hipHostFree(h_stop);
-    (void)hipHostFree(h_act);
-    if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(s->stream));
-    s->in_range = true;
-    if (steps_run) *steps_run = t_run;
-    if (first_sat_step) HIP_TRY(hipMemcpy(first_sat_step, s->sat_step, s->B * 8, hipMemcpyDeviceToHost));
-    if (steps_done) HIP_TRY(hipMemcpy(steps_done, s->steps_done, s->B * 8, hipMemcpyDeviceToHost));
-    if (dt_out) {
-        if (!adaptive) {
-            for (int64_t r = 0; r < s->B; ++r) dt_out[r] = p->dt;
-        } else if ((rc = get_dt(s, dt_out))) {
-            return rc;
-        }
-    }
-    return s->profile ? ODESAT_OK : drain_profile(s);
+    return finish_simulate(s, p, adaptive, t_run, first_sat_step, steps_done, dt_out, steps_run);
+}
+
+extern "C" int odesat_simulate(odesat_solver *s, const odesat_params *p, int64_t *first_sat_step,
+                               int64_t *steps_done, double *dt_out, int64_t *steps_run) {
+    return simulate_impl(s, p, false, first_sat_step, steps_done, dt_out, steps_run);
+}
+
+extern "C" int odesat_simulate_continue(odesat_solver *s, const odesat_params *p, int64_t *first_sat_step,
+                                        int64_t *steps_done, double *dt_out, int64_t *steps_run) {
+    return simulate_impl(s, p, true, first_sat_step, steps_done, dt_out, steps_run);
 }
 
 // ---- batched evaluate_cnf ----------------------------------------------
@@ -1560,8 +1643,10 @@ extern "C" int odesat_evaluate(odesat_solver *s, uint8_t *satisfied, int64_t *fi
     if ((rc = check_solver(s))) return rc;
     uint32_t *flags = nullptr;
     int64_t *first = nullptr;
-    HIP_TRY(hipMalloc(&flags, (size_t)s->B * 4 + 8));
-    first = reinterpret_cast<int64_t *>(flags + ((s->B + 1) & ~int64_t(1)));
+    // B flags, padded to an 8-byte boundary, then the first-satisfied index
+    const int64_t padded = (s->B + 1) & ~int64_t(1);
+    HIP_TRY(hipMalloc(&flags, (size_t)padded * 4 + 8));
+    first = reinterpret_cast<int64_t *>(flags + padded);
     rc = s->dtype == ODESAT_F64 ? evaluate_t<double>(s, flags, first) : evaluate_t<float>(s, flags, first);
     std::vector<uint32_t> u;
     int64_t f = -1;
@@ -1580,6 +1665,60 @@ extern "C" int odesat_evaluate(odesat_solver *s, uint8_t *satisfied, int64_t *fi
     if (satisfied)
         for (int64_t r = 0; r < s->B; ++r) satisfied[r] = u[(size_t)r] ? 0 : 1;
     if (first_satisfied) *first_satisfied = f;
+    return ODESAT_OK;
+}
+
+// ---- checkpoint / rollback ------------------------------------------------------------------
+static int checkpoint_copy(odesat_solver *s, bool to_ck) {
+    const int threads = 256, blocks = 2048;
+    const int64_t vw = (int64_t)s->n * s->W * (int64_t)s->tsize / 4, cw = 2 * (int64_t)s->m * s->W * (int64_t)s->tsize / 4;
+    auto cp = [&](void *dst, const void *src, size_t bytes) {
+        return hipMemcpyAsync(to_ck ? dst : const_cast<void *>(src), to_ck ? src : dst, bytes, hipMemcpyDeviceToDevice,
+                              s->stream);
+    };
+    if (!to_ck) HIP_TRY(cp(s->ck_par, s->par, s->G));  // the groups' current buffers first
+    hipLaunchKernelGGL(k_group_copy, dim3(blocks), dim3(threads), 0, s->stream, (uint32_t *)s->ck_v, (uint32_t *)s->v[0],
+                       (uint32_t *)s->v[1], s->par, vw, s->G, to_ck ? 1 : 0);
+    HIP_TRY(hipGetLastError());
+    if (cw > 0) {
+        hipLaunchKernelGGL(k_group_copy, dim3(blocks), dim3(threads), 0, s->stream, (uint32_t *)s->ck_c,
+                           (uint32_t *)s->c[0], (uint32_t *)s->c[1], s->par, cw, s->G, to_ck ? 1 : 0);
+        HIP_TRY(hipGetLastError());
+    }
+    if (to_ck) HIP_TRY(cp(s->ck_par, s->par, s->G));
+    HIP_TRY(cp(s->ck_act, s->act, s->Bp));
+    HIP_TRY(cp(s->ck_sat, s->sat_step, s->Bp * 8));
+    HIP_TRY(cp(s->ck_done, s->steps_done, s->Bp * 8));
+    HIP_TRY(cp(s->ck_dt, s->dtr, s->Bp * s->tsize));
+    HIP_TRY(cp(s->ck_stop, s->stop, 4));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    return ODESAT_OK;
+}
+
+extern "C" int odesat_checkpoint(odesat_solver *s) {
+    int rc;
+    if ((rc = check_solver(s))) return rc;
+    if (!s->ck_v) {
+        if ((rc = dmalloc(s, &s->ck_v, state_elems(s, s->n) * s->tsize)) ||
+            (rc = dmalloc(s, &s->ck_c, 2 * state_elems(s, s->m) * s->tsize)) ||
+            (rc = dmalloc(s, &s->ck_dt, s->Bp * s->tsize)) || (rc = dmalloc(s, (void **)&s->ck_par, s->G)) ||
+            (rc = dmalloc(s, (void **)&s->ck_act, s->Bp)) || (rc = dmalloc(s, (void **)&s->ck_sat, s->Bp * 8)) ||
+            (rc = dmalloc(s, (void **)&s->ck_done, s->Bp * 8)) || (rc = dmalloc(s, (void **)&s->ck_stop, 16)))
+            return rc;
+    }
+    if ((rc = checkpoint_copy(s, true))) return rc;
+    s->ck_t_base = s->t_base;
+    s->ck_in_range = s->in_range;
+    return ODESAT_OK;
+}
+
+extern "C" int odesat_rollback(odesat_solver *s) {
+    int rc;
+    if ((rc = check_solver(s))) return rc;
+    if (s->ck_t_base < 0) return fail(ODESAT_ESTATE, "odesat_rollback: no checkpoint");
+    if ((rc = checkpoint_copy(s, false))) return rc;
+    s->t_base = s->ck_t_base;
+    s->in_range = s->ck_in_range;
     return ODESAT_OK;
 }
 

@@ -30,6 +30,7 @@
 #pragma clang fp contract(off)
 
 #include "onchip.hpp"
+#include "devattr.hpp"
 
 #include <climits>
 #include <utility>
@@ -260,6 +261,9 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
     float *V = (p ? a.v1 : a.v0) + (size_t)g * a.n;
     float2 *CM = reinterpret_cast<float2 *>((p ? a.c1 : a.c0) + (size_t)g * a.m * 2);
+    // out of place (a.oop, STOP_ANY launches of several steps): the final state goes to the other
+    // buffer and par flips, so the launch's starting state survives for a replay
+    const bool q = a.oop ? !p : p;
     const int n2 = a.n + SINKS;
     const uint32_t UNS = DVC + 4u * (uint32_t)n2;  // two unsat flags
     int64_t sat = a.sat_step[g], done = a.steps_done[g];
@@ -303,20 +307,22 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         }
     }
 
-    for (int i = lane; i < a.n; i += NTH) V[i] = lds_f(4u * i);  // written by this lane in the last update
+    float *Vo = (q ? a.v1 : a.v0) + (size_t)g * a.n;
+    for (int i = lane; i < a.n; i += NTH) Vo[i] = lds_f(4u * i);  // written by this lane in the last update
     {   // opaque copies: the store addresses are recomputed here instead of being kept live (two
         // VGPRs per tile) across the step loop from the loads above
-        float2 *CMs = CM;
+        float2 *CMs = reinterpret_cast<float2 *>((q ? a.c1 : a.c0) + (size_t)g * a.m * 2);
         const cint32 *tcs = tc;
         asm volatile("" : "+s"(CMs), "+s"(tcs));
         mem_io<TR>(std::make_integer_sequence<int, TR>{}, tcs, a.ntiles, CMs, mr, lane, false);
-    }
-    for (int t = 0; t < a.tl; ++t) {  // this lane's own LDS slots: no barrier needed
-        const int c0 = tc[min(TR + t, a.ntiles)], c1 = tc[min(TR + t + 1, a.ntiles)];
-        const int c = c0 + lane;
-        if (c < c1) CM[c] = *lds_f2(mem_addr(a, t, lane));
+        for (int t = 0; t < a.tl; ++t) {  // this lane's own LDS slots: no barrier needed
+            const int c0 = tc[min(TR + t, a.ntiles)], c1 = tc[min(TR + t + 1, a.ntiles)];
+            const int c = c0 + lane;
+            if (c < c1) CMs[c] = *lds_f2(mem_addr(a, t, lane));
+        }
     }
     if (lane == 0) {
+        if (a.oop) a.par[g] = (uint8_t)q;
         a.act[g] = (uint8_t)act;
         a.sat_step[g] = sat;
         a.steps_done[g] = done;
@@ -324,13 +330,8 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
 }
 
 template <int TR> hipError_t launch_t(const Args &a, int G, size_t lds, hipStream_t stream) {
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_onchip<TR>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_MAX);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    hipError_t e = odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_onchip<TR>), (int)LDS_MAX);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_onchip<TR>), dim3((unsigned)G), dim3(NTH), lds, stream, a);
     return hipGetLastError();
 }

@@ -53,12 +53,13 @@ struct Args {
     const int32_t *tc;   // [ntiles + 1] first internal clause of each tile (constant memory reads)
     float *v0, *v1;      // voltages, [B][n] (par selects the buffer holding the current state)
     float *c0, *c1;      // clause memories, [B][m][2] (xs, xl), internal clause order
-    const uint8_t *par;  // [B]
+    uint8_t *par;        // [B] (flipped by an out-of-place launch)
     uint8_t *act;        // [B] replica still stepping
     int64_t *sat_step, *steps_done;
     int32_t *stop;       // first stop step (STOP_ANY), INT_MAX = none
     int32_t n, m, ntiles, tl;  // tiles [0, TR) live in VGPRs, [TR, TR + tl) in LDS
     int32_t step0, nsteps, stop_mode;
+    int32_t oop;         // 1: write the final state to the other buffer and flip par (replayable launch)
     float dt, xl_max;
     Lds lds;
 };

@@ -36,7 +36,7 @@ template <typename T> struct RArgs {
     const int32_t *__restrict__ lits;  // [L] literals by internal slot
     const int32_t *__restrict__ tc;    // [ntiles+1] first internal clause of each tile
     T *v0, *v1, *c0, *c1;              // state buffers, group layout with W == R
-    const uint8_t *par;
+    uint8_t *par;                      // flipped by an out-of-place launch
     T *cf, *ch;                        // adaptive scratch memories (full step, first half)
     T *dtr;
     uint8_t *act;
@@ -44,6 +44,8 @@ template <typename T> struct RArgs {
     int32_t *stop;
     int32_t n, m, ntiles;
     int32_t step0, nsteps, stop_mode;
+    int32_t oop;  // fixed steps: the first step reads the par buffer and writes the other one (the
+                  // launch's starting state survives for a STOP_ANY replay), then par flips
     T dt, zeta, xl_max;
     double tol;
 };
@@ -91,15 +93,20 @@ __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> 
 }
 
 // Memory update of one clause (system.rs:84-85, 94-95 / :124-132); returns the max_error terms.
+// copy: a fixed step written out of place -- a replica that does not step copies its memories.
 template <typename T, int R, int PK>
 __device__ __forceinline__ T res_mem_update(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, uint32_t ci, T C,
-                                            const Vec<T, 2> &mem, const Vec<T, 2> &full, bool on, T h) {
+                                            const Vec<T, 2> &mem, const Vec<T, 2> &full, bool on, T h,
+                                            bool copy) {
     const T one = (T)1.0, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
     const T xs_m = mem.e[0], xl_m = mem.e[1];
     const T dxs = (T)20.0 * (xs_m + eps) * (C - (T)0.25);  // :84
     const T dxl = (T)5.0 * (C - (T)0.05);                  // :85
     T e = (T)0.0;
-    if (!on) return e;
+    if (!on) {
+        if (PK == P_FIXED && copy) stv<T, 2>(at(CM, ci), mem);
+        return e;
+    }
     if (PK == P_FIXED) {
         Vec<T, 2> o;
         o.e[0] = dmin(dmax(xs_m + h * dxs, eps), xs_hi);
@@ -137,7 +144,8 @@ template <typename T> struct Pend {
 // the dv updates.
 template <typename T, int R, int PK>
 __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t,
-                                            const TileLoad<T> &ld, Pend<T> &P, bool on, T h, bool &uns, T &e) {
+                                            const TileLoad<T> &ld, Pend<T> &P, bool on, T h, bool &uns, T &e,
+                                            bool copy) {
     P.ok = ld.ok;
     if (!ld.ok) return;
     const T one = (T)1.0, halfc = (T)0.5;
@@ -172,7 +180,7 @@ __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R
         }
     }
     if (PK != P_ADA2) uns = uns || (on && !(C < (T)0.25));  // :88
-    e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, (uint32_t)(c * R + x.r) * 2u, C, ld.mem, ld.full, on, h));
+    e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, (uint32_t)(c * R + x.r) * 2u, C, ld.mem, ld.full, on, h, copy));
 }
 
 // :80 for one clause: dv[i_j] += d_j for j = 0, 1, 2 in order.  The three reads are issued
@@ -192,14 +200,14 @@ template <typename T, int R> __device__ __forceinline__ void res_apply3(const Re
 
 // Tile t, any clause width (empty clauses included); loads issued here.
 template <typename T, int R, int PK>
-__device__ __forceinline__ void res_clause_any(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t, bool on,
-                                               T h, bool &uns, T &e) {
+__device__ __forceinline__ void res_clause_any(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, int t,
+                                               bool on, T h, bool &uns, T &e) {
     const T one = (T)1.0, halfc = (T)0.5;
     const int c = ldc(a.tc, t) + x.lc;
     if (c >= ldc(a.tc, t + 1)) return;
     const int s0 = a.cptr[c], s1 = a.cptr[c + 1];
     const uint32_t ci = (uint32_t)(c * R + x.r) * 2u;
-    const Vec<T, 2> mem = ldv<T, 2>((PK == P_ADA2 ? x.ch : CM) + ci);
+    const Vec<T, 2> mem = ldv<T, 2>((PK == P_ADA2 ? x.ch : CMr) + ci);
     Vec<T, 2> full{};
     if (PK == P_ADA2) full = ldv<T, 2>(x.cf + ci);
     T mn = inf_v<T>(), sec = inf_v<T>();
@@ -222,27 +230,27 @@ __device__ __forceinline__ void res_clause_any(const RArgs<T> &a, const ResCtx<T
         x.dvL[idx] += tt * g_ + tr * r_;
     }
     if (PK != P_ADA2) uns = uns || (on && !(C < (T)0.25));
-    e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, ci, C, mem, full, on, h));
+    e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, ci, C, mem, full, on, h, CMr != CM));
 }
 
 // One step of the 3-SAT tile pipeline: the terms of tile t+1 are computed from slot S (which is
 // then refilled with tile t+1+RES_DEPTH), tile t's terms P are applied to dv, barrier (tile t+1
 // may touch the same dv entries).
 template <typename T, int R, int PK>
-__device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t, TileLoad<T> &S,
-                                          Pend<T> &P, bool on, T h, bool &uns, T &e) {
+__device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, int t,
+                                          TileLoad<T> &S, Pend<T> &P, bool on, T h, bool &uns, T &e) {
     Pend<T> Q;
-    res_clause3<T, R, PK>(a, x, CM, t + 1, S, Q, on, h, uns, e);  // Q.ok = false past the last tile
+    res_clause3<T, R, PK>(a, x, CM, t + 1, S, Q, on, h, uns, e, CMr != CM);  // Q.ok = false past the last tile
     res_apply3<T, R>(x, P);
-    res_load3<T, R, PK>(a, x, CM, t + 1 + RES_DEPTH, S);
+    res_load3<T, R, PK>(a, x, CMr, t + 1 + RES_DEPTH, S);
     __syncthreads();
     P = Q;
 }
 
-// One RHS pass over all tiles: dv (LDS) accumulates; memories are read from the pass's source and
-// written by kind.  Ends with a barrier (dv complete).
+// One RHS pass over all tiles: dv (LDS) accumulates; memories are read from CMr (or the adaptive
+// scratch) and written by kind (P_FIXED: to CM).  Ends with a barrier (dv complete).
 template <typename T, int R, int PK, bool K3>
-__device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, bool on, T h,
+__device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, bool on, T h,
                                          bool &uns, T &e) {
     const int NT_ = a.ntiles;
     if constexpr (K3) {
@@ -255,21 +263,21 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
         }
         TileLoad<T> b0, b1, b2, b3;
         Pend<T> P;
-        res_load3<T, R, PK>(a, x, CM, 0, b0);
-        res_load3<T, R, PK>(a, x, CM, 1, b1);
-        res_load3<T, R, PK>(a, x, CM, 2, b2);
-        res_load3<T, R, PK>(a, x, CM, 3, b3);
-        res_clause3<T, R, PK>(a, x, CM, 0, b0, P, on, h, uns, e);
-        res_load3<T, R, PK>(a, x, CM, RES_DEPTH, b0);
+        res_load3<T, R, PK>(a, x, CMr, 0, b0);
+        res_load3<T, R, PK>(a, x, CMr, 1, b1);
+        res_load3<T, R, PK>(a, x, CMr, 2, b2);
+        res_load3<T, R, PK>(a, x, CMr, 3, b3);
+        res_clause3<T, R, PK>(a, x, CM, 0, b0, P, on, h, uns, e, CMr != CM);
+        res_load3<T, R, PK>(a, x, CMr, RES_DEPTH, b0);
         for (int t0 = 0; t0 < NT_; t0 += 4) {  // iteration t computes tile t+1 from slot (t+1) % 4
-            res_iter3<T, R, PK>(a, x, CM, t0, b1, P, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CM, t0 + 1, b2, P, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CM, t0 + 2, b3, P, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CM, t0 + 3, b0, P, on, h, uns, e);
+            res_iter3<T, R, PK>(a, x, CMr, CM, t0, b1, P, on, h, uns, e);
+            res_iter3<T, R, PK>(a, x, CMr, CM, t0 + 1, b2, P, on, h, uns, e);
+            res_iter3<T, R, PK>(a, x, CMr, CM, t0 + 2, b3, P, on, h, uns, e);
+            res_iter3<T, R, PK>(a, x, CMr, CM, t0 + 3, b0, P, on, h, uns, e);
         }
     } else {
         for (int t = 0; t < NT_; ++t) {
-            res_clause_any<T, R, PK>(a, x, CM, t, on, h, uns, e);
+            res_clause_any<T, R, PK>(a, x, CMr, CM, t, on, h, uns, e);
             __syncthreads();
         }
     }
@@ -299,8 +307,11 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     x.dvL = x.vL + nR;
     x.vfL = x.dvL + nR;
     const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;  // uniform: SGPR bases
+    const bool oop = !ADAPTIVE && a.oop;
     T *V = (p ? a.v1 : a.v0) + (size_t)g * nR;
     T *CM = (p ? a.c1 : a.c0) + (size_t)g * a.m * R * 2;
+    T *CMo = oop ? (p ? a.c0 : a.c1) + (size_t)g * a.m * R * 2 : CM;  // written (out of place: the other buffer)
+    const T *CMr = CM;  // read: the launch's first step reads the starting state
     x.cf = ADAPTIVE ? a.cf + (size_t)g * a.m * R * 2 : nullptr;
     x.ch = ADAPTIVE ? a.ch + (size_t)g * a.m * R * 2 : nullptr;
     // per-replica bookkeeping (k_status's job in the other algorithms) lives in thread r < R
@@ -336,7 +347,8 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
         bool uns = false;
         T e = (T)0.0;
         if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154)
-            res_pass<T, R, P_FIXED, K3>(a, x, CM, on, h, uns, e);
+            res_pass<T, R, P_FIXED, K3>(a, x, CMr, CMo, on, h, uns, e);
+            CMr = CMo;
             if (uns) unsL[x.r] = 1u;
             for (int i = x.lc; i < a.n; i += NL) {  // :96, dv restarts at 0 (:33)
                 const int idx = i * R + x.r;
@@ -354,7 +366,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
                 }
             }
         } else {  // euler_step (system.rs:111-139), per-replica dt
-            res_pass<T, R, P_ADA1, K3>(a, x, CM, on, h, uns, e);
+            res_pass<T, R, P_ADA1, K3>(a, x, CM, CM, on, h, uns, e);
             if (uns) unsL[x.r] = 1u;
             __syncthreads();
             const bool st = on && unsL[x.r] != 0u;  // allsat replicas take no step (:122)
@@ -375,7 +387,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
             for (int j = 0; j < R; ++j) any_st = any_st || (actL[j] != 0 && unsL[j] != 0u);
             if (any_st) {  // uniform
                 bool u2 = false;
-                res_pass<T, R, P_ADA2, K3>(a, x, CM, st, h, u2, e);
+                res_pass<T, R, P_ADA2, K3>(a, x, CM, CM, st, h, u2, e);
                 for (int i = x.lc; i < a.n; i += NL) {
                     const int idx = i * R + x.r;
                     const T d = x.dvL[idx];
@@ -413,7 +425,12 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
         for (int j = 0; j < R; ++j) still = still || actL[j] != 0;
         if (!still) break;  // uniform
     }
-    for (size_t i = tid; i < nR; i += NTH) V[i] = x.vL[i];
+    T *Vo = oop ? (p ? a.v0 : a.v1) + (size_t)g * nR : V;
+    if (oop && CMr != CMo) {  // no step ran (every replica of the group stopped at once): carry the memories
+        for (size_t i = tid; i < (size_t)a.m * R * 2; i += NTH) CMo[i] = CM[i];
+    }
+    for (size_t i = tid; i < nR; i += NTH) Vo[i] = x.vL[i];
+    if (oop && tid == 0) a.par[g] = (uint8_t)!p;
     if (tid < R) {
         const int rg = g * R + tid;
         a.act[rg] = (uint8_t)act;

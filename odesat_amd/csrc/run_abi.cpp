@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -37,6 +38,15 @@ void to_replica_major(const float *src, int64_t items, int64_t B, std::vector<do
     dst.resize((size_t)(items * B));
     for (int64_t i = 0; i < items; ++i)
         for (int64_t b = 0; b < B; ++b) dst[(size_t)(b * items + i)] = (double)src[i * B + b];
+}
+
+// steps per bounded call of an unbounded run (ODESAT_RUN_CHUNK overrides: tests force several calls)
+int64_t chunk_steps() {
+    if (const char *ev = std::getenv("ODESAT_RUN_CHUNK")) {
+        const long long c = std::atoll(ev);
+        if (c > 0) return (int64_t)c;
+    }
+    return (int64_t)1 << 16;
 }
 
 void to_replica_inner(const std::vector<double> &src, int64_t items, int64_t B, float *dst) {
@@ -129,54 +139,27 @@ extern "C" int odesat_run(odesat_ctx *x, const odesat_params *p, int32_t B, cons
     to_replica_major(xl0, x->m, B, hxl);
     if ((rc = odesat_set_state(x->solver, 0, B, hv.data(), x->m ? hxs.data() : nullptr, x->m ? hxl.data() : nullptr)))
         return rc;
-    std::vector<int64_t> sat((size_t)B, -1), done((size_t)B, 0), s1((size_t)B), d1((size_t)B);
+    std::vector<int64_t> sat((size_t)B, -1), done((size_t)B, 0);
     odesat_params q = *p;
     if (p->max_steps > 0) {
         if ((rc = odesat_simulate(x->solver, &q, sat.data(), done.data(), nullptr, nullptr))) return rc;
-    }
-    std::vector<double> ov((size_t)(x->n * B)), oxs((size_t)(x->m * B)), oxl((size_t)(x->m * B));
-    if (p->max_steps == 0) {  // None (system.rs:198, :296): until every replica (EACH) / some replica (ANY) is allsat
-        // A simulate call restarts every replica, so a replica that stopped in an earlier chunk
-        // (EACH) would step on: its state is kept from the chunk it stopped in.
-        q.max_steps = 1 << 16;
-        std::vector<uint8_t> newly((size_t)B);
+    } else {  // None (system.rs:198, :296): until every replica (EACH) / some replica (ANY) is allsat,
+              // one run in bounded calls (odesat_simulate_continue keeps dt, frozen replicas, step count)
+        q.max_steps = chunk_steps();
+        if ((rc = odesat_simulate(x->solver, &q, sat.data(), done.data(), nullptr, nullptr))) return rc;
         for (;;) {
-            if ((rc = odesat_simulate(x->solver, &q, s1.data(), d1.data(), nullptr, nullptr))) return rc;
-            bool any = false, all = true, fresh = false;
+            bool any = false, all = true;
             for (int32_t b = 0; b < B; ++b) {
-                newly[b] = 0;
-                if (sat[b] < 0) {  // still running before this chunk
-                    if (s1[b] >= 0) {
-                        sat[b] = done[b] + s1[b];
-                        newly[b] = 1;
-                        fresh = true;
-                    }
-                    done[b] += d1[b];
-                }
                 any = any || sat[b] >= 0;
                 all = all && sat[b] >= 0;
             }
-            const bool finished = p->stop == ODESAT_STOP_ANY ? any : all;
-            if (fresh || finished) {  // keep the states of the replicas that stopped in this chunk
-                std::vector<double> cv((size_t)(x->n * B)), cxs((size_t)(x->m * B)), cxl((size_t)(x->m * B));
-                if ((rc = odesat_get_state(x->solver, 0, B, cv.data(), x->m ? cxs.data() : nullptr,
-                                           x->m ? cxl.data() : nullptr)))
-                    return rc;
-                for (int32_t b = 0; b < B; ++b) {
-                    // ANY: every replica stops at the chunk's first allsat step (simulate_inter)
-                    if (!newly[b] && !(p->stop == ODESAT_STOP_ANY && finished)) continue;
-                    const size_t vn = (size_t)x->n, cm = (size_t)x->m;
-                    std::copy(cv.begin() + b * vn, cv.begin() + (b + 1) * vn, ov.begin() + b * vn);
-                    std::copy(cxs.begin() + b * cm, cxs.begin() + (b + 1) * cm, oxs.begin() + b * cm);
-                    std::copy(cxl.begin() + b * cm, cxl.begin() + (b + 1) * cm, oxl.begin() + b * cm);
-                }
-            }
-            if (finished) break;
+            if (p->stop == ODESAT_STOP_ANY ? any : all) break;
+            if ((rc = odesat_simulate_continue(x->solver, &q, sat.data(), done.data(), nullptr, nullptr))) return rc;
         }
-    } else if ((rc = odesat_get_state(x->solver, 0, B, ov.data(), x->m ? oxs.data() : nullptr,
-                                      x->m ? oxl.data() : nullptr))) {
-        return rc;
     }
+    std::vector<double> ov((size_t)(x->n * B)), oxs((size_t)(x->m * B)), oxl((size_t)(x->m * B));
+    if ((rc = odesat_get_state(x->solver, 0, B, ov.data(), x->m ? oxs.data() : nullptr, x->m ? oxl.data() : nullptr)))
+        return rc;
     if (v_out) to_replica_inner(ov, x->n, B, v_out);
     if (xs_out) to_replica_inner(oxs, x->m, B, xs_out);
     if (xl_out) to_replica_inner(oxl, x->m, B, xl_out);

@@ -377,9 +377,10 @@ constexpr size_t STOCH_LDS_MAX = 160 * 1024 - 1024;
 size_t round16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // The wave kernel's width: the widest WPW in {8, 4, 2, 1} whose LDS fits and that still gives
-// every CU (256) a workgroup; 0 (3-kernel path) when one replica's state and the topology do not
-// fit.  ODESAT_STOCH_WAVE=0 forces the 3-kernel path, ODESAT_STOCH_WPW=w forces a width that fits.
-int stoch_wave_width(int64_t B, size_t topo, size_t rep) {
+// every CU of the device (`cus`) a workgroup; 0 (3-kernel path) when one replica's state and the
+// topology do not fit.  ODESAT_STOCH_WAVE=0 forces the 3-kernel path, ODESAT_STOCH_WPW=w forces a
+// width that fits.
+int stoch_wave_width(int64_t B, size_t topo, size_t rep, int cus) {
     const char *e = std::getenv("ODESAT_STOCH_WAVE");
     if (e && e[0] == '0') return 0;
     auto fits = [&](int w) { return topo + (size_t)w * rep <= STOCH_LDS_MAX; };
@@ -389,7 +390,7 @@ int stoch_wave_width(int64_t B, size_t topo, size_t rep) {
         if ((w == 1 || w == 2 || w == 4 || w == 8) && fits(w)) return w;
     }
     for (int w : {8, 4, 2}) {
-        if (fits(w) && (B + w - 1) / w >= 256) return w;
+        if (fits(w) && (B + w - 1) / w >= cus) return w;
     }
     return 1;
 }
@@ -504,7 +505,10 @@ extern "C" int odesat_stoch_create(int device, const odesat_cnf *f, int64_t batc
         topo.resize(s->topo_bytes / 4, 0);
         // xl[m] u64 | sat[m] | v[n] | flag[n] | (4-aligned) list[n] int32
         s->rep_bytes = round16((((size_t)9 * m + 2 * n + 3) & ~(size_t)3) + (size_t)4 * n);
-        s->wpw = stoch_wave_width(batch, s->topo_bytes, s->rep_bytes);
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+            cus = 256;
+        s->wpw = stoch_wave_width(batch, s->topo_bytes, s->rep_bytes, cus);
         if (s->wpw) {
             if ((rc = dalloc(&s->topo, topo.size()))) return bail(rc);
             if (hipMemcpy(s->topo, topo.data(), s->topo_bytes, hipMemcpyHostToDevice) != hipSuccess)

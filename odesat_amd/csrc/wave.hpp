@@ -31,7 +31,7 @@ template <typename T> struct WArgs {
     const int4 *__restrict__ tp4;     // [m] variable-major position of each literal's term
     const int32_t *__restrict__ vst;  // [n+1] variable -> first term position
     T *v0, *v1, *c0, *c1;             // state buffers, group width 1
-    const uint8_t *par;
+    uint8_t *par;                     // flipped by an out-of-place launch
     T *dtr;
     uint8_t *act;
     int64_t *sat_step, *steps_done;
@@ -39,6 +39,7 @@ template <typename T> struct WArgs {
     int32_t n, m, L, G;                 // G: replicas (groups of width 1)
     uint32_t topo_bytes, rep_bytes;     // LDS: the shared topology, then WPW replicas of rep_bytes
     int32_t step0, nsteps, stop_mode;
+    int32_t oop;  // 1: the final state goes to the other buffer and par flips (STOP_ANY replay)
     T dt, zeta, xl_max;
     double tol;
 };
@@ -221,9 +222,13 @@ __global__ __launch_bounds__(WAVE_NTH * WPW) void k_wave(WArgs<T> a) {
         if (!act) break;  // uniform per wave
     }
     wave_sync();
-    for (int i = l; i < a.n; i += WAVE_NTH) V[i] = vL[i];
-    for (int i = l; i < 2 * a.m; i += WAVE_NTH) CM[i] = cmL[i];
+    const bool q = a.oop ? !p : p;
+    T *Vo = (q ? a.v1 : a.v0) + (size_t)g * a.n;
+    T *CMo = (q ? a.c1 : a.c0) + (size_t)g * a.m * 2;
+    for (int i = l; i < a.n; i += WAVE_NTH) Vo[i] = vL[i];
+    for (int i = l; i < 2 * a.m; i += WAVE_NTH) CMo[i] = cmL[i];
     if (l == 0) {
+        if (a.oop) a.par[g] = (uint8_t)q;
         a.act[g] = (uint8_t)act;
         a.sat_step[g] = sat;
         a.steps_done[g] = done;

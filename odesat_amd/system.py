@@ -135,8 +135,10 @@ class Solver:
 
     # -- drivers -----------------------------------------------------------------------------------
     def simulate(self, *, adaptive=False, dt=0.01, tol=1e-3, zeta=None, max_steps=1000,
-                 stop=ODESAT_STOP_EACH, poll_interval=0):
-        """Returns dict(first_sat_step[B], steps_done[B], dt[B], steps_run)."""
+                 stop=ODESAT_STOP_EACH, poll_interval=0, resume=False):
+        """Returns dict(first_sat_step[B], steps_done[B], dt[B], steps_run).  resume=True continues
+        the previous run (odesat_simulate_continue): bookkeeping carries over, steps are numbered
+        from the run's start."""
         p = _lib.Params(1 if adaptive else 0, int(stop), float(tol), float(dt),
                         -1.0 if zeta is None else float(zeta), int(max_steps), int(poll_interval), 0)
         B = self.batch
@@ -144,12 +146,20 @@ class Solver:
         done = np.zeros(B, np.int64)
         dts = np.zeros(B, np.float64)
         run = C.c_int64(0)
-        check(lib().odesat_simulate(self._h, C.byref(p), _lib.i64ptr(sat), _lib.i64ptr(done), _lib.dptr(dts),
-                                    C.byref(run)))
+        fn = lib().odesat_simulate_continue if resume else lib().odesat_simulate
+        check(fn(self._h, C.byref(p), _lib.i64ptr(sat), _lib.i64ptr(done), _lib.dptr(dts), C.byref(run)))
         return {"first_sat_step": sat, "steps_done": done, "dt": dts, "steps_run": run.value}
 
     def synchronize(self):
         check(lib().odesat_synchronize(self._h))
+
+    def checkpoint(self):
+        """Device-side copy of every replica's state and bookkeeping (odesat_checkpoint)."""
+        check(lib().odesat_checkpoint(self._h))
+
+    def rollback(self):
+        """Back to the last checkpoint (odesat_rollback)."""
+        check(lib().odesat_rollback(self._h))
 
     def set_chunk_replicas(self, replicas: int):
         check(lib().odesat_set_chunk_replicas(self._h, int(replicas)))
@@ -252,11 +262,10 @@ def simulate(state: State, formula: CNFFormula, tolerance=None, step_size=None, 
         if steps is not None:
             if steps > 0:
                 s.simulate(max_steps=steps, **kw)
-        else:
-            while True:
-                r = s.simulate(max_steps=_UNBOUNDED_CHUNK, **kw)
-                if r["first_sat_step"][0] >= 0:
-                    break
+        else:  # one run in bounded calls: dt and the step count carry over (system.rs:198-234)
+            r = s.simulate(max_steps=_UNBOUNDED_CHUNK, **kw)
+            while r["first_sat_step"][0] < 0:
+                r = s.simulate(max_steps=_UNBOUNDED_CHUNK, resume=True, **kw)
         _load_back(s, state)
     return state.v > 0.0
 
@@ -272,10 +281,9 @@ def simulate_inter(states: list, formula: CNFFormula, tolerance=None, step_size=
         kw = dict(adaptive=step_size is None, dt=step_size or 0.01,
                   tol=1e-3 if tolerance is None else tolerance, zeta=learning_rate, stop=ODESAT_STOP_ANY)
         if steps is None:
-            while True:
-                r = s.simulate(max_steps=_UNBOUNDED_CHUNK, **kw)
-                if (r["first_sat_step"] >= 0).any():
-                    break
+            r = s.simulate(max_steps=_UNBOUNDED_CHUNK, **kw)
+            while not (r["first_sat_step"] >= 0).any():
+                r = s.simulate(max_steps=_UNBOUNDED_CHUNK, resume=True, **kw)
         elif steps > 0:
             r = s.simulate(max_steps=steps, **kw)
         else:

@@ -86,3 +86,16 @@ def init_voltages(seed: int, replica0: int, count: int, n: int) -> np.ndarray:
     i = np.arange(n, dtype=np.uint64)[None, :]
     h = hash3(seed, r, i)
     return (h >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0) * 2.0 - 1.0
+
+
+def planted_ksat(n: int, m: int, k: int = 3, seed: int = 1, plant_seed: int = 7):
+    """random_ksat(n, m, k, seed) made satisfiable by a planted assignment: every clause that the
+    assignment star (bool[n], star[i] = value of variable i+1; counter hash of plant_seed) falsifies
+    gets the sign of one literal (position chosen by the hash) flipped.  Returns (var, neg, star)."""
+    var, neg = random_ksat(n, m, k, seed)
+    star = (hash3(plant_seed, np.arange(n, dtype=np.uint64), np.uint64(0)) >> np.uint64(63)).astype(bool)
+    bad = np.flatnonzero(~(star[var - 1] != neg).any(axis=1))
+    j = (hash3(plant_seed, bad.astype(np.uint64), np.uint64(1)) % np.uint64(k)).astype(np.int64)
+    neg = neg.copy()
+    neg[bad, j] = ~neg[bad, j]
+    return var, neg, star

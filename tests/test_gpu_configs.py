@@ -1,0 +1,253 @@
+"""BASELINE.json's configs at their real sizes, on the GPU, against the oracle:
+
+  config 1  tests/easy.cnf, `odesat solve` (adaptive, tol 1e-3, -r 7): the CLI's assignment equals the
+            f64 oracle's run of the same preprocessed formula and initial state, driven through
+            several bounded calls (odesat_simulate_continue);
+  config 2  n=10k m=42k f32 at the bench's horizon (200 steps): the f32 GPU against the f64 oracle --
+            the north star's fp32 tolerance on (v, xs, xl) and the identical v > 0 assignment;
+  config 3  uf250-style n=250 m=1065 seed 2, adaptive, B=1024 (k_wave): replicas bit-exact vs oc32;
+  config 4  n=50k m=210k seed 3, B=1024 f32: replicas bit-exact vs oc32, every replica by property;
+            inter (STOP_ANY) on the planted variant: the winner and the stop step;
+  config 5  n=1M m=4.2M seed 4, one replica partitioned (VARIABLES world 2 bit-exact; CLAUSES world 1
+            bit-exact, world 2 within a stated tolerance) vs oc32's fixed steps.
+Subsets of replicas are checked bit for bit; the rest through size-independent properties (the
+clamp ranges of system.rs:94-96, finiteness)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle, init_voltages
+from odesat_amd import cnf
+from odesat_amd import workloads as wl
+from odesat_amd.system import ODESAT_STOP_ANY, ODESAT_STOP_EACH, ODESAT_STOP_NONE, Solver
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def same(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint64), b.view(np.uint64))
+
+
+def instance(name):
+    c = wl.CONFIGS[name]
+    var, neg = wl.random_ksat(c["n"], c["m"], 3, c["seed"])
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    return cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"]), (cp, v_, n_), c["n"], c["m"]
+
+
+def assert_in_range(v, xs, xl, m):
+    """system.rs:94-96 clamp ranges (f32 constants) and finiteness."""
+    assert np.isfinite(v).all() and np.isfinite(xs).all() and np.isfinite(xl).all()
+    assert v.min() >= -1 and v.max() <= 1
+    eps = np.float32(0.001)
+    assert xs.min() >= eps and xs.max() <= np.float32(1) - eps
+    assert xl.min() >= 1 and xl.max() <= np.float32(1e4) * np.float32(m)
+
+
+# ----------------------------------------------------------------------------------- config 4 ---
+def test_config4_full_size_subset_bitexact_and_properties():
+    f, (cp, v_, n_), n, m = instance("config4")
+    o = Oracle(cp, v_, n_, n, "f32")
+    B, K = 1024, 10
+    pick = [0, 511, 1023]
+    with Solver(f, B, "f32") as s:
+        s.init_state(42)
+        r = s.simulate(dt=0.01, max_steps=K, stop=ODESAT_STOP_NONE)
+        assert r["steps_run"] == K and np.all(r["steps_done"] == K)
+        states = {b: s.get_state(b, 1) for b in pick}
+        for r0 in range(0, B, 128):  # every replica, 128 at a time (0.5 GB of f64 per chunk)
+            assert_in_range(*s.get_state(r0, 128), m)
+    for b in pick:
+        ov = init_voltages(42, b, 1, n)[0].astype(np.float32)
+        oxs, oxl = o.init_short_term_memory(), np.ones(m, np.float32)
+        o.simulate(ov, oxs, oxl, dt=np.float32(0.01), steps=K, zeta=np.float32(0.001))
+        gv, gxs, gxl = states[b]
+        assert same(gv[0], ov) and same(gxs[0], oxs) and same(gxl[0], oxl)
+
+
+def test_config4_inter_winner_on_planted_instance():
+    """simulate_inter (system.rs:278-294, 353-358) at config 4's size.  The instance is config 4's
+    with a planted satisfying assignment x*.  Replica 700 starts at v = 0.6 x* (allsat at step 0:
+    every clause has a literal with q v = 0.6 > 0.5, C = 0.2 < 0.25), replica 300 at 0.49 x* (not:
+    C = 0.255), the rest random.  The lowest allsat index at the first allsat step is 700: every
+    replica takes exactly that one step (the fixed step updates after the check, :148-152)."""
+    c = wl.CONFIGS["config4"]
+    n, m = c["n"], c["m"]
+    var, neg, star = wl.planted_ksat(n, m, 3, c["seed"])
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    f = cnf.CNFFormula.from_arrays(cp, v_, n_, n)
+    o = Oracle(cp, v_, n_, n, "f32")
+    sgn = np.where(star, 1.0, -1.0)
+    B = 1024
+    xs0 = o.init_short_term_memory().astype(np.float64)
+    special = {300: 0.49 * sgn, 700: 0.6 * sgn}
+    with Solver(f, B, "f32") as s:
+        s.init_state(42)
+        for b, v in special.items():
+            s.set_state(v[None], xs0[None], np.ones((1, m)), r0=b)
+        r = s.simulate(dt=0.01, max_steps=64, stop=ODESAT_STOP_ANY, poll_interval=16)
+        pick = [0, 300, 700, 1023]
+        states = {b: s.get_state(b, 1) for b in pick}
+    sat = np.flatnonzero(r["first_sat_step"] >= 0)
+    assert list(sat) == [700] and r["first_sat_step"][700] == 0
+    assert np.all(r["steps_done"] == 1)
+    for b in pick:
+        ov = (special[b] if b in special else init_voltages(42, b, 1, n)[0]).astype(np.float32)
+        oxs, oxl = o.init_short_term_memory(), np.ones(m, np.float32)
+        allsat = o.euler_step_fixed(ov, oxs, oxl, np.float32(0.01), np.float32(0.001))
+        assert allsat == (b == 700)
+        gv, gxs, gxl = states[b]
+        assert same(gv[0], ov) and same(gxs[0], oxs) and same(gxl[0], oxl)
+
+
+# ----------------------------------------------------------------------------------- config 3 ---
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_config3_wave_kernel_vs_oracle(prec):
+    """Adaptive steps (tol 1e-3, dt0 0.01, per-replica dt), B = 1024, on k_wave (the default for
+    this size): replicas {0, 511, 1023} bit-exact against the oracle's simulate, sat steps included."""
+    from odesat_amd import _lib
+    f, (cp, v_, n_), n, m = instance("config3")
+    T = np.float32 if prec == "f32" else np.float64
+    o = Oracle(cp, v_, n_, n, prec)
+    B, K = 1024, 60
+    pick = [0, 511, 1023]
+    with Solver(f, B, prec) as s:
+        assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.group_width == 1  # k_wave
+        s.init_state(42)
+        r = s.simulate(adaptive=True, tol=1e-3, max_steps=K, stop=ODESAT_STOP_EACH, poll_interval=16)
+        states = {b: s.get_state(b, 1) for b in pick}
+    for b in pick:
+        ov = init_voltages(42, b, 1, n)[0].astype(T)
+        oxs, oxl = o.init_short_term_memory(), np.ones(m, T)
+        t, sat, _, h, _ = o.simulate(ov, oxs, oxl, tol=T(1e-3), steps=K, zeta=T(0.001))
+        assert r["steps_done"][b] == t and (r["first_sat_step"][b] >= 0) == sat
+        assert T(r["dt"][b]) == T(h)
+        gv, gxs, gxl = states[b]
+        assert same(gv[0], ov) and same(gxs[0], oxs) and same(gxl[0], oxl)
+
+
+# ----------------------------------------------------------------------------------- config 2 ---
+F32_TOL = 1e-4  # stated fp32 tolerance at the bench horizon (profiles/r02_f32_vs_f64_horizon.txt)
+
+
+def test_config2_f32_tracks_f64_reference_at_bench_horizon():
+    """The north star's bar for the fp32 path: (v, xs, xl) within a stated fp32 tolerance of the
+    reference's f64 trajectory and the SAME final boolean assignment (v > 0, system.rs:238), at the
+    bench's horizon (200 fixed steps, B = 1024; the driver's 20-step run is inside it).  Both start
+    from the f32-rounded initial voltages.  Measured horizon (oracle, same replicas): identical
+    assignments through 300 steps, the first differing variable near step 500, decorrelated by
+    ~1000 steps (chaotic divergence, ~x2 per 45 steps)."""
+    f, (cp, v_, n_), n, m = instance("config2")
+    o = Oracle(cp, v_, n_, n, "f64")
+    B, K = 1024, 200
+    pick = [0, 517, 1023]
+    with Solver(f, B, "f32") as s:
+        s.init_state(42)
+        s.simulate(dt=0.01, max_steps=K, stop=ODESAT_STOP_NONE, poll_interval=K)
+        states = {b: s.get_state(b, 1) for b in pick}
+    for b in pick:
+        ov = init_voltages(42, b, 1, n)[0].astype(np.float32).astype(np.float64)
+        oxs, oxl = o.init_short_term_memory(), np.ones(m)
+        o.simulate(ov, oxs, oxl, dt=0.01, steps=K, zeta=0.001)
+        gv, gxs, gxl = (x[0] for x in states[b])
+        assert np.max(np.abs(gv - ov)) <= F32_TOL
+        assert np.max(np.abs(gxs - oxs)) <= F32_TOL
+        assert np.max(np.abs(gxl - oxl) / oxl) <= F32_TOL
+        assert np.array_equal(gv > 0, ov > 0)
+
+
+# ----------------------------------------------------------------------------------- config 1 ---
+def test_config1_cli_solve_easy_adaptive_matches_oracle(tmp_path):
+    """`odesat solve -f easy.cnf` exactly as BASELINE states config 1 (adaptive step, tol 1e-3,
+    -r 7, the reference's f64), run unbounded in bounded calls of 64 steps (ODESAT_RUN_CHUNK) so the
+    continue path carries dt and the step count across calls: the printed assignment equals the f64
+    oracle's continuous run of the same preprocessed formula from the same initial state, mapped
+    back through the same trace, and satisfies the input."""
+    from odesat_amd import preprocess as pp
+    path = os.path.join(ROOT, "tests", "golden", "easy.cnf")
+    out = tmp_path / "easy.txt"
+    env = dict(os.environ, ODESAT_RUN_CHUNK="64")
+    binp = os.path.join(ROOT, "odesat_amd", "bin", "odesat")
+    r = subprocess.run([binp, "solve", "-f", path, "-o", str(out)], capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0, r.stderr
+    assert "Checking if solution vector satisfies formula: true" in r.stdout
+    got = {}
+    for line in out.read_text().strip().splitlines():
+        a, b = line.split()
+        got[int(a)] = b == "1"
+    text = open(path).read()
+    formula = cnf.parse_dimacs_format(text)
+    reduced, trace = pp.repeatedly_resolve_and_update(formula, 7.0)
+    mapping, norm = cnf.normalize_cnf_variables(reduced)
+    ncp, nvar, nneg = norm.arrays()
+    o = Oracle(ncp, nvar, nneg, norm.varnum, "f64")
+    v = init_voltages(42, 0, 1, norm.varnum)[0]
+    xs, xl = o.init_short_term_memory(), np.ones(norm.nclauses)
+    t, sat, assign, _, _ = o.simulate(v, xs, xl, tol=1e-3, steps=1 << 22, zeta=None)
+    assert sat and t > 64  # the run crossed several bounded calls
+    vals = cnf.map_values_by_indices(mapping, assign)
+    pp.calculate_trace(vals, trace, formula)
+    assert pp.evaluate_cnf_assign(vals, formula)
+    assert got == {k: bool(v) for k, v in vals.items()}
+
+
+# ----------------------------------------------------------------------------------- config 5 ---
+CLAUSES_TOL = 1e-5  # CLAUSES at world > 1 sums per-rank partial dv (reordered fold), max |dv| after 5 steps
+
+
+def test_config5_partitioned_full_size_vs_oracle():
+    """One replica of n = 1M, m = 4.2M over 2 ranks on the box's GPU (the exchange done in-process):
+    VARIABLES bit-exact, CLAUSES bit-exact at world 1 and within CLAUSES_TOL at world 2, against
+    oc32's fixed steps (system.rs:141-154), 5 steps of dt 0.01."""
+    import torch
+
+    from odesat_amd.partition import CLAUSES, VARIABLES, LocalComm, PartitionedSolver, default_zeta
+    c = wl.CONFIGS["config5"]
+    n, m = c["n"], c["m"]
+    var, neg = wl.random_ksat(n, m, 3, c["seed"])
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    del var, neg
+    o = Oracle(cp, v_, n_, n, "f32")
+    K, dt = 5, 0.01
+    zeta = default_zeta(n, m)
+    v0 = init_voltages(42, 0, 1, n)[0].astype(np.float32)
+    xs0 = o.init_short_term_memory()
+    v, xs, xl = v0.copy(), xs0.copy(), np.ones(m, np.float32)
+    for _ in range(K):
+        o.euler_step_fixed(v, xs, xl, np.float32(dt), np.float32(zeta))
+    for mode, world in ((VARIABLES, 2), (CLAUSES, 1), (CLAUSES, 2)):
+        parts = [PartitionedSolver(cp, v_, n_, n, mode, comm=LocalComm(r, world)) for r in range(world)]
+        for p in parts:
+            p.set_state(v0, xs0, np.ones(m))
+        for _ in range(K):
+            for p in parts:
+                p.rhs(dt, zeta, False)
+            if mode == VARIABLES:
+                g = torch.cat([p.out for p in parts])
+                for p in parts:
+                    p.v.copy_(g)
+            else:
+                tot = torch.stack([p.out for p in parts]).sum(0)
+                for p in parts:
+                    p.out.copy_(tot)
+            for p in parts:
+                p.post(dt)
+        for p in parts:
+            st = p.status(False)
+            assert st["steps_done"] == K
+            gv, gxs, gxl, loc = p.get_state()
+            if mode == VARIABLES or world == 1:
+                assert np.array_equal(gv.astype(np.float32), v)
+                assert np.array_equal(gxs.astype(np.float32), xs[loc]) and np.array_equal(gxl.astype(np.float32), xl[loc])
+            else:
+                assert np.max(np.abs(gv - v)) <= CLAUSES_TOL
+                assert np.max(np.abs(gxs - xs[loc])) <= CLAUSES_TOL
+                assert np.max(np.abs(gxl - xl[loc]) / xl[loc]) <= CLAUSES_TOL
+            p.close()

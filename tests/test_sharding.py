@@ -11,7 +11,8 @@ import socket
 import numpy as np
 import pytest
 
-from odesat_amd.sharding import NO_SAT, global_first_sat, local_first_sat, max_over_ranks, shard_range
+from odesat_amd.sharding import (NO_SAT, global_first_sat, global_first_satisfied, local_first_sat, max_over_ranks,
+                                  min_over_ranks, shard_range)
 
 
 def test_shard_range_disjoint_cover():
@@ -30,6 +31,10 @@ def test_local_first_sat_tie_break():
     assert local_first_sat(np.array([7, 3, -1, 3]), 100) == (3, 101)  # earliest step, lowest index
     assert global_first_sat(None, np.array([5, 2]), 0) == (2, 1)
     assert max_over_ranks(None, 1.5) == 1.5
+    # batch's rule (main.rs:302-307): the lowest index that satisfies, whatever its sat step
+    assert global_first_satisfied(None, np.array([False, True, True]), 40) == 41
+    assert global_first_satisfied(None, np.zeros(3, bool), 0) == NO_SAT
+    assert min_over_ranks(None, 7) == 7
 
 
 def _free_port():
@@ -58,9 +63,14 @@ def _worker(rank, world, port, out, per, seed, steps):
     crafted = np.array([9, -1, -1, -1]) if rank == 0 else np.array([-1, 4, -1, 4])
     cw = global_first_sat(td, crafted, r0 if per == 4 else rank * 4)
     none = global_first_sat(td, np.full(3, -1), rank * 3)
+    # batch: rank 0 has no satisfying replica, rank 1 its replicas 2 and 3 -> global 4 + 2
+    bsat = np.zeros(4, bool) if rank == 0 else np.array([False, False, True, True])
+    bw = global_first_satisfied(td, bsat, rank * 4)
+    bnone = global_first_satisfied(td, np.zeros(2, bool), rank * 2)
     if rank == 0:
         with open(out, "w") as fh:
-            json.dump({"winner": winner, "wall": wall, "crafted": cw, "none": none}, fh)
+            json.dump({"winner": winner, "wall": wall, "crafted": cw, "none": none, "batch": bw, "batch_none": bnone},
+                      fh)
     td.destroy_process_group()
 
 
@@ -86,3 +96,18 @@ def test_two_rank_gloo_matches_single_process(tmp_path, seed):
     assert res["wall"] == 2.0
     assert tuple(res["crafted"]) == (4, 5)  # rank 1's replica 1 -> global 4 + 1
     assert tuple(res["none"]) == (NO_SAT, NO_SAT)
+    assert res["batch"] == 6 and res["batch_none"] == NO_SAT
+
+
+def test_bench_gpus_without_enough_devices_fails_loudly():
+    """`bench.py --gpus 2` starts the ranks itself, and refuses when fewer GPUs are visible (here: none)
+    instead of quietly timing one device."""
+    import subprocess
+    import sys
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("two GPUs are visible")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "GPU(s) are visible" in r.stderr
