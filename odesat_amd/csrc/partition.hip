@@ -28,6 +28,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <new>
 #include <string>
 #include <vector>
@@ -36,6 +37,16 @@
 #include "cnf.hpp"
 
 using odesat::fail;
+
+// Where the clause kernel puts a literal's term for the variable kernel (w):
+//   SLOT    at its literal slot (coalesced stores); the variable kernel gathers it at random;
+//   ELL     at its place in the variable kernel's sliced-ELL reads (scattered stores, coalesced reads);
+//   REGION  the local variables are cut into `regions` contiguous ranges and region r's terms are
+//           stored together, in slot order; the variable kernel folds region r on the blocks
+//           b % 8 == r % 8 (one XCD under round-robin placement), so every line of w is fetched into
+//           one XCD's L2 and its 16 terms are all read there -- the stores land in runs (a wave's 192
+//           terms fall into `regions` runs), the gathers hit L2.  Placement is speed, never results.
+enum { TERMS_SLOT = 0, TERMS_ELL = 1, TERMS_REGION = 2 };
 
 // Device bookkeeping of the replica (the partitioned analogue of act / sat_step / steps_done).
 struct PartStat {
@@ -49,6 +60,11 @@ struct odesat_part {
     int device = 0, world = 1;
     int64_t n = 0, m = 0, mloc = 0, L = 0, v0 = 0, v1 = 0, S = 0, voff = 0;
     int32_t *cptr = nullptr, *lits = nullptr, *cstart = nullptr, *deg = nullptr, *islot = nullptr;
+    int32_t *tpos = nullptr;  // ELL / REGION term layouts: slot -> the term's position in w
+    int terms = 0;            // TERMS_SLOT / TERMS_ELL / TERMS_REGION (odesat_part_create)
+    int regions = 0;          // TERMS_REGION: variable ranges, each folded on one XCD
+    int4 *lit4 = nullptr, *tpos4 = nullptr;  // every local clause has 3 literals: one record per clause
+    int xcd_ranges = 0;  // k_part_clause3 placement: 8 = clause range x on the blocks b with b % 8 == x
     float *xs = nullptr, *xl = nullptr, *w = nullptr;
     PartStat *stat = nullptr;
     int64_t bytes = 0;
@@ -80,12 +96,16 @@ __global__ void k_part_status(PartStat *st, const float *flags, int64_t stride, 
 }
 
 // Local clauses, one thread each: C (system.rs:43-60), each literal's term xl xs G + (1 + zeta xl)
-// (1 - xs) R into w[slot] (:62-80), the memory update (:84-85, :94-95) and the unsat flag (:88).
-// lits hold the voltage's index in v's layout (premapped on the host) << 1 | neg.
+// (1 - xs) R into w (:62-80), the memory update (:84-85, :94-95) and the unsat flag (:88).  lits hold
+// the voltage's index in v's layout (premapped on the host) << 1 | neg.  The term of slot s goes to
+// w[s] (SLOT layout: the variable kernel gathers it) or to w[tpos[s]] (ELL layout: its position in
+// the variable kernel's coalesced reads; slots of variables another rank folds go to sink words).
+template <bool ELL>
 __global__ __launch_bounds__(256) void k_part_clause(const int32_t *__restrict__ cptr, const int32_t *__restrict__ lits,
-                                                     const float *__restrict__ v, float *__restrict__ xs,
-                                                     float *__restrict__ xl, float *__restrict__ w, int32_t mloc, float dt,
-                                                     float zeta, float xl_max, float *__restrict__ unsat,
+                                                     const int32_t *__restrict__ tpos, const float *__restrict__ v,
+                                                     float *__restrict__ xs, float *__restrict__ xl,
+                                                     float *__restrict__ w, int32_t mloc, float dt, float zeta,
+                                                     float xl_max, float *__restrict__ unsat,
                                                      const PartStat *__restrict__ st) {
     if (st->frozen) return;  // uniform
     const int32_t c = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -111,7 +131,7 @@ __global__ __launch_bounds__(256) void k_part_clause(const int32_t *__restrict__
             const float val = one - q * vi;
             const float g = halfc * q * (val != mn ? mn : sec);
             const float r = (C == one - q * vi) ? halfc * (q - vi) : 0.0f;
-            w[s] = xl_m * xs_m * g + (one + zeta * xl_m) * (one - xs_m) * r;
+            w[ELL ? tpos[s] : s] = xl_m * xs_m * g + (one + zeta * xl_m) * (one - xs_m) * r;
         }
         const float dxs = 20.0f * (xs_m + 0.001f) * (C - 0.25f);  // :84
         const float dxl = 5.0f * (C - 0.05f);                      // :85
@@ -123,17 +143,100 @@ __global__ __launch_bounds__(256) void k_part_clause(const int32_t *__restrict__
     if (__syncthreads_or(uns) && threadIdx.x == 0 && *(volatile float *)unsat == 0.0f) *unsat = 1.0f;
 }
 
+// The same for a 3-SAT slice: one 16-byte literal record (and one term-position record) per clause, so
+// the three voltage gathers are independent loads in flight together (the generic loop above chains
+// each gather behind its literal's load and the min / second-min update).
+// The voltage table is gathered at random and should stay in the XCD's L2; the clause memories and
+// the terms stream past it once per step, so they are loaded / stored non-temporally.  XR = 8: the
+// (min-variable-sorted) clauses are cut into 8 equal ranges and range x runs on the blocks b with
+// b % 8 == x -- under the round-robin block placement one XCD -- so an XCD's gathers touch only the
+// voltages from its range's smallest variable up (placement is a speed choice, never correctness).
+template <bool ELL, int XR>
+__global__ __launch_bounds__(256) void k_part_clause3(const int4 *__restrict__ lit4, const int4 *__restrict__ tpos4,
+                                                      const float *__restrict__ v, float *__restrict__ xs,
+                                                      float *__restrict__ xl, float *__restrict__ w, int32_t mloc,
+                                                      float dt, float zeta, float xl_max, float *__restrict__ unsat,
+                                                      const PartStat *__restrict__ st) {
+    if (st->frozen) return;  // uniform
+    int32_t c, cend = mloc;
+    if (XR > 1) {
+        const int32_t chunk = (mloc + XR - 1) / XR, x = (int32_t)(blockIdx.x % XR);
+        c = x * chunk + (int32_t)(blockIdx.x / XR) * (int32_t)blockDim.x + (int32_t)threadIdx.x;
+        cend = min(mloc, (x + 1) * chunk);
+    } else {
+        c = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    }
+    bool uns = false;
+    if (c < cend) {
+        typedef int i4v __attribute__((ext_vector_type(4)));
+        const i4v l4 = __builtin_nontemporal_load(reinterpret_cast<const i4v *>(lit4) + c);
+        const int lit[3] = {l4[0], l4[1], l4[2]};
+        float vv[3], q[3], val[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) vv[j] = v[lit[j] >> 1];
+        const float xs_m = __builtin_nontemporal_load(&xs[c]), xl_m = __builtin_nontemporal_load(&xl[c]);
+        const float one = 1.0f, halfc = 0.5f;
+        float mn = __builtin_huge_valf(), sec = __builtin_huge_valf();
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {  // :43-57, strict <
+            q[j] = (lit[j] & 1) ? -1.0f : 1.0f;
+            val[j] = one - q[j] * vv[j];
+            const bool lt = val[j] < mn;
+            sec = lt ? mn : (val[j] < sec ? val[j] : sec);
+            mn = lt ? val[j] : mn;
+        }
+        const float C = halfc * mn;  // :60
+        float t[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {  // :62-80
+            const float g = halfc * q[j] * (val[j] != mn ? mn : sec);
+            const float r = (C == one - q[j] * vv[j]) ? halfc * (q[j] - vv[j]) : 0.0f;
+            t[j] = xl_m * xs_m * g + (one + zeta * xl_m) * (one - xs_m) * r;
+        }
+        if (ELL) {  // scattered: plain stores (non-temporal scattered stores measured 2x slower)
+            const i4v p4 = __builtin_nontemporal_load(reinterpret_cast<const i4v *>(tpos4) + c);
+            w[p4[0]] = t[0];
+            w[p4[1]] = t[1];
+            w[p4[2]] = t[2];
+        } else {
+            __builtin_nontemporal_store(t[0], &w[3 * c]);
+            __builtin_nontemporal_store(t[1], &w[3 * c + 1]);
+            __builtin_nontemporal_store(t[2], &w[3 * c + 2]);
+        }
+        const float dxs = 20.0f * (xs_m + 0.001f) * (C - 0.25f);  // :84
+        const float dxl = 5.0f * (C - 0.05f);                      // :85
+        __builtin_nontemporal_store(fminf(fmaxf(xs_m + dt * dxs, 0.001f), 1.0f - 0.001f), &xs[c]);  // :94
+        __builtin_nontemporal_store(fminf(fmaxf(xl_m + dt * dxl, one), xl_max), &xl[c]);            // :95
+        uns = !(C < 0.25f);                                                                          // :88
+    }
+    if (__syncthreads_or(uns) && threadIdx.x == 0 && *(volatile float *)unsat == 0.0f) *unsat = 1.0f;
+}
+
 // Variables [v0, v1), one thread each: dv = the fold of the local terms in clause order (:33, :80).
 // The incidences are sliced-ELL: chunk k of 64 variables stores its j-th incidences contiguously
-// ([chunk][j][64], padded to the chunk's largest degree), so the slot loads coalesce.
-// CLAUSES (apply == 0): out[i] = partial dv[i].  VARIABLES (apply == 1): out[i - v0] = the updated
-// voltage (:96), v[i + voff] being variable i in the gathered layout.
+// ([chunk][j][64], padded to the chunk's largest degree): SLOT layout reads the slot there and
+// gathers its term, ELL layout reads the term itself there (the clause kernel put it there), both
+// coalesced.  CLAUSES (apply == 0): out[i] = partial dv[i].  VARIABLES (apply == 1): out[i - v0] =
+// the updated voltage (:96), v[i + voff] being variable i in the gathered layout.
+// REGION (RG > 0 regions, a multiple of 8): block b runs region x + 8 g (x = b % 8) with bpr blocks
+// per region, so every region's variables are folded on one residue class of blockIdx mod 8.
+template <bool ELL, bool REGION>
 __global__ __launch_bounds__(256) void k_part_var(const int32_t *__restrict__ cstart, const int32_t *__restrict__ deg,
                                                   const int32_t *__restrict__ islot, const float *__restrict__ w,
                                                   const float *__restrict__ v, int32_t voff, int32_t v0, int32_t v1,
                                                   float dt, int apply, float *__restrict__ out,
-                                                  const PartStat *__restrict__ st) {
-    const int32_t k = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+                                                  const PartStat *__restrict__ st, int32_t RG, int32_t bpr) {
+    int32_t k;
+    if (REGION) {
+        const int32_t nv = v1 - v0, x = (int32_t)(blockIdx.x % 8), kk = (int32_t)(blockIdx.x / 8);
+        const int32_t r = x + 8 * (kk / bpr);
+        if (r >= RG) return;
+        const int32_t r0 = (int32_t)((int64_t)r * nv / RG), r1 = (int32_t)((int64_t)(r + 1) * nv / RG);
+        k = r0 + (kk % bpr) * (int32_t)blockDim.x + (int32_t)threadIdx.x;
+        if (k >= r1) return;
+    } else {
+        k = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    }
     const int32_t i = v0 + k;
     if (i >= v1) return;
     if (st->frozen) {  // the replica stopped: v is re-sent unchanged, no dv
@@ -141,10 +244,17 @@ __global__ __launch_bounds__(256) void k_part_var(const int32_t *__restrict__ cs
         else out[i] = 0.0f;
         return;
     }
-    const int32_t *p = islot + cstart[k >> 6] + (k & 63);
+    const int32_t base = cstart[k >> 6] + (k & 63);
     const int32_t d = deg[k];
     float dv = 0.0f;
-    for (int32_t j = 0; j < d; ++j) dv += w[p[64 * j]];
+    if (ELL) {
+        const float *q = w + base;
+#pragma unroll 4
+        for (int32_t j = 0; j < d; ++j) dv += q[64 * j];
+    } else {
+        const int32_t *p = islot + base;
+        for (int32_t j = 0; j < d; ++j) dv += w[p[64 * j]];
+    }
     if (apply) out[k] = fminf(fmaxf(v[i + voff] + dt * dv, -1.0f), 1.0f);
     else out[i] = dv;
 }
@@ -173,7 +283,7 @@ unsigned blocks_for(int64_t items) { return (unsigned)std::max<int64_t>(1, (item
 extern "C" void odesat_part_destroy(odesat_part *p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
-    void *ptrs[] = {p->cptr, p->lits, p->cstart, p->deg, p->islot, p->xs, p->xl, p->w, p->stat};
+    void *ptrs[] = {p->cptr, p->lits, p->cstart, p->deg, p->islot, p->xs, p->xl, p->w, p->stat, p->tpos, p->lit4, p->tpos4};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     delete p;
@@ -241,12 +351,73 @@ extern "C" int odesat_part_create(int device, int world, int64_t n, int64_t m, i
     for (int64_t k = 0; k < nv; ++k)
         for (int64_t j = 0; j < deg[k]; ++j) ell[cstart[k / 64] + 64 * j + (k % 64)] = inc_slot[var_ptr[k] + j];
     p->voff = block > 0 ? v0 / block : 0;
+    // term layout: REGION (default), ELL or SLOT (ODESAT_PART_TERMS=region|ell|slot)
+    p->terms = TERMS_REGION;
+    if (const char *tl = std::getenv("ODESAT_PART_TERMS")) {
+        const std::string t(tl);
+        p->terms = t == "slot" ? TERMS_SLOT : (t == "ell" ? TERMS_ELL : TERMS_REGION);
+    }
+    p->regions = 16;
+    if (const char *rg = std::getenv("ODESAT_PART_REGIONS")) p->regions = std::max(8, std::atoi(rg) / 8 * 8);
+    const int64_t ell_words = cstart[nchunk];
+    // w's size: SLOT L words, ELL the padded sliced-ELL, REGION the in-range incidences; + 64 sink words
+    const int64_t ninc_all = nv ? var_ptr[nv] : 0;
+    const int64_t wdata = p->terms == TERMS_SLOT ? L : (p->terms == TERMS_ELL ? ell_words : ninc_all);
+    std::vector<int64_t> tpos;
+    if (p->terms != TERMS_SLOT) {  // slot -> term position; slots of variables outside [v0, v1) -> sink words
+        tpos.assign((size_t)std::max<int64_t>(L, 1), 0);
+        for (int64_t sl = 0; sl < L; ++sl) tpos[sl] = wdata + (sl & 63);
+        if (p->terms == TERMS_ELL) {
+            for (int64_t k = 0; k < nv; ++k)
+                for (int64_t j = 0; j < deg[k]; ++j) tpos[inc_slot[var_ptr[k] + j]] = cstart[k / 64] + 64 * j + (k % 64);
+        } else {  // REGION: region r's terms together, in slot order
+            const int64_t RG = p->regions;
+            std::vector<int64_t> rcount((size_t)RG + 1, 0), slot_region((size_t)std::max<int64_t>(L, 1), -1);
+            for (int64_t k = 0; k < nv; ++k) {
+                const int64_t r = std::min(RG - 1, k * RG / nv);
+                // the range of region r is [r nv / RG, (r+1) nv / RG): k belongs to the r with r0 <= k < r1
+                int64_t rr = r;
+                while (rr > 0 && k < rr * nv / RG) --rr;
+                while (rr + 1 < RG && k >= (rr + 1) * nv / RG) ++rr;
+                for (int64_t j = 0; j < deg[k]; ++j) slot_region[inc_slot[var_ptr[k] + j]] = rr;
+                rcount[rr + 1] += deg[k];
+            }
+            for (int64_t r = 0; r < RG; ++r) rcount[r + 1] += rcount[r];
+            std::vector<int64_t> fill(rcount.begin(), rcount.end() - 1);
+            for (int64_t sl = 0; sl < L; ++sl)
+                if (slot_region[sl] >= 0) tpos[sl] = fill[slot_region[sl]]++;
+            for (int64_t q = 0; q < (int64_t)ell.size() && ell_words > 0; ++q) ell[q] = 0;
+            for (int64_t k = 0; k < nv; ++k)  // the variable kernel gathers its terms at these positions
+                for (int64_t j = 0; j < deg[k]; ++j) ell[cstart[k / 64] + 64 * j + (k % 64)] = tpos[inc_slot[var_ptr[k] + j]];
+        }
+    }
     int rc;
     if ((rc = upload(p, &p->cptr, cp.data(), mloc + 1)) || (rc = upload(p, &p->lits, lits.data(), L)) ||
         (rc = upload(p, &p->cstart, cstart.data(), nchunk + 1)) || (rc = upload(p, &p->deg, deg.data(), nv)) ||
-        (rc = upload(p, &p->islot, ell.data(), cstart[nchunk]))) {
+        (p->terms != TERMS_ELL && (rc = upload(p, &p->islot, ell.data(), ell_words))) ||
+        (p->terms != TERMS_SLOT && (rc = upload(p, &p->tpos, tpos.data(), L)))) {
         odesat_part_destroy(p);
         return rc;
+    }
+    bool k3 = mloc > 0 && L == 3 * mloc;
+    for (int64_t c = 0; c < mloc && k3; ++c) k3 = cp[c] == 3 * c;
+    if (const char *ev = std::getenv("ODESAT_PART_K3"))
+        if (std::atoi(ev) == 0) k3 = false;
+    if (const char *ev = std::getenv("ODESAT_PART_XCD")) p->xcd_ranges = std::atoi(ev) != 0 ? 8 : 0;
+    if (k3) {  // 3-SAT slice: 16-byte literal / term-position records per clause
+        std::vector<int4> l4((size_t)mloc), t4((size_t)mloc);
+        for (int64_t c = 0; c < mloc; ++c) {
+            l4[c] = make_int4((int)lits[3 * c], (int)lits[3 * c + 1], (int)lits[3 * c + 2], 0);
+            if (p->terms != TERMS_SLOT) t4[c] = make_int4((int)tpos[3 * c], (int)tpos[3 * c + 1], (int)tpos[3 * c + 2], 0);
+        }
+        if (hipMalloc((void **)&p->lit4, (size_t)mloc * 16) != hipSuccess ||
+            hipMemcpy(p->lit4, l4.data(), (size_t)mloc * 16, hipMemcpyHostToDevice) != hipSuccess ||
+            (p->terms != TERMS_SLOT && (hipMalloc((void **)&p->tpos4, (size_t)mloc * 16) != hipSuccess ||
+                              hipMemcpy(p->tpos4, t4.data(), (size_t)mloc * 16, hipMemcpyHostToDevice) != hipSuccess))) {
+            odesat_part_destroy(p);
+            return fail(ODESAT_ENOMEM, "hipMalloc failed");
+        }
+        p->bytes += mloc * (p->terms != TERMS_SLOT ? 32 : 16);
     }
     for (float **b : {&p->xs, &p->xl}) {
         if (hipMalloc((void **)b, std::max<size_t>(16, (size_t)mloc * 4)) != hipSuccess) {
@@ -267,11 +438,12 @@ extern "C" int odesat_part_create(int device, int world, int64_t n, int64_t m, i
             return fail(ODESAT_EDEVICE, "hipMemcpy failed");
         }
     }
-    if (hipMalloc((void **)&p->w, std::max<size_t>(16, (size_t)L * 4)) != hipSuccess) {
+    const int64_t wwords = wdata + 64;
+    if (hipMalloc((void **)&p->w, std::max<size_t>(16, (size_t)wwords * 4)) != hipSuccess) {
         odesat_part_destroy(p);
         return fail(ODESAT_ENOMEM, "hipMalloc failed");
     }
-    p->bytes += L * 4;
+    p->bytes += wwords * 4;
     *out = p;
     return ODESAT_OK;
 }
@@ -341,13 +513,44 @@ extern "C" int odesat_part_rhs(odesat_part *p, const float *v, float *out, doubl
     float *unsat = apply ? out + p->S : out + p->n;
     PART_TRY(hipMemsetAsync(unsat, 0, 4, st));
     const float xl_max = 1e4f * (float)p->m;  // system.rs:95, as the oracle's (T)1e4 * (T)m
-    if (p->mloc)
-        hipLaunchKernelGGL(k_part_clause, dim3(blocks_for(p->mloc)), dim3(256), 0, st, p->cptr, p->lits, v, p->xs,
-                           p->xl, p->w, (int32_t)p->mloc, (float)dt, (float)zeta, xl_max, unsat, p->stat);
+    if (p->mloc && p->lit4) {
+        const unsigned nb = p->xcd_ranges ? 8u * blocks_for((p->mloc + 7) / 8) : blocks_for(p->mloc);
+#define PART_C3(E, X)                                                                                         \
+    hipLaunchKernelGGL((k_part_clause3<E, X>), dim3(nb), dim3(256), 0, st, p->lit4, p->tpos4, v, p->xs, p->xl, p->w, \
+                       (int32_t)p->mloc, (float)dt, (float)zeta, xl_max, unsat, p->stat)
+        const bool scat = p->terms != TERMS_SLOT;
+        if (scat && p->xcd_ranges) PART_C3(true, 8);
+        else if (scat) PART_C3(true, 1);
+        else if (p->xcd_ranges) PART_C3(false, 8);
+        else PART_C3(false, 1);
+#undef PART_C3
+    } else if (p->mloc) {
+        if (p->terms != TERMS_SLOT)
+            hipLaunchKernelGGL(k_part_clause<true>, dim3(blocks_for(p->mloc)), dim3(256), 0, st, p->cptr, p->lits,
+                               p->tpos, v, p->xs, p->xl, p->w, (int32_t)p->mloc, (float)dt, (float)zeta, xl_max, unsat,
+                               p->stat);
+        else
+            hipLaunchKernelGGL(k_part_clause<false>, dim3(blocks_for(p->mloc)), dim3(256), 0, st, p->cptr, p->lits,
+                               p->tpos, v, p->xs, p->xl, p->w, (int32_t)p->mloc, (float)dt, (float)zeta, xl_max, unsat,
+                               p->stat);
+    }
     PART_TRY(hipGetLastError());
-    if (p->v1 > p->v0)
-        hipLaunchKernelGGL(k_part_var, dim3(blocks_for(p->v1 - p->v0)), dim3(256), 0, st, p->cstart, p->deg, p->islot,
-                           p->w, v, (int32_t)p->voff, (int32_t)p->v0, (int32_t)p->v1, (float)dt, apply, out, p->stat);
+    if (p->v1 > p->v0) {
+        const int64_t nv = p->v1 - p->v0;
+        const int32_t bpr = (int32_t)((nv / p->regions + 1 + 255) / 256);
+        if (p->terms == TERMS_ELL)
+            hipLaunchKernelGGL((k_part_var<true, false>), dim3(blocks_for(nv)), dim3(256), 0, st, p->cstart, p->deg,
+                               p->islot, p->w, v, (int32_t)p->voff, (int32_t)p->v0, (int32_t)p->v1, (float)dt, apply,
+                               out, p->stat, 0, 0);
+        else if (p->terms == TERMS_REGION)
+            hipLaunchKernelGGL((k_part_var<false, true>), dim3((unsigned)(p->regions * bpr)), dim3(256), 0, st,
+                               p->cstart, p->deg, p->islot, p->w, v, (int32_t)p->voff, (int32_t)p->v0, (int32_t)p->v1,
+                               (float)dt, apply, out, p->stat, (int32_t)p->regions, bpr);
+        else
+            hipLaunchKernelGGL((k_part_var<false, false>), dim3(blocks_for(nv)), dim3(256), 0, st, p->cstart, p->deg,
+                               p->islot, p->w, v, (int32_t)p->voff, (int32_t)p->v0, (int32_t)p->v1, (float)dt, apply,
+                               out, p->stat, 0, 0);
+    }
     PART_TRY(hipGetLastError());
     return ODESAT_OK;
 }

@@ -47,13 +47,16 @@ def default_zeta(n: int, m: int) -> float:
     return 0.1 if d >= 6.0 else (0.01 if d >= 4.9 else 0.001)
 
 
-def local_topology(cp, var, neg, n: int, mode: int, rank: int, world: int) -> dict:
+def local_topology(cp, var, neg, n: int, mode: int, rank: int, world: int, order: str = "minvar") -> dict:
     """Rank `rank`'s share of a normalised formula (clause_ptr cp[m+1], var[L], neg[L]).
 
-    Returns the local clauses (global indices, ascending = the reference's order), their CSR, the
-    variable range [v0, v1) this rank folds, and for each of those variables its local literal slots
-    in clause-then-literal order -- the order of the reference's dv accumulation (system.rs:35, :62,
-    :80)."""
+    Returns the local clauses (global indices) in the order the clause kernel processes them, their
+    CSR, the variable range [v0, v1) this rank folds, and for each of those variables its local
+    literal slots in the reference's clause-then-literal order -- the order of its dv accumulation
+    (system.rs:35, :62, :80), whatever the processing order.  order = "file" keeps the reference's
+    clause order; "minvar" (default) sorts the clauses by their smallest variable, so neighbouring
+    threads gather neighbouring voltages and write neighbouring terms (a random instance has no other
+    locality to offer)."""
     cp = np.asarray(cp, np.int64)
     var = np.asarray(var, np.int64)
     neg = np.asarray(neg, np.uint8)
@@ -74,6 +77,13 @@ def local_topology(cp, var, neg, n: int, mode: int, rank: int, world: int) -> di
         local = np.flatnonzero(touch).astype(np.int64)
     else:
         raise ValueError("mode must be CLAUSES or VARIABLES")
+    if order not in ("file", "minvar"):
+        raise ValueError("order must be 'file' or 'minvar'")
+    if order == "minvar" and len(local) and len(var):
+        owner = np.repeat(np.arange(m, dtype=np.int64), lens_all)
+        vmin = np.full(m, n, np.int64)
+        np.minimum.at(vmin, owner, var)
+        local = local[np.argsort(vmin[local], kind="stable")]
     lens = lens_all[local]
     lcp = np.zeros(len(local) + 1, np.int64)
     np.cumsum(lens, out=lcp[1:])
@@ -81,7 +91,7 @@ def local_topology(cp, var, neg, n: int, mode: int, rank: int, world: int) -> di
     gslot = np.repeat(cp[local], lens) + (np.arange(L, dtype=np.int64) - np.repeat(lcp[:-1], lens))
     lvar, lneg = var[gslot], neg[gslot]
     sel = np.flatnonzero((lvar >= v0) & (lvar < v1))
-    inc = sel[np.argsort(lvar[sel], kind="stable")]  # per variable: ascending slot = clause, literal order
+    inc = sel[np.lexsort((gslot[sel], lvar[sel]))]  # per variable: ascending global slot = clause, literal order
     counts = np.bincount(lvar[sel] - v0, minlength=v1 - v0)
     vptr = np.zeros(v1 - v0 + 1, np.int64)
     np.cumsum(counts, out=vptr[1:])
@@ -133,11 +143,12 @@ class LocalComm:
 class PartitionedSolver:
     """Rank `comm.rank`'s share of one replica of a normalised formula (f32), on `device`."""
 
-    def __init__(self, cp, var, neg, n: int, mode: int = VARIABLES, comm=None, device: int = 0):
+    def __init__(self, cp, var, neg, n: int, mode: int = VARIABLES, comm=None, device: int = 0,
+                 order: str = "minvar"):
         import torch
         self.comm = comm or LocalComm()
         self.mode, self.n = int(mode), int(n)
-        self.topo = t = local_topology(cp, var, neg, n, mode, self.comm.rank, self.comm.world)
+        self.topo = t = local_topology(cp, var, neg, n, mode, self.comm.rank, self.comm.world, order=order)
         self.m = t["m"]
         h = C.c_void_p()
         check(lib().odesat_part_create(int(device), self.comm.world, self.n, self.m, len(t["clauses"]),
@@ -235,12 +246,49 @@ class PartitionedSolver:
                                        apply, int(stop), self._stream(), C.byref(sd), C.byref(ss), C.byref(fr)))
         return {"steps_done": sd.value, "first_sat_step": ss.value, "frozen": bool(fr.value)}
 
+    def capturable(self) -> bool:
+        """A step can be captured into a HIP graph: world 1, or a device collective (RCCL)."""
+        return isinstance(self.comm, LocalComm) or not getattr(self.comm, "staged", True)
+
+    def graph(self, steps: int, dt: float, zeta: float, stop: bool = True):
+        """`steps` whole steps (RHS + memory update, the collective, the voltage update) captured into
+        one HIP graph (torch.cuda.CUDAGraph over the library's launches and the RCCL call): a replay
+        costs one host call instead of three per step."""
+        import torch
+        if not self.capturable():
+            raise ValueError("host-staged collectives (gloo) cannot be captured")
+        if not isinstance(self.comm, LocalComm):  # the communicator exists before the capture
+            if self.mode == VARIABLES:
+                self.comm.all_gather(torch.empty_like(self.v), torch.empty_like(self.out))
+            else:
+                self.comm.all_reduce_sum(torch.zeros_like(self.out))
+        torch.cuda.synchronize(self.dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(steps):
+                self.step(dt, zeta, stop)
+        return g
+
     def simulate(self, dt: float = 0.01, steps: int = 1000, zeta: float | None = None, stop: bool = True,
-                 poll: int = 32) -> dict:
+                 poll: int = 32, graph: bool | None = None) -> dict:
         """simulate (system.rs:190-203, fixed step): run until the first allsat step (that step's
         update included, :148-152) or `steps`; the stop condition is polled every `poll` steps
-        (exact regardless: a frozen replica does not step).  Returns status()."""
+        (exact regardless: a frozen replica does not step).  graph (default: when capturable) replays
+        `poll` steps per HIP graph launch.  Returns status()."""
         zeta = default_zeta(self.n, self.m) if zeta is None else zeta
+        if graph is None:
+            graph = self.capturable() and steps >= poll
+        if graph:
+            g = self.graph(poll, dt, zeta, stop)
+            k = 0
+            while k + poll <= steps:
+                g.replay()
+                k += poll
+                if stop and k < steps and self.status(stop)["frozen"]:
+                    return self.status(stop)
+            for _ in range(steps - k):
+                self.step(dt, zeta, stop)
+            return self.status(stop)
         for k in range(steps):
             self.step(dt, zeta, stop)
             if stop and (k + 1) % poll == 0 and k + 1 < steps and self.status(stop)["frozen"]:

@@ -30,6 +30,9 @@ def main():
     p.add_argument("--seed", type=int, default=7)
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--check-out", default=None)
+    p.add_argument("--order", default="minvar", choices=["file", "minvar"], help="clause processing order")
+    p.add_argument("--graph", type=int, default=50,
+                   help="steps per captured HIP graph (0 = one host call per kernel, the eager loop)")
     args = p.parse_args()
 
     import numpy as np
@@ -66,7 +69,7 @@ def main():
     mode = VARIABLES if args.mode == "variables" else CLAUSES
     comm = TorchComm(dist) if dist is not None else LocalComm()
     t0 = time.perf_counter()
-    s = PartitionedSolver(cp, var, neg, n, mode, comm=comm, device=device)
+    s = PartitionedSolver(cp, var, neg, n, mode, comm=comm, device=device, order=args.order)
     setup_s = time.perf_counter() - t0
     v0 = wl.init_voltages(args.seed, 0, 1, n)[0]
     # system.rs:361-372: +1 if the clause has a negated literal, else -1 (empty clauses too)
@@ -82,12 +85,21 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    graph = None
+    if args.graph and s.capturable():
+        if args.steps % args.graph:
+            raise SystemExit("--steps must be a multiple of --graph")
+        graph = s.graph(args.graph, args.dt, zeta, stop=False)  # captured, not run
     for _ in range(args.warmup):
         s.step(args.dt, zeta, stop=False)
     sync()
     t1 = time.perf_counter()
-    for _ in range(args.steps):
-        s.step(args.dt, zeta, stop=False)
+    if graph is not None:
+        for _ in range(args.steps // args.graph):
+            graph.replay()
+    else:
+        for _ in range(args.steps):
+            s.step(args.dt, zeta, stop=False)
     sync()
     wall = time.perf_counter() - t1
     if dist is not None:
@@ -108,7 +120,9 @@ def main():
             "value": args.steps / wall, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True,
             "scaling": "strong", "dtype": "fp32", "data": "synthetic: seeded random 3-SAT + counter-RNG voltages",
-            "config": {"workload": workload, "mode": args.mode,
+            "config": {"workload": workload, "mode": args.mode, "order": args.order,
+                       "terms": os.environ.get("ODESAT_PART_TERMS", "ell"),
+                       "graph_steps": args.graph if graph is not None else 0,
                        "collective": "all_gather" if mode == VARIABLES else "all_reduce",
                        "exchange_bytes_per_step": exchange, "local_clauses_rank0": int(len(t["clauses"])),
                        "setup_s": setup_s, "backend": dist.get_backend() if dist is not None else None},

@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU session producing a round's measurement evidence: PMC passes (separate --pmc runs, kernel
 # trace only) of the two persistent kernels at two launch sizes -> profiles/profile_<kernel>.json fits,
-# the bench line reading them, and the rocprofv3 kernel stats of the same bench command.  Each GPU
+# the bench line reading them, and the rocprofv3 kernel stats of the same bench command (its warmup
+# launch as long as the timed one, so the kernel's rocprof average is the timed launch's length).  Each GPU
 # step has its own time limit; any failure ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -37,7 +38,7 @@ grep '^{' "$OUT/bench.log" > "$OUT/bench.json"
 export TMPDIR=/tmp
 cd /tmp
 run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --output-format csv -- \
-    python3 "$ROOT/bench.py" --steps ${STEPS:-200} --warmup ${WARMUP:-50} --no-cpu --extra-batch 0 --no-inter \
+    python3 "$ROOT/bench.py" --steps ${STEPS:-200} --warmup ${STEPS:-200} --no-cpu --extra-batch 0 --no-inter \
     --profile-dir "$OUT/profile" || exit $?
 cd "$ROOT"
 find "$OUT/rocprof" -name '*kernel_stats.csv' -exec cat {} \;

@@ -45,15 +45,22 @@ def _global_incidences(cp, var, i):
 
 @pytest.mark.parametrize("name", ["rand200", "easy", "small"])
 @pytest.mark.parametrize("world", [1, 2, 3])
-def test_variables_topology_folds_exactly_the_reference_order(name, world):
+@pytest.mark.parametrize("order", ["file", "minvar"])
+def test_variables_topology_folds_exactly_the_reference_order(name, world, order):
+    """Whatever order the clause kernel processes the local clauses in, every variable's incidences
+    are listed in the reference's (clause, literal) order."""
     cp, var, neg, n = _arrays(name)
     m = len(cp) - 1
     seen = []
     for r in range(world):
-        t = local_topology(cp, var, neg, n, VARIABLES, r, world)
+        t = local_topology(cp, var, neg, n, VARIABLES, r, world, order=order)
         assert t["block"] == block_size(n, world) and t["v1"] - t["v0"] <= t["block"]
         loc = t["clauses"]
-        assert np.all(np.diff(loc) > 0)  # the reference's clause order
+        if order == "file":
+            assert np.all(np.diff(loc) > 0)  # the reference's clause order
+        else:  # ascending smallest variable
+            vmin = [int(var[cp[c]:cp[c + 1]].min()) if cp[c + 1] > cp[c] else n for c in loc]
+            assert vmin == sorted(vmin)
         touching = {c for c in range(m)
                     if np.any((var[cp[c]:cp[c + 1]] >= t["v0"]) & (var[cp[c]:cp[c + 1]] < t["v1"]))}
         assert set(loc.tolist()) == touching
@@ -79,7 +86,8 @@ def test_clauses_topology_partitions_the_clauses(world):
         t = local_topology(cp, var, neg, n, CLAUSES, r, world)
         assert (t["v0"], t["v1"], t["block"]) == (0, n, 0)
         assert t["var_ptr"][-1] == t["clause_ptr"][-1]  # every local literal is one incidence
-        allc.extend(t["clauses"].tolist())
+        assert sorted(t["clauses"].tolist()) == list(range(r * m // world, (r + 1) * m // world))
+        allc.extend(sorted(t["clauses"].tolist()))
     assert allc == list(range(m))
 
 
@@ -115,7 +123,7 @@ def _gloo_worker(rank, world, port, out, mode, steps, dt):
     from oracle.oracle import init_voltages
     cp, var, neg, n = _arrays("rand200")
     m = len(cp) - 1
-    t = local_topology(cp, var, neg, n, mode, rank, world)
+    t = local_topology(cp, var, neg, n, mode, rank, world, order="file")  # the emulation folds in local order
     T = np.float32
     v = init_voltages(7, 0, 1, n)[0].astype(T)
     xs = _xs0(cp, neg).astype(T)[t["clauses"]]
