@@ -731,11 +731,6 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
 int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zeta, int stop_mode, bool oop) {
     onchip::Args a{};
     a.oop = oop ? 1 : 0;
-    static const int prio = [] {
-        const char *ev = std::getenv("ODESAT_ONCHIP_PRIO");
-        return ev ? std::atoi(ev) : 0;
-    }();
-    a.prio = prio;
     a.rec = s->oc_rec;
     a.rec_bytes = (uint32_t)s->oc_rec_bytes;
     a.lds = onchip::lds_map(s->n);

@@ -255,8 +255,6 @@ __device__ __forceinline__ void mem_io(std::integer_sequence<int, Js...>, const 
 template <int TR>
 __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     const int g = blockIdx.x, lane = threadIdx.x;
-    if (a.prio == 1 && (lane >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
-    if (a.prio == 2 && (lane >> 6) < 4) __builtin_amdgcn_s_setprio(1);
     int act = a.act[g];
     if (!act) return;  // frozen replica (uniform)
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica

@@ -60,8 +60,6 @@ struct Args {
     int32_t n, m, ntiles, tl;  // tiles [0, TR) live in VGPRs, [TR, TR + tl) in LDS
     int32_t step0, nsteps, stop_mode;
     int32_t oop;         // 1: write the final state to the other buffer and flip par (replayable launch)
-    int32_t prio;        // wave priority experiment (ODESAT_ONCHIP_PRIO): 1 = waves 4-7 at s_setprio 1,
-                         // 2 = waves 0-3 (MI355X_MICROARCH.md, two waves per SIMD item 4)
     float dt, xl_max;
     Lds lds;
 };
