@@ -1,7 +1,7 @@
 """The `odesat` command line (odesat_amd/csrc/cli.cpp; the reference's src/main.rs:12-397).
 
-CPU: argument handling (clap's required flags, bad values, the out-of-scope stoch command) -- no
-solver is created on those paths.  GPU: solve / batch / inter / stoch end to end on small formulas, the
+CPU: argument handling (clap's required flags, bad values, stoch's restricted flags) -- no solver is
+created on those paths.  GPU: solve / batch / inter / stoch end to end on small formulas, the
 reported assignment re-checked on the host against the file's clauses."""
 import os
 import subprocess
