@@ -318,6 +318,22 @@ __device__ __forceinline__ void flush_flags(const KArgs<T> &a, int r0, const boo
     }
 }
 
+// dst[i] = src[i] for i = first, first + stride, ... < count (dst in LDS): U loads issued together, then
+// their U stores -- one memory round trip per U elements instead of one per element (a plain loop
+// waits for each load before its store).
+template <int U, typename T>
+__device__ __forceinline__ void copy_to_lds(T *dst, const T *src, int first, int count, int stride) {
+    if (count <= 0) return;
+    for (int i0 = first; i0 < count; i0 += stride * U) {
+        T x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = src[min(i0 + u * stride, count - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + u * stride < count) dst[i0 + u * stride] = x[u];
+    }
+}
+
 // strict-< min / second-min update (system.rs:50-55), branch-free
 template <typename T> __device__ __forceinline__ void minsec(T val, T &mn, T &sec) {
     const bool lt = val < mn;

@@ -237,15 +237,18 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
 
 typedef const __attribute__((address_space(4))) int32_t cint32;
 
-// Load (in) or store the register tiles' memories from / to the replica's clause memories.
+// Load (in) or store the register tiles' memories from / to the replica's clause memories.  The loads
+// are unconditional (an empty slot reads clause `mlast`'s memories, which nothing uses: its literals
+// point at the sink words, so its terms go to the dv sinks and its update is not stored), so the
+// compiler issues all of them back to back instead of one branch and one wait per tile.
 template <int TR, int... Js>
 __device__ __forceinline__ void mem_io(std::integer_sequence<int, Js...>, const cint32 *tc, int nt, float2 *CM,
-                                       float2 (&mr)[TR], int lane, bool in) {
+                                       float2 (&mr)[TR], int lane, bool in, int mlast) {
     auto one = [&](auto J) {
         constexpr int j = decltype(J)::value;
         const int c0 = tc[min(j, nt)], c1 = tc[min(j + 1, nt)];
         const int c = c0 + lane;
-        if (in) mr[j] = c < c1 ? CM[c] : make_float2(0.0f, 0.0f);
+        if (in) mr[j] = CM[min(c, mlast)];
         else if (c < c1) CM[c] = mr[j];
     };
     (one(std::integral_constant<int, Js>{}), ...);
@@ -269,16 +272,28 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     int64_t sat = a.sat_step[g], done = a.steps_done[g];
     const cint32 *tc = (const cint32 *)a.tc;
 
-    for (int i = lane; i < n2; i += NTH) {
-        lds_st(4u * i, i < a.n ? V[i] : 1.0f);
-        lds_st(4u * i + DVC, 0.0f);  // :33
+    {   // v (sinks = 1.0) into LDS, dv = 0 (:33): the loads of a pass issued together, then the stores
+        constexpr int U = 16;
+        for (int i0 = lane; i0 < n2; i0 += NTH * U) {
+            float x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = V[min(i0 + u * NTH, a.n - 1)];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * NTH;
+                if (i < n2) {
+                    lds_st(4u * i, i < a.n ? x[u] : 1.0f);
+                    lds_st(4u * i + DVC, 0.0f);
+                }
+            }
+        }
     }
+    const int mlast = a.m - 1;
     float2 mr[TR];
-    mem_io<TR>(std::make_integer_sequence<int, TR>{}, tc, a.ntiles, CM, mr, lane, true);
+    mem_io<TR>(std::make_integer_sequence<int, TR>{}, tc, a.ntiles, CM, mr, lane, true, mlast);
     for (int t = 0; t < a.tl; ++t) {
-        const int c0 = tc[min(TR + t, a.ntiles)], c1 = tc[min(TR + t + 1, a.ntiles)];
-        const int c = c0 + lane;
-        *lds_f2(mem_addr(a, t, lane)) = c < c1 ? CM[c] : make_float2(0.0f, 0.0f);
+        const int c0 = tc[min(TR + t, a.ntiles)];
+        *lds_f2(mem_addr(a, t, lane)) = CM[min(c0 + lane, mlast)];  // (empty slots: as mem_io)
     }
     if (lane < 2) lds_st(UNS + 4u * lane, 0.0f);
     __syncthreads();
@@ -314,7 +329,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         float2 *CMs = reinterpret_cast<float2 *>((q ? a.c1 : a.c0) + (size_t)g * a.m * 2);
         const cint32 *tcs = tc;
         asm volatile("" : "+s"(CMs), "+s"(tcs));
-        mem_io<TR>(std::make_integer_sequence<int, TR>{}, tcs, a.ntiles, CMs, mr, lane, false);
+        mem_io<TR>(std::make_integer_sequence<int, TR>{}, tcs, a.ntiles, CMs, mr, lane, false, 0);
         for (int t = 0; t < a.tl; ++t) {  // this lane's own LDS slots: no barrier needed
             const int c0 = tc[min(TR + t, a.ntiles)], c1 = tc[min(TR + t + 1, a.ntiles)];
             const int c = c0 + lane;

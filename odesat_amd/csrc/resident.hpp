@@ -335,10 +335,8 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
 #pragma unroll
     for (int j = 0; j < R; ++j) any = any || actL[j] != 0;
     if (skipL || !any) return;  // uniform
-    for (size_t i = tid; i < nR; i += NTH) {
-        x.vL[i] = V[i];
-        x.dvL[i] = (T)0.0;  // :33
-    }
+    copy_to_lds<8>(x.vL, V, tid, (int)nR, NTH);
+    for (size_t i = tid; i < nR; i += NTH) x.dvL[i] = (T)0.0;  // :33
     __syncthreads();
     for (int k = 0; k < a.nsteps; ++k) {
         const int step = a.step0 + k;

@@ -154,11 +154,9 @@ __global__ __launch_bounds__(WAVE_NTH * WPW) void k_wave(WArgs<T> a) {
     int4 *cl4 = reinterpret_cast<int4 *>(wave_smem);
     int4 *tp4 = cl4 + a.m;
     int32_t *vst = reinterpret_cast<int32_t *>(tp4 + a.m);
-    for (int i = threadIdx.x; i < a.m; i += WAVE_NTH * WPW) {
-        cl4[i] = a.cl4[i];
-        tp4[i] = a.tp4[i];
-    }
-    for (int i = threadIdx.x; i <= a.n; i += WAVE_NTH * WPW) vst[i] = a.vst[i];
+    copy_to_lds<8>(cl4, a.cl4, (int)threadIdx.x, a.m, WAVE_NTH * WPW);
+    copy_to_lds<8>(tp4, a.tp4, (int)threadIdx.x, a.m, WAVE_NTH * WPW);
+    copy_to_lds<8>(vst, a.vst, (int)threadIdx.x, a.n + 1, WAVE_NTH * WPW);
     __syncthreads();  // the workgroup's only barrier: from here on every wave is on its own
     if (g >= a.G) return;
     int act = a.act[g];
@@ -174,8 +172,8 @@ __global__ __launch_bounds__(WAVE_NTH * WPW) void k_wave(WArgs<T> a) {
     const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
     T *V = (p ? a.v1 : a.v0) + (size_t)g * a.n;
     T *CM = (p ? a.c1 : a.c0) + (size_t)g * a.m * 2;
-    for (int i = l; i < a.n; i += WAVE_NTH) vL[i] = V[i];
-    for (int i = l; i < 2 * a.m; i += WAVE_NTH) cmL[i] = CM[i];
+    copy_to_lds<8>(vL, V, l, a.n, WAVE_NTH);
+    copy_to_lds<8>(cmL, CM, l, 2 * a.m, WAVE_NTH);
     wave_sync();
     for (int k = 0; k < a.nsteps; ++k) {
         const int step = a.step0 + k;

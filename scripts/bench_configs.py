@@ -35,6 +35,8 @@ def main():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--alg", default="auto", help="auto | resident | fused | twopass | onchip")
     p.add_argument("--batch", type=int, default=0, help="override the config's B")
+    p.add_argument("--chunk", type=int, default=0, help="replicas per chunk (FUSED / TWOPASS; 0 = automatic)")
+    p.add_argument("--schedule", type=int, default=0, help="0 auto, 1 step-major, 2 chunk-major")
     args = p.parse_args()
 
     import numpy as np
@@ -56,6 +58,9 @@ def main():
         with Solver(f, B, "f32") as s:
             if args.alg != "auto":
                 s.set_algorithm(getattr(_lib, "ODESAT_ALG_" + args.alg.upper()))
+            if args.chunk:
+                s.set_chunk_replicas(args.chunk)
+            s.set_schedule(args.schedule)
             s.init_state(42)
             s.simulate(max_steps=args.warmup, **kw)
             s.synchronize()
@@ -69,7 +74,8 @@ def main():
         per_rs = (8 * n + 16 * m) * (3 if spec["adaptive"] else 1)
         out = {"config": cfg, "workload": f"random 3-SAT n={n} m={m} seed={c['seed']}, "
                                           f"{'adaptive tol 1e-3' if spec['adaptive'] else 'fixed dt 0.01'}",
-               "batch": B, "steps": args.steps, "algorithm": alg,
+               "batch": B, "steps": args.steps, "algorithm": alg, "chunk": args.chunk, "schedule": args.schedule,
+               "env": {k: v for k, v in os.environ.items() if k.startswith("ODESAT_")},
                "steps_per_s": args.steps / wall, "replica_steps_per_s": B * args.steps / wall,
                "ms_per_step": wall * 1e3 / args.steps,
                "algorithmic_bytes_per_replica_step": per_rs,

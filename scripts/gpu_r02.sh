@@ -11,3 +11,7 @@ tail -25 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 python bench.py --steps 20 --warmup 5 > gpurun_out/bench20.log 2>&1 || { tail -20 gpurun_out/bench20.log; exit 1; }
 tail -1 gpurun_out/bench20.log
+if [ "${LONG:-0}" = 1 ]; then
+    timeout -k 10 600 python bench.py --steps 200 --warmup 50 --no-cpu > gpurun_out/bench200.log 2>&1 || { tail -20 gpurun_out/bench200.log; exit 1; }
+    tail -1 gpurun_out/bench200.log
+fi
