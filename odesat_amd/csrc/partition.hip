@@ -63,7 +63,11 @@ struct odesat_part {
     int32_t *tpos = nullptr;  // ELL / REGION term layouts: slot -> the term's position in w
     int terms = 0;            // TERMS_SLOT / TERMS_ELL / TERMS_REGION (odesat_part_create)
     int regions = 0;          // TERMS_REGION: variable ranges, each folded on one XCD
-    int4 *lit4 = nullptr, *tpos4 = nullptr;  // every local clause has 3 literals: one record per clause
+    // every local clause has 3 literals: one literal record per clause (8 bytes, three 21-bit literals,
+    // when every literal is below 2^21, else 16 bytes) and its 3 term positions as 3 planes of mloc
+    void *lit3 = nullptr;
+    int32_t *tpos3 = nullptr;
+    bool lit_packed = false;
     int xcd_ranges = 0;  // k_part_clause3 placement: 8 = clause range x on the blocks b with b % 8 == x
     float *xs = nullptr, *xl = nullptr, *w = nullptr;
     PartStat *stat = nullptr;
@@ -143,16 +147,17 @@ __global__ __launch_bounds__(256) void k_part_clause(const int32_t *__restrict__
     if (__syncthreads_or(uns) && threadIdx.x == 0 && *(volatile float *)unsat == 0.0f) *unsat = 1.0f;
 }
 
-// The same for a 3-SAT slice: one 16-byte literal record (and one term-position record) per clause, so
-// the three voltage gathers are independent loads in flight together (the generic loop above chains
-// each gather behind its literal's load and the min / second-min update).
+// The same for a 3-SAT slice: one literal record per clause (PACK: 8 bytes, literal j in bits
+// [21j, 21j + 21); else 16 bytes) and three planes of term positions, so the three voltage gathers
+// are independent loads in flight together (the generic loop above chains each gather behind its
+// literal's load and the min / second-min update).
 // The voltage table is gathered at random and should stay in the XCD's L2; the clause memories and
 // the terms stream past it once per step, so they are loaded / stored non-temporally.  XR = 8: the
 // (min-variable-sorted) clauses are cut into 8 equal ranges and range x runs on the blocks b with
 // b % 8 == x -- under the round-robin block placement one XCD -- so an XCD's gathers touch only the
 // voltages from its range's smallest variable up (placement is a speed choice, never correctness).
-template <bool ELL, int XR>
-__global__ __launch_bounds__(256) void k_part_clause3(const int4 *__restrict__ lit4, const int4 *__restrict__ tpos4,
+template <bool ELL, int XR, bool PACK>
+__global__ __launch_bounds__(256) void k_part_clause3(const void *__restrict__ lit3, const int32_t *__restrict__ tpos3,
                                                       const float *__restrict__ v, float *__restrict__ xs,
                                                       float *__restrict__ xl, float *__restrict__ w, int32_t mloc,
                                                       float dt, float zeta, float xl_max, float *__restrict__ unsat,
@@ -168,9 +173,17 @@ __global__ __launch_bounds__(256) void k_part_clause3(const int4 *__restrict__ l
     }
     bool uns = false;
     if (c < cend) {
-        typedef int i4v __attribute__((ext_vector_type(4)));
-        const i4v l4 = __builtin_nontemporal_load(reinterpret_cast<const i4v *>(lit4) + c);
-        const int lit[3] = {l4[0], l4[1], l4[2]};
+        int lit[3];
+        if (PACK) {
+            const uint64_t r = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(lit3) + c);
+            lit[0] = (int)(r & 0x1FFFFF);
+            lit[1] = (int)((r >> 21) & 0x1FFFFF);
+            lit[2] = (int)(r >> 42);
+        } else {
+            typedef int i4v __attribute__((ext_vector_type(4)));
+            const i4v l4 = __builtin_nontemporal_load(reinterpret_cast<const i4v *>(lit3) + c);
+            lit[0] = l4[0], lit[1] = l4[1], lit[2] = l4[2];
+        }
         float vv[3], q[3], val[3];
 #pragma unroll
         for (int j = 0; j < 3; ++j) vv[j] = v[lit[j] >> 1];
@@ -194,10 +207,9 @@ __global__ __launch_bounds__(256) void k_part_clause3(const int4 *__restrict__ l
             t[j] = xl_m * xs_m * g + (one + zeta * xl_m) * (one - xs_m) * r;
         }
         if (ELL) {  // scattered: plain stores (non-temporal scattered stores measured 2x slower)
-            const i4v p4 = __builtin_nontemporal_load(reinterpret_cast<const i4v *>(tpos4) + c);
-            w[p4[0]] = t[0];
-            w[p4[1]] = t[1];
-            w[p4[2]] = t[2];
+            w[__builtin_nontemporal_load(&tpos3[c])] = t[0];
+            w[__builtin_nontemporal_load(&tpos3[mloc + c])] = t[1];
+            w[__builtin_nontemporal_load(&tpos3[2 * (int64_t)mloc + c])] = t[2];
         } else {
             __builtin_nontemporal_store(t[0], &w[3 * c]);
             __builtin_nontemporal_store(t[1], &w[3 * c + 1]);
@@ -252,8 +264,21 @@ __global__ __launch_bounds__(256) void k_part_var(const int32_t *__restrict__ cs
 #pragma unroll 4
         for (int32_t j = 0; j < d; ++j) dv += q[64 * j];
     } else {
+        // 8 incidences at a time: their positions, then their terms, are loaded together (clamped to
+        // the last one, so the loads are unconditional), then added in order -- the fold stays the
+        // reference's left fold; the loop trip count differs per lane, not the order of its adds
         const int32_t *p = islot + base;
-        for (int32_t j = 0; j < d; ++j) dv += w[p[64 * j]];
+        for (int32_t j0 = 0; j0 < d; j0 += 8) {
+            int32_t pos[8];
+            float t[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) pos[u] = p[64 * min(j0 + u, d - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) t[u] = w[pos[u]];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (j0 + u < d) dv += t[u];
+        }
     }
     if (apply) out[k] = fminf(fmaxf(v[i + voff] + dt * dv, -1.0f), 1.0f);
     else out[i] = dv;
@@ -283,7 +308,7 @@ unsigned blocks_for(int64_t items) { return (unsigned)std::max<int64_t>(1, (item
 extern "C" void odesat_part_destroy(odesat_part *p) {
     if (!p) return;
     (void)hipSetDevice(p->device);
-    void *ptrs[] = {p->cptr, p->lits, p->cstart, p->deg, p->islot, p->xs, p->xl, p->w, p->stat, p->tpos, p->lit4, p->tpos4};
+    void *ptrs[] = {p->cptr, p->lits, p->cstart, p->deg, p->islot, p->xs, p->xl, p->w, p->stat, p->tpos, p->lit3, p->tpos3};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     delete p;
@@ -404,20 +429,33 @@ extern "C" int odesat_part_create(int device, int world, int64_t n, int64_t m, i
     if (const char *ev = std::getenv("ODESAT_PART_K3"))
         if (std::atoi(ev) == 0) k3 = false;
     if (const char *ev = std::getenv("ODESAT_PART_XCD")) p->xcd_ranges = std::atoi(ev) != 0 ? 8 : 0;
-    if (k3) {  // 3-SAT slice: 16-byte literal / term-position records per clause
-        std::vector<int4> l4((size_t)mloc), t4((size_t)mloc);
+    if (k3) {  // 3-SAT slice: one literal record per clause, term positions in 3 planes
+        bool pack = true;
+        for (int64_t q = 0; q < L && pack; ++q) pack = lits[q] < (1 << 21);
+        if (const char *ev = std::getenv("ODESAT_PART_PACK"))
+            if (std::atoi(ev) == 0) pack = false;
+        p->lit_packed = pack;
+        const size_t rb = pack ? 8 : 16;
+        std::vector<uint64_t> l8(pack ? (size_t)mloc : 0);
+        std::vector<int4> l4(pack ? 0 : (size_t)mloc);
+        std::vector<int32_t> t3(p->terms != TERMS_SLOT ? 3 * (size_t)mloc : 0);
         for (int64_t c = 0; c < mloc; ++c) {
-            l4[c] = make_int4((int)lits[3 * c], (int)lits[3 * c + 1], (int)lits[3 * c + 2], 0);
-            if (p->terms != TERMS_SLOT) t4[c] = make_int4((int)tpos[3 * c], (int)tpos[3 * c + 1], (int)tpos[3 * c + 2], 0);
+            if (pack)
+                l8[c] = (uint64_t)lits[3 * c] | (uint64_t)lits[3 * c + 1] << 21 | (uint64_t)lits[3 * c + 2] << 42;
+            else
+                l4[c] = make_int4((int)lits[3 * c], (int)lits[3 * c + 1], (int)lits[3 * c + 2], 0);
+            if (!t3.empty())
+                for (int j = 0; j < 3; ++j) t3[j * mloc + c] = (int32_t)tpos[3 * c + j];
         }
-        if (hipMalloc((void **)&p->lit4, (size_t)mloc * 16) != hipSuccess ||
-            hipMemcpy(p->lit4, l4.data(), (size_t)mloc * 16, hipMemcpyHostToDevice) != hipSuccess ||
-            (p->terms != TERMS_SLOT && (hipMalloc((void **)&p->tpos4, (size_t)mloc * 16) != hipSuccess ||
-                              hipMemcpy(p->tpos4, t4.data(), (size_t)mloc * 16, hipMemcpyHostToDevice) != hipSuccess))) {
+        const void *src = pack ? (const void *)l8.data() : (const void *)l4.data();
+        if (hipMalloc(&p->lit3, (size_t)mloc * rb) != hipSuccess ||
+            hipMemcpy(p->lit3, src, (size_t)mloc * rb, hipMemcpyHostToDevice) != hipSuccess ||
+            (!t3.empty() && (hipMalloc((void **)&p->tpos3, t3.size() * 4) != hipSuccess ||
+                             hipMemcpy(p->tpos3, t3.data(), t3.size() * 4, hipMemcpyHostToDevice) != hipSuccess))) {
             odesat_part_destroy(p);
             return fail(ODESAT_ENOMEM, "hipMalloc failed");
         }
-        p->bytes += mloc * (p->terms != TERMS_SLOT ? 32 : 16);
+        p->bytes += mloc * (rb + t3.size() / std::max<int64_t>(mloc, 1) * 4);
     }
     for (float **b : {&p->xs, &p->xl}) {
         if (hipMalloc((void **)b, std::max<size_t>(16, (size_t)mloc * 4)) != hipSuccess) {
@@ -513,16 +551,20 @@ extern "C" int odesat_part_rhs(odesat_part *p, const float *v, float *out, doubl
     float *unsat = apply ? out + p->S : out + p->n;
     PART_TRY(hipMemsetAsync(unsat, 0, 4, st));
     const float xl_max = 1e4f * (float)p->m;  // system.rs:95, as the oracle's (T)1e4 * (T)m
-    if (p->mloc && p->lit4) {
+    if (p->mloc && p->lit3) {
         const unsigned nb = p->xcd_ranges ? 8u * blocks_for((p->mloc + 7) / 8) : blocks_for(p->mloc);
-#define PART_C3(E, X)                                                                                         \
-    hipLaunchKernelGGL((k_part_clause3<E, X>), dim3(nb), dim3(256), 0, st, p->lit4, p->tpos4, v, p->xs, p->xl, p->w, \
-                       (int32_t)p->mloc, (float)dt, (float)zeta, xl_max, unsat, p->stat)
+#define PART_C3(E, X, P)                                                                                      \
+    hipLaunchKernelGGL((k_part_clause3<E, X, P>), dim3(nb), dim3(256), 0, st, p->lit3, p->tpos3, v, p->xs, p->xl, \
+                       p->w, (int32_t)p->mloc, (float)dt, (float)zeta, xl_max, unsat, p->stat)
+#define PART_C3P(E, X)                  \
+    if (p->lit_packed) PART_C3(E, X, true); \
+    else PART_C3(E, X, false)
         const bool scat = p->terms != TERMS_SLOT;
-        if (scat && p->xcd_ranges) PART_C3(true, 8);
-        else if (scat) PART_C3(true, 1);
-        else if (p->xcd_ranges) PART_C3(false, 8);
-        else PART_C3(false, 1);
+        if (scat && p->xcd_ranges) { PART_C3P(true, 8); }
+        else if (scat) { PART_C3P(true, 1); }
+        else if (p->xcd_ranges) { PART_C3P(false, 8); }
+        else { PART_C3P(false, 1); }
+#undef PART_C3P
 #undef PART_C3
     } else if (p->mloc) {
         if (p->terms != TERMS_SLOT)

@@ -7,11 +7,11 @@ OUT=gpurun_out/part5; mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_partition.py tests/test_gpu_configs.py -k "partition or config5" -m gpu -x -q \
     --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 tail -2 $OUT/pytest.log
-for v in ${VARIANTS:-"variables minvar 0 slot 1 0 16" "variables minvar 0 region 1 0 16" "variables minvar 0 region 1 1 16" "variables file 0 region 1 0 16" "variables minvar 0 region 1 0 8" "variables minvar 0 region 1 0 32" "variables minvar 50 region 1 0 16" "clauses minvar 50 region 1 0 16"}; do
+for v in ${VARIANTS:-"variables minvar 0 region 1 0 16 1" "variables minvar 0 region 1 0 16 0" "clauses minvar 0 region 1 0 16 1"}; do
     set -- $v
-    ODESAT_PART_TERMS=$4 ODESAT_PART_K3=$5 ODESAT_PART_XCD=$6 ODESAT_PART_REGIONS=$7 timeout -k 10 300 python scripts/bench_partition.py --mode $1 --order $2 --graph $3 --steps 200 --warmup 20 \
+    ODESAT_PART_TERMS=$4 ODESAT_PART_K3=$5 ODESAT_PART_XCD=$6 ODESAT_PART_REGIONS=$7 ODESAT_PART_PACK=${8:-1} timeout -k 10 300 python scripts/bench_partition.py --mode $1 --order $2 --graph $3 --steps 200 --warmup 20 \
         >> $OUT/bench.jsonl 2> $OUT/err.log || { tail -20 $OUT/err.log; exit 1; }
-    tail -1 $OUT/bench.jsonl | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['config']['mode'], d['config']['order'], d['config']['terms'], 'k3=$5 xcd=$6 rg=$7', d['config']['graph_steps'], round(d['ms_per_step'],4))"
+    tail -1 $OUT/bench.jsonl | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print(d['config']['mode'], d['config']['order'], d['config']['terms'], 'k3=$5 xcd=$6 rg=$7 pack=${8:-1}', d['config']['graph_steps'], round(d['ms_per_step'],4))"
 done
 export TMPDIR=/tmp
 ROOT=$(pwd)

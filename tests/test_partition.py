@@ -256,6 +256,26 @@ def test_partition_kernels_match_oracle(name, mode, world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("env", [
+    {"ODESAT_PART_TERMS": "slot"}, {"ODESAT_PART_TERMS": "ell"}, {"ODESAT_PART_TERMS": "region"},
+    {"ODESAT_PART_PACK": "0"}, {"ODESAT_PART_K3": "0"}, {"ODESAT_PART_XCD": "1"},
+    {"ODESAT_PART_REGIONS": "24", "ODESAT_PART_PACK": "0"}])
+@pytest.mark.parametrize("mode,world", [(VARIABLES, 2), (CLAUSES, 1)])
+def test_partition_layouts_match_oracle(monkeypatch, env, mode, world):
+    """Every term layout / clause record / clause kernel / placement choice (read when a slice is
+    created) folds the same terms in the same order: the same bits as the oracle."""
+    for k, val in env.items():
+        monkeypatch.setenv(k, val)
+    steps, dt = 20, 0.05
+    _, (v, xs, xl), _, _ = _oracle_run("rand200", steps, dt)
+    sts, states = _run_parts("rand200", mode, world, steps, dt, stop=False)
+    for st, (gv, gxs, gxl, loc) in zip(sts, states):
+        assert st["steps_done"] == steps
+        assert np.array_equal(gv.astype(np.float32), v)
+        assert np.array_equal(gxs.astype(np.float32), xs[loc]) and np.array_equal(gxl.astype(np.float32), xl[loc])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode,world", [(VARIABLES, 2), (CLAUSES, 1)])
 def test_partition_stop_matches_simulate(mode, world):
     """easy.cnf is SAT: the replica freezes at simulate's stop step, polled every 7 steps."""
