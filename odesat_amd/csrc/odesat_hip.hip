@@ -65,7 +65,8 @@ struct odesat_solver {
     bool res_wave = false;    // RESIDENT as k_wave (wave.hpp): small 3-SAT, one wave per replica, variable fold
     int4 *wv_tp4 = nullptr;   // [m] k_wave: variable-major term position of each literal
     int32_t *wv_vst = nullptr;  // [n+1] k_wave: first term position of each variable
-    int wv_wpw = 1;             // k_wave: replicas (waves) per workgroup sharing the LDS topology
+    int wv_wpw = 1;             // k_wave: replicas per workgroup sharing the LDS topology
+    int wv_tw = 1;              // k_wave: waves per replica (2 when one per replica leaves SIMDs idle)
     bool res_ada = false; // adaptive steps fit in LDS too (else they run FUSED on the same layout)
     int res_ntiles = 0;
     int32_t *res_tc = nullptr, *cmap = nullptr;
@@ -617,15 +618,15 @@ int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     return ODESAT_OK;
 }
 
-template <typename T, bool ADA, int WPW> int launch_wave_k(odesat_solver *s, WArgs<T> a) {
+template <typename T, bool ADA, int WPW, int TW> int launch_wave_k(odesat_solver *s, WArgs<T> a) {
     a.topo_bytes = (uint32_t)wave_topo_bytes(s->n, s->m);
     a.rep_bytes = (uint32_t)wave_lds_bytes(s->n, s->m, s->L, sizeof(T), ADA);
     const size_t lds = a.topo_bytes + (size_t)WPW * a.rep_bytes;
-    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_wave<T, ADA, WPW>), (int)RES_LDS_MAX));
+    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_wave<T, ADA, WPW, TW>), (int)RES_LDS_MAX));
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_wave<T, ADA, WPW>), dim3((unsigned)((s->G + WPW - 1) / WPW)), dim3(WAVE_NTH * WPW), lds,
-                           s->stream, a);
+        hipLaunchKernelGGL((k_wave<T, ADA, WPW, TW>), dim3((unsigned)((s->G + WPW - 1) / WPW)),
+                           dim3(WAVE_NTH * WPW * TW), lds, s->stream, a);
     }
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
@@ -660,14 +661,25 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     a.xl_max = (T)1e4 * (T)s->m;  // system.rs:95
     a.tol = tol;
     a.G = s->G;
-    auto go = [&](auto ww) -> int {
-        constexpr int WPW = decltype(ww)::value;
-        return adaptive ? launch_wave_k<T, true, WPW>(s, a) : launch_wave_k<T, false, WPW>(s, a);
+    auto go = [&](auto ww, auto tw) -> int {
+        constexpr int WPW = decltype(ww)::value, TW = decltype(tw)::value;
+        return adaptive ? launch_wave_k<T, true, WPW, TW>(s, a) : launch_wave_k<T, false, WPW, TW>(s, a);
     };
-    switch (s->wv_wpw) {
-        case 4: return go(IC<4>{});
-        case 2: return go(IC<2>{});
-        default: return go(IC<1>{});
+    // (replicas per workgroup, waves per replica): at most 16 waves per workgroup
+    switch (s->wv_wpw * 100 + s->wv_tw) {
+        case 401: return go(IC<4>{}, IC<1>{});
+        case 402: return go(IC<4>{}, IC<2>{});
+        case 404: return go(IC<4>{}, IC<4>{});
+        case 201: return go(IC<2>{}, IC<1>{});
+        case 202: return go(IC<2>{}, IC<2>{});
+        case 204: return go(IC<2>{}, IC<4>{});
+        case 208: return go(IC<2>{}, IC<8>{});
+        case 101: return go(IC<1>{}, IC<1>{});
+        case 102: return go(IC<1>{}, IC<2>{});
+        case 104: return go(IC<1>{}, IC<4>{});
+        case 108: return go(IC<1>{}, IC<8>{});
+        case 116: return go(IC<1>{}, IC<16>{});
+        default: return fail(ODESAT_EINVAL, "k_wave shape not available");
     }
 }
 
@@ -1018,6 +1030,19 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         const size_t topo = wave_topo_bytes(n, m), rep = wave_lds_bytes(n, m, L, s->tsize, true);
         s->wv_wpw = topo + 4 * rep <= RES_LDS_MAX ? 4 : (topo + 2 * rep <= RES_LDS_MAX ? 2 : 1);
         s->res_wave = ev ? (std::atoi(ev) != 0 && topo + rep <= RES_LDS_MAX) : topo + 2 * rep <= RES_LDS_MAX;
+        // waves per replica: LDS holds one workgroup (wv_wpw replicas) per CU, so a replica of one
+        // wave leaves a lone wave on each SIMD, which issues a VALU instruction every 4 cycles.  A
+        // team of TW waves splits the replica's clauses and variables over 64 TW lanes: the workgroup
+        // fills 16 waves (4 per SIMD), fewer while the instance has under 32 clauses per wave.
+        // Measured (config 3, B = 1024, adaptive / fixed): 59 / 120 M replica-steps/s at TW = 1,
+        // 77 / 162 M at TW = 4; hard.cnf (m = 160) at B = 1: 36 / 17 ms per 10 000 steps at TW = 1,
+        // 26 / 14 ms at TW = 4.  ODESAT_WAVE_TEAM = 1/2/4/8/16 overrides (if the shape exists).
+        s->wv_tw = 16 / s->wv_wpw;
+        while (s->wv_tw > 1 && 32 * (int64_t)s->wv_tw > m) s->wv_tw /= 2;
+        if (const char *et = std::getenv("ODESAT_WAVE_TEAM")) {
+            const int t = std::atoi(et);
+            if ((t == 1 || t == 2 || t == 4 || t == 8 || t == 16) && t * s->wv_wpw <= 16) s->wv_tw = t;
+        }
     }
     if (s->res_wave) {
         res_r = lw = 1;

@@ -56,30 +56,60 @@ inline size_t wave_topo_bytes(int64_t n, int64_t m) { return ((size_t)m * 32 + (
 
 enum WPass : int { W_FIXED = 0, W_ADA1 = 1, W_ADA2 = 2 };
 
+// One clause's inputs, loaded ahead of its arithmetic.
+template <typename T> struct WClause {
+    int lit[3], pos[3];
+    T v[3], xs, xl, C1;
+};
+
 // Phase 1 over the replica's clauses.  Returns (wave-uniform) whether some clause is unsat (:88,
 // W_FIXED / W_ADA1) and raises e to the memories' max_error terms (W_ADA2).
-template <typename T, int PK>
+// Lane l of the replica's NL lanes takes clauses l, l + NL, ...  Software-pipelined: the records of
+// clause c + 2 NL and the voltages / memories of clause c + NL are loaded before clause c's
+// arithmetic and stores (nothing phase 1 stores is read by another
+// clause: terms, memories and C are per clause and v is constant), so one wave per SIMD keeps
+// three clauses' LDS reads in flight instead of waiting on each clause's dependent load chain.
+template <typename T, int PK, int NL>
 __device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *cl4, const int4 *tp4, const T *vL, T *tL,
                                              T *cmL, T *cL, int l, T h, T &e) {
     const T one = (T)1.0, halfc = (T)0.5, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
     bool uns = false;
-    for (int c = l; c < a.m; c += WAVE_NTH) {
-        const int4 l4 = cl4[c], p4 = tp4[c];
-        const int lit[3] = {l4.x, l4.y, l4.z}, pos[3] = {p4.x, p4.y, p4.z};
-        T v[3], q[3], val[3], d[3];
+    if (l >= a.m) return __any(uns);  // (NL > m: the lanes without a clause)
+    const int last = a.m - 1;
+    auto gather = [&](int c, const int4 &l4, const int4 &p4, WClause<T> &W) {  // clamped: always loadable
+        W.lit[0] = l4.x, W.lit[1] = l4.y, W.lit[2] = l4.z;
+        W.pos[0] = p4.x, W.pos[1] = p4.y, W.pos[2] = p4.z;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) W.v[j] = vL[W.lit[j] >> 1];
+        W.xs = cmL[2 * c];
+        W.xl = cmL[2 * c + 1];
+        if (PK == W_ADA2) W.C1 = cL[c];
+    };
+    int4 rl = cl4[min(l + NL, last)], rp = tp4[min(l + NL, last)];  // records of the next clause
+    WClause<T> W;
+    {
+        const int4 l4 = cl4[l], p4 = tp4[l];
+        gather(l, l4, p4, W);
+    }
+    for (int c = l; c < a.m; c += NL) {
+        const WClause<T> X = W;  // this clause
+        const int cn = min(c + NL, last);
+        gather(cn, rl, rp, W);   // the next clause's voltages and memories
+        rl = cl4[min(c + 2 * NL, last)];
+        rp = tp4[min(c + 2 * NL, last)];
+        T q[3], val[3], d[3];
         T mn = inf_v<T>(), sec = inf_v<T>();
 #pragma unroll
         for (int j = 0; j < 3; ++j) {  // :43-57
-            q[j] = (lit[j] & 1) ? (T)-1.0 : (T)1.0;
-            v[j] = vL[lit[j] >> 1];
-            val[j] = one - q[j] * v[j];
+            q[j] = (X.lit[j] & 1) ? (T)-1.0 : (T)1.0;
+            val[j] = one - q[j] * X.v[j];
             minsec(val[j], mn, sec);
         }
         const T C = halfc * mn;  // :60
-        T xs_m = cmL[2 * c], xl_m = cmL[2 * c + 1];
+        T xs_m = X.xs, xl_m = X.xl;
         T xs_f = xs_m, xl_f = xl_m;
         if (PK == W_ADA2) {  // y's memories -> the full-step clone and the first half step (:124-128)
-            const T C1 = cL[c], half = (T)0.5 * h;
+            const T C1 = X.C1, half = (T)0.5 * h;
             const T dxs1 = (T)20.0 * (xs_m + eps) * (C1 - (T)0.25);  // :84
             const T dxl1 = (T)5.0 * (C1 - (T)0.05);                  // :85
             xs_f = dmin(dmax(xs_m + h * dxs1, eps), xs_hi);
@@ -95,9 +125,9 @@ __device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *cl4,
         for (int j = 0; j < 3; ++j) d[j] = tt * (halfc * q[j] * (val[j] != mn ? mn : sec));  // :64-70
 #pragma unroll
         for (int j = 0; j < 3; ++j) {  // :73-80 (zero unless C == val_j; adding it keeps the sum exact)
-            const T r_ = (C == one - q[j] * v[j]) ? halfc * (q[j] - v[j]) : (T)0.0;
+            const T r_ = (C == one - q[j] * X.v[j]) ? halfc * (q[j] - X.v[j]) : (T)0.0;
             d[j] = d[j] + tr * r_;
-            tL[pos[j]] = d[j];
+            tL[X.pos[j]] = d[j];
         }
         if (PK != W_ADA2) uns = uns || !(C < (T)0.25);  // :88
         const T dxs = (T)20.0 * (xs_m + eps) * (C - (T)0.25);  // :84
@@ -116,7 +146,7 @@ __device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *cl4,
             cmL[2 * c + 1] = xl_n;
         }
     }
-    return __any(uns);
+    return __any(uns);  // this wave's; the caller combines a replica's waves
 }
 
 // Phase 2 for variable i: dv[i] as the reference's left fold of its terms (:33, :80).  The term
@@ -143,88 +173,121 @@ __device__ __forceinline__ void wave_sync() {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-// WPW replicas (one per wave) per workgroup share one LDS copy of the topology.
-template <typename T, bool ADAPTIVE, int WPW>
-__global__ __launch_bounds__(WAVE_NTH * WPW) void k_wave(WArgs<T> a) {
+// WPW replicas per workgroup share one LDS copy of the topology; each replica is a team of TW waves
+// (NL = 64 TW lanes).  TW = 1: a wave is on its own after the topology copy (its LDS operations
+// complete in issue order, so wave_sync only fences the compiler).  TW = 2 (small batches, where one
+// wave per replica would leave one wave per SIMD): the team's phases are ordered by workgroup
+// barriers, which every wave of the workgroup reaches the same number of times -- a frozen replica's
+// team skips the work but not the barriers, and the step loop ends when no team is active.
+template <int TW> __device__ __forceinline__ void team_sync() {
+    if (TW == 1) wave_sync();
+    else __syncthreads();
+}
+
+template <typename T, bool ADAPTIVE, int WPW, int TW>
+__global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
+    constexpr int NL = WAVE_NTH * TW;
     extern __shared__ __attribute__((aligned(16))) unsigned char wave_smem[];
     using U = typename Bits<T>::U;
     __shared__ U errL[WPW];
-    const int w = threadIdx.x / WAVE_NTH, l = threadIdx.x % WAVE_NTH;
-    const int g = blockIdx.x * WPW + w;  // this wave's replica (group width 1)
+    __shared__ int unsL[WPW * TW];  // TW > 1: each wave's "some clause unsat"
+    const int w = threadIdx.x / NL, l = threadIdx.x % NL;
+    const int g = blockIdx.x * WPW + w;  // this team's replica (group width 1)
     int4 *cl4 = reinterpret_cast<int4 *>(wave_smem);
     int4 *tp4 = cl4 + a.m;
     int32_t *vst = reinterpret_cast<int32_t *>(tp4 + a.m);
-    copy_to_lds<8>(cl4, a.cl4, (int)threadIdx.x, a.m, WAVE_NTH * WPW);
-    copy_to_lds<8>(tp4, a.tp4, (int)threadIdx.x, a.m, WAVE_NTH * WPW);
-    copy_to_lds<8>(vst, a.vst, (int)threadIdx.x, a.n + 1, WAVE_NTH * WPW);
-    __syncthreads();  // the workgroup's only barrier: from here on every wave is on its own
-    if (g >= a.G) return;
-    int act = a.act[g];
-    if (!act) return;  // uniform per wave
+    copy_to_lds<8>(cl4, a.cl4, (int)threadIdx.x, a.m, NL * WPW);
+    copy_to_lds<8>(tp4, a.tp4, (int)threadIdx.x, a.m, NL * WPW);
+    copy_to_lds<8>(vst, a.vst, (int)threadIdx.x, a.n + 1, NL * WPW);
+    __syncthreads();
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
-    int64_t sat = a.sat_step[g], done = a.steps_done[g];
-    T dtr = ADAPTIVE ? a.dtr[g] : a.dt;
+    const bool live = g < a.G && a.act[g] != 0;  // uniform per team
+    if (TW == 1 ? !live : !__syncthreads_or(live)) return;
+    int act = live;
+    int64_t sat = live ? a.sat_step[g] : -1, done = live ? a.steps_done[g] : 0;
+    T dtr = ADAPTIVE && live ? a.dtr[g] : a.dt;
     T *vL = reinterpret_cast<T *>(wave_smem + a.topo_bytes + (size_t)w * a.rep_bytes);
     T *vfL = vL + (ADAPTIVE ? a.n : 0);
     T *tL = vfL + a.n;
     T *cmL = tL + a.L;
     T *cL = cmL + 2 * a.m;
-    const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
-    T *V = (p ? a.v1 : a.v0) + (size_t)g * a.n;
-    T *CM = (p ? a.c1 : a.c0) + (size_t)g * a.m * 2;
-    copy_to_lds<8>(vL, V, l, a.n, WAVE_NTH);
-    copy_to_lds<8>(cmL, CM, l, 2 * a.m, WAVE_NTH);
-    wave_sync();
+    const bool p = live && __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
+    if (live) {
+        const T *V = (p ? a.v1 : a.v0) + (size_t)g * a.n;
+        const T *CM = (p ? a.c1 : a.c0) + (size_t)g * a.m * 2;
+        copy_to_lds<8>(vL, V, l, a.n, NL);
+        copy_to_lds<8>(cmL, CM, l, 2 * a.m, NL);
+    }
+    team_sync<TW>();
+    const int wi = (int)(threadIdx.x % NL) / WAVE_NTH;  // wave within the team
+    auto team_any = [&](bool u) {  // after the next team_sync: some wave of the team saw u
+        if (TW == 1) return u;
+        if ((threadIdx.x % WAVE_NTH) == 0) unsL[w * TW + wi] = u ? 1 : 0;
+        team_sync<TW>();
+        bool r = false;
+#pragma unroll
+        for (int j = 0; j < TW; ++j) r = r || unsL[w * TW + j] != 0;
+        return r;
+    };
     for (int k = 0; k < a.nsteps; ++k) {
         const int step = a.step0 + k;
         const T h = dtr;
         T e = (T)0.0;
-        bool uns;
+        bool uns = false;
         if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
-            uns = wave_clauses<T, W_FIXED>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
-            wave_sync();
-            for (int i = l; i < a.n; i += WAVE_NTH) vL[i] = dmin(dmax(vL[i] + h * wave_fold(vst, tL, i), (T)-1.0), (T)1.0);
-            wave_sync();
+            if (act) uns = wave_clauses<T, W_FIXED, NL>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
+            uns = team_any(uns);
+            team_sync<TW>();
+            if (act)
+                for (int i = l; i < a.n; i += NL) vL[i] = dmin(dmax(vL[i] + h * wave_fold(vst, tL, i), (T)-1.0), (T)1.0);
+            team_sync<TW>();
         } else {  // euler_step (:111-139)
-            uns = wave_clauses<T, W_ADA1>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
-            wave_sync();
-            if (uns) {  // an allsat replica takes no step (:122)
-                const T half = (T)0.5 * h;
-                for (int i = l; i < a.n; i += WAVE_NTH) {
+            if (act) uns = wave_clauses<T, W_ADA1, NL>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
+            uns = team_any(uns);
+            team_sync<TW>();
+            const bool go = act && uns;  // an allsat replica takes no step (:122)
+            const T half = (T)0.5 * h;
+            if (go)
+                for (int i = l; i < a.n; i += NL) {
                     const T d = wave_fold(vst, tL, i), v = vL[i];
                     vfL[i] = dmin(dmax(v + h * d, (T)-1.0), (T)1.0);    // full-step clone
                     vL[i] = dmin(dmax(v + half * d, (T)-1.0), (T)1.0);  // first half step
                 }
-                wave_sync();
-                wave_clauses<T, W_ADA2>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
-                wave_sync();
-                for (int i = l; i < a.n; i += WAVE_NTH) {
+            team_sync<TW>();
+            if (go) wave_clauses<T, W_ADA2, NL>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
+            team_sync<TW>();
+            if (go)
+                for (int i = l; i < a.n; i += NL) {
                     const T vn = dmin(dmax(vL[i] + half * wave_fold(vst, tL, i), (T)-1.0), (T)1.0);  // second half
                     e = dmax(e, dabs(vfL[i] - vn));  // :101-108
                     vL[i] = vn;
                 }
-                if (l == 0) errL[w] = 0;
-                wave_sync();
-                atomicMax(&errL[w], tobits(e));
-                wave_sync();
+            if (l == 0) errL[w] = 0;
+            team_sync<TW>();
+            if (go) atomicMax(&errL[w], tobits(e));
+            team_sync<TW>();
+            if (go) {
                 const T error = frombits(errL[w]);  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
                 dtr = dmax(dmin(dtr * dsqrt((T)a.tol / error), (T)1e3), (T)0.0078125);
             }
         }
-        done += 1;
-        if (!uns) {  // allsat: the fixed step was still taken (:148-152); adaptive took none
-            if (sat < 0) sat = step;
-            if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                            // simulate() breaks (:193)
-            if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
+        if (act) {
+            done += 1;
+            if (!uns) {  // allsat: the fixed step was still taken (:148-152); adaptive took none
+                if (sat < 0) sat = step;
+                if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                            // simulate() breaks (:193)
+                if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
+            }
         }
-        if (!act) break;  // uniform per wave
+        if (TW == 1 ? !act : !__syncthreads_or(act)) break;  // uniform per wave / per workgroup
     }
-    wave_sync();
+    team_sync<TW>();
+    if (!live) return;
     const bool q = a.oop ? !p : p;
     T *Vo = (q ? a.v1 : a.v0) + (size_t)g * a.n;
     T *CMo = (q ? a.c1 : a.c0) + (size_t)g * a.m * 2;
-    for (int i = l; i < a.n; i += WAVE_NTH) Vo[i] = vL[i];
-    for (int i = l; i < 2 * a.m; i += WAVE_NTH) CMo[i] = cmL[i];
+    for (int i = l; i < a.n; i += NL) Vo[i] = vL[i];
+    for (int i = l; i < 2 * a.m; i += NL) CMo[i] = cmL[i];
     if (l == 0) {
         if (a.oop) a.par[g] = (uint8_t)q;
         a.act[g] = (uint8_t)act;

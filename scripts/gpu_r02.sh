@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-    ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+    ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 tail -25 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc

@@ -549,10 +549,14 @@ def test_onchip_long_launches_sat_and_freeze(monkeypatch):
             assert same(x, y)
 
 
+@pytest.mark.parametrize("team", [None, "1", "2"])
 @pytest.mark.parametrize("n,m,prec,wave_env,wpw", [(250, 1065, "f64", None, 2), (600, 2520, "f32", "1", 1)])
-def test_wave_workgroup_widths(monkeypatch, n, m, prec, wave_env, wpw):
+def test_wave_workgroup_widths(monkeypatch, n, m, prec, wave_env, wpw, team):
     """k_wave with 2 (config 3 in f64) and 1 (a larger instance, forced) replicas per workgroup
-    equals FUSED bit for bit, fixed and adaptive."""
+    equals FUSED bit for bit, fixed and adaptive -- with the automatic team (8 and 16 waves per
+    replica) and with teams of 1 and 2 waves."""
+    if team is not None:
+        monkeypatch.setenv("ODESAT_WAVE_TEAM", team)
     from odesat_amd import _lib
     var, neg = wl.random_ksat(n, m, 3, 7)
     cp, v_, n_ = wl.formula_arrays(var, neg)
@@ -574,4 +578,30 @@ def test_wave_workgroup_widths(monkeypatch, n, m, prec, wave_env, wpw):
         assert np.array_equal(out[0][0]["first_sat_step"], out[1][0]["first_sat_step"])
         assert np.array_equal(out[0][0]["steps_done"], out[1][0]["steps_done"]) and same(out[0][0]["dt"], out[1][0]["dt"])
         for x, y in zip(out[0][1], out[1][1]):
+            assert same(x, y)
+
+
+@pytest.mark.parametrize("stop", [ODESAT_STOP_EACH, ODESAT_STOP_ANY, ODESAT_STOP_NONE])
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_wave_teams_equal_fused(monkeypatch, stop, adaptive):
+    """k_wave with one and with two waves per replica (ODESAT_WAVE_TEAM) equals FUSED bit for bit on
+    easy.cnf, where replicas satisfy and freeze at their own steps inside long launches: a frozen
+    replica's team keeps reaching the workgroup barriers of the others."""
+    from odesat_amd import _lib
+    f = product_formula("easy")
+    out = []
+    for alg, team in ((_lib.ODESAT_ALG_FUSED, "1"), (_lib.ODESAT_ALG_RESIDENT, "1"), (_lib.ODESAT_ALG_RESIDENT, "2"),
+                      (_lib.ODESAT_ALG_RESIDENT, "4")):
+        monkeypatch.setenv("ODESAT_WAVE", "1")
+        monkeypatch.setenv("ODESAT_WAVE_TEAM", team)
+        with Solver(f, 37, "f32") as s:
+            s.set_algorithm(alg)
+            s.init_state(6)
+            r = s.simulate(adaptive=adaptive, dt=0.1, tol=1e-3, max_steps=1500, stop=stop, poll_interval=300)
+            out.append((r, s.get_state()))
+    assert (out[0][0]["first_sat_step"] >= 0).any()
+    for r, st in out[1:]:
+        assert np.array_equal(out[0][0]["first_sat_step"], r["first_sat_step"])
+        assert np.array_equal(out[0][0]["steps_done"], r["steps_done"]) and same(out[0][0]["dt"], r["dt"])
+        for x, y in zip(out[0][1], st):
             assert same(x, y)
