@@ -63,7 +63,7 @@ struct odesat_solver {
     int res_R = 0;        // 0 = the layout does not admit the resident kernel
     bool res_narrow = false;  // RESIDENT with one wave per workgroup (R = 1, 64-clause tiles)
     bool res_wave = false;    // RESIDENT as k_wave (wave.hpp): small 3-SAT, one wave per replica, variable fold
-    int4 *wv_tp4 = nullptr;   // [m] k_wave: variable-major term position of each literal
+    int4 *wv_rec4 = nullptr;  // [m] k_wave: literal | variable-major term position << 16, per literal
     int32_t *wv_vst = nullptr;  // [n+1] k_wave: first term position of each variable
     int wv_wpw = 1;             // k_wave: replicas per workgroup sharing the LDS topology
     int wv_tw = 1;              // k_wave: waves per replica (2 when one per replica leaves SIMDs idle)
@@ -637,8 +637,7 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
                 int stop_mode, bool oop) {
     WArgs<T> a{};
     a.oop = oop ? 1 : 0;
-    a.cl4 = s->res_cl4;
-    a.tp4 = s->wv_tp4;
+    a.rec4 = s->wv_rec4;
     a.vst = s->wv_vst;
     a.v0 = (T *)s->v[0];
     a.v1 = (T *)s->v[1];
@@ -965,7 +964,7 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     for (auto e : s->pool) (void)hipEventDestroy(e);
     void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->pc, s->ps, s->empty, s->inc, s->v[0], s->v[1], s->c[0],
                     s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
-                    s->sat_step, s->steps_done, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec, s->wv_tp4, s->wv_vst};
+                    s->sat_step, s->steps_done, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec, s->wv_rec4, s->wv_vst};
     for (void *p : ptrs) dfree(p);
     void *snaps[] = {s->snap_par, s->snap_sat, s->snap_done, s->snap_dt, s->ck_v, s->ck_c, s->ck_dt, s->ck_par,
                      s->ck_act, s->ck_sat, s->ck_done, s->ck_stop};
@@ -1025,7 +1024,8 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     // k_wave (wave.hpp) for small 3-SAT instances whose replica -- with the adaptive clones --
     // fits in 64 KiB of LDS (two or more waves per CU); ODESAT_WAVE=0/1 overrides, an explicit
     // ODESAT_GROUP_WIDTH selects the tile kernels
-    if (s->uniform_k == 3 && m > 0 && !std::getenv("ODESAT_GROUP_WIDTH") && m < (1 << 26) && L < (1 << 26)) {
+    // (its clause records pack a literal and a term position in 16 bits each)
+    if (s->uniform_k == 3 && m > 0 && !std::getenv("ODESAT_GROUP_WIDTH") && 2 * n + 1 < (1 << 16) && L < (1 << 16)) {
         const char *ev = std::getenv("ODESAT_WAVE");
         const size_t topo = wave_topo_bytes(n, m), rep = wave_lds_bytes(n, m, L, s->tsize, true);
         s->wv_wpw = topo + 4 * rep <= RES_LDS_MAX ? 4 : (topo + 2 * rep <= RES_LDS_MAX ? 2 : 1);
@@ -1188,18 +1188,18 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             std::vector<int32_t> vst((size_t)n + 1, 0), fillc((size_t)n, 0);
             for (int64_t k = 0; k < L; ++k) vst[(lits[k] >> 1) + 1] += 1;
             for (int64_t i = 0; i < n; ++i) vst[i + 1] += vst[i];
-            std::vector<int4> tp4((size_t)m);
+            std::vector<int4> rec4((size_t)m);
             for (int64_t c = 0; c < m; ++c) {
                 int q[3];
                 for (int j = 0; j < 3; ++j) {
                     const int32_t v = lits[3 * c + j] >> 1;
-                    q[j] = vst[v] + fillc[v]++;
+                    q[j] = lits[3 * c + j] | (vst[v] + fillc[v]++) << 16;  // both < 2^16 (selection)
                 }
-                tp4[c] = make_int4(q[0], q[1], q[2], 0);
+                rec4[c] = make_int4(q[0], q[1], q[2], 0);
             }
-            if ((rc = dmalloc(s, (void **)&s->wv_tp4, (size_t)m * 16)) || (rc = dmalloc(s, (void **)&s->wv_vst, (n + 1) * 4)))
+            if ((rc = dmalloc(s, (void **)&s->wv_rec4, (size_t)m * 16)) || (rc = dmalloc(s, (void **)&s->wv_vst, (n + 1) * 4)))
                 return bail(rc);
-            if (hipMemcpy(s->wv_tp4, tp4.data(), (size_t)m * 16, hipMemcpyHostToDevice) != hipSuccess ||
+            if (hipMemcpy(s->wv_rec4, rec4.data(), (size_t)m * 16, hipMemcpyHostToDevice) != hipSuccess ||
                 hipMemcpy(s->wv_vst, vst.data(), (n + 1) * 4, hipMemcpyHostToDevice) != hipSuccess)
                 return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
             s->res_ada = true;  // wave_lds_bytes(adaptive) fits by selection

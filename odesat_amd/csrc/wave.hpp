@@ -27,8 +27,8 @@ namespace odk {
 constexpr int WAVE_NTH = 64;
 
 template <typename T> struct WArgs {
-    const int4 *__restrict__ cl4;     // [m] the clause's literals (var << 1 | neg), file order
-    const int4 *__restrict__ tp4;     // [m] variable-major position of each literal's term
+    const int4 *__restrict__ rec4;    // [m] per literal j: (var << 1 | neg) | (variable-major position of
+                                      // its term) << 16 -- both below 2^16 whenever k_wave is chosen
     const int32_t *__restrict__ vst;  // [n+1] variable -> first term position
     T *v0, *v1, *c0, *c1;             // state buffers, group width 1
     uint8_t *par;                     // flipped by an out-of-place launch
@@ -52,7 +52,7 @@ inline size_t wave_lds_bytes(int64_t n, int64_t m, int64_t L, size_t tsize, bool
     return (((adaptive ? 2 : 1) * (size_t)n + (size_t)L + (adaptive ? 3 : 2) * (size_t)m) * tsize + 15) / 16 * 16;
 }
 // the topology every wave of a workgroup reads: literal and position records, variable starts
-inline size_t wave_topo_bytes(int64_t n, int64_t m) { return ((size_t)m * 32 + (size_t)(n + 1) * 4 + 15) / 16 * 16; }
+inline size_t wave_topo_bytes(int64_t n, int64_t m) { return ((size_t)m * 16 + (size_t)(n + 1) * 4 + 15) / 16 * 16; }
 
 enum WPass : int { W_FIXED = 0, W_ADA1 = 1, W_ADA2 = 2 };
 
@@ -70,33 +70,31 @@ template <typename T> struct WClause {
 // clause: terms, memories and C are per clause and v is constant), so one wave per SIMD keeps
 // three clauses' LDS reads in flight instead of waiting on each clause's dependent load chain.
 template <typename T, int PK, int NL>
-__device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *cl4, const int4 *tp4, const T *vL, T *tL,
-                                             T *cmL, T *cL, int l, T h, T &e) {
+__device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *rec4, const T *vL, T *tL, T *cmL, T *cL,
+                                             int l, T h, T &e) {
     const T one = (T)1.0, halfc = (T)0.5, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
     bool uns = false;
     if (l >= a.m) return __any(uns);  // (NL > m: the lanes without a clause)
     const int last = a.m - 1;
-    auto gather = [&](int c, const int4 &l4, const int4 &p4, WClause<T> &W) {  // clamped: always loadable
-        W.lit[0] = l4.x, W.lit[1] = l4.y, W.lit[2] = l4.z;
-        W.pos[0] = p4.x, W.pos[1] = p4.y, W.pos[2] = p4.z;
+    typedef HIP_vector_type<T, 2> T2;  // a clause's (xs, xl): one 8- / 16-byte LDS access
+    auto gather = [&](int c, const int4 &r4, WClause<T> &W) {  // clamped: always loadable
+        W.lit[0] = r4.x & 0xffff, W.lit[1] = r4.y & 0xffff, W.lit[2] = r4.z & 0xffff;
+        W.pos[0] = (int)((uint32_t)r4.x >> 16), W.pos[1] = (int)((uint32_t)r4.y >> 16), W.pos[2] = (int)((uint32_t)r4.z >> 16);
 #pragma unroll
         for (int j = 0; j < 3; ++j) W.v[j] = vL[W.lit[j] >> 1];
-        W.xs = cmL[2 * c];
-        W.xl = cmL[2 * c + 1];
+        const T2 m2 = reinterpret_cast<const T2 *>(cmL)[c];
+        W.xs = m2.x;
+        W.xl = m2.y;
         if (PK == W_ADA2) W.C1 = cL[c];
     };
-    int4 rl = cl4[min(l + NL, last)], rp = tp4[min(l + NL, last)];  // records of the next clause
+    int4 rn = rec4[min(l + NL, last)];  // the record of the next clause
     WClause<T> W;
-    {
-        const int4 l4 = cl4[l], p4 = tp4[l];
-        gather(l, l4, p4, W);
-    }
+    gather(l, rec4[l], W);
     for (int c = l; c < a.m; c += NL) {
         const WClause<T> X = W;  // this clause
         const int cn = min(c + NL, last);
-        gather(cn, rl, rp, W);   // the next clause's voltages and memories
-        rl = cl4[min(c + 2 * NL, last)];
-        rp = tp4[min(c + 2 * NL, last)];
+        gather(cn, rn, W);       // the next clause's voltages and memories
+        rn = rec4[min(c + 2 * NL, last)];
         T q[3], val[3], d[3];
         T mn = inf_v<T>(), sec = inf_v<T>();
 #pragma unroll
@@ -133,8 +131,10 @@ __device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *cl4,
         const T dxs = (T)20.0 * (xs_m + eps) * (C - (T)0.25);  // :84
         const T dxl = (T)5.0 * (C - (T)0.05);                  // :85
         if (PK == W_FIXED) {
-            cmL[2 * c] = dmin(dmax(xs_m + h * dxs, eps), xs_hi);  // :94-95
-            cmL[2 * c + 1] = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
+            T2 m2;
+            m2.x = dmin(dmax(xs_m + h * dxs, eps), xs_hi);  // :94-95
+            m2.y = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
+            reinterpret_cast<T2 *>(cmL)[c] = m2;
         } else if (PK == W_ADA1) {
             cL[c] = C;  // the memories stay y until the second pass (an allsat replica takes no step)
         } else {
@@ -142,8 +142,10 @@ __device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *cl4,
             const T xs_n = dmin(dmax(xs_m + half * dxs, eps), xs_hi);
             const T xl_n = dmin(dmax(xl_m + half * dxl, one), a.xl_max);
             e = dmax(e, dmax(dabs(xs_f - xs_n), dabs(xl_f - xl_n)));
-            cmL[2 * c] = xs_n;
-            cmL[2 * c + 1] = xl_n;
+            T2 m2;
+            m2.x = xs_n;
+            m2.y = xl_n;
+            reinterpret_cast<T2 *>(cmL)[c] = m2;
         }
     }
     return __any(uns);  // this wave's; the caller combines a replica's waves
@@ -193,11 +195,9 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
     __shared__ int unsL[WPW * TW];  // TW > 1: each wave's "some clause unsat"
     const int w = threadIdx.x / NL, l = threadIdx.x % NL;
     const int g = blockIdx.x * WPW + w;  // this team's replica (group width 1)
-    int4 *cl4 = reinterpret_cast<int4 *>(wave_smem);
-    int4 *tp4 = cl4 + a.m;
-    int32_t *vst = reinterpret_cast<int32_t *>(tp4 + a.m);
-    copy_to_lds<8>(cl4, a.cl4, (int)threadIdx.x, a.m, NL * WPW);
-    copy_to_lds<8>(tp4, a.tp4, (int)threadIdx.x, a.m, NL * WPW);
+    int4 *rec4 = reinterpret_cast<int4 *>(wave_smem);
+    int32_t *vst = reinterpret_cast<int32_t *>(rec4 + a.m);
+    copy_to_lds<8>(rec4, a.rec4, (int)threadIdx.x, a.m, NL * WPW);
     copy_to_lds<8>(vst, a.vst, (int)threadIdx.x, a.n + 1, NL * WPW);
     __syncthreads();
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
@@ -206,11 +206,13 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
     int act = live;
     int64_t sat = live ? a.sat_step[g] : -1, done = live ? a.steps_done[g] : 0;
     T dtr = ADAPTIVE && live ? a.dtr[g] : a.dt;
-    T *vL = reinterpret_cast<T *>(wave_smem + a.topo_bytes + (size_t)w * a.rep_bytes);
+    // the replica's LDS: memories first (16-byte aligned: read and written as (xs, xl) pairs), the
+    // first pass's C (adaptive), v, its full-step clone (adaptive), the terms
+    T *cmL = reinterpret_cast<T *>(wave_smem + a.topo_bytes + (size_t)w * a.rep_bytes);
+    T *cL = cmL + 2 * a.m;
+    T *vL = cL + (ADAPTIVE ? a.m : 0);
     T *vfL = vL + (ADAPTIVE ? a.n : 0);
     T *tL = vfL + a.n;
-    T *cmL = tL + a.L;
-    T *cL = cmL + 2 * a.m;
     const bool p = live && __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
     if (live) {
         const T *V = (p ? a.v1 : a.v0) + (size_t)g * a.n;
@@ -235,14 +237,14 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
         T e = (T)0.0;
         bool uns = false;
         if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
-            if (act) uns = wave_clauses<T, W_FIXED, NL>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
+            if (act) uns = wave_clauses<T, W_FIXED, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
             uns = team_any(uns);
             team_sync<TW>();
             if (act)
                 for (int i = l; i < a.n; i += NL) vL[i] = dmin(dmax(vL[i] + h * wave_fold(vst, tL, i), (T)-1.0), (T)1.0);
             team_sync<TW>();
         } else {  // euler_step (:111-139)
-            if (act) uns = wave_clauses<T, W_ADA1, NL>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
+            if (act) uns = wave_clauses<T, W_ADA1, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
             uns = team_any(uns);
             team_sync<TW>();
             const bool go = act && uns;  // an allsat replica takes no step (:122)
@@ -254,7 +256,7 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
                     vL[i] = dmin(dmax(v + half * d, (T)-1.0), (T)1.0);  // first half step
                 }
             team_sync<TW>();
-            if (go) wave_clauses<T, W_ADA2, NL>(a, cl4, tp4, vL, tL, cmL, cL, l, h, e);
+            if (go) wave_clauses<T, W_ADA2, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
             team_sync<TW>();
             if (go)
                 for (int i = l; i < a.n; i += NL) {

@@ -563,7 +563,7 @@ def test_wave_workgroup_widths(monkeypatch, n, m, prec, wave_env, wpw, team):
     f = cnf.CNFFormula.from_arrays(cp, v_, n_, n)
     if wave_env is not None:
         monkeypatch.setenv("ODESAT_WAVE", wave_env)
-    topo = m * 32 + (n + 1) * 4
+    topo = m * 16 + (n + 1) * 4
     rep = ((2 * n + 3 * m + 3 * m) * (8 if prec == "f64" else 4) + 15) // 16 * 16
     assert (topo + 4 * rep > 159 * 1024) and (wpw == 1) == (topo + 2 * rep > 159 * 1024)
     for adaptive in (False, True):
