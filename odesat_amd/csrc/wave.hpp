@@ -62,19 +62,19 @@ template <typename T> struct WClause {
     T v[3], xs, xl, C1;
 };
 
-// Phase 1 over the replica's clauses.  Returns (wave-uniform) whether some clause is unsat (:88,
-// W_FIXED / W_ADA1) and raises e to the memories' max_error terms (W_ADA2).
+// Phase 1 over the replica's clauses, one lane's share.  Returns whether one of this lane's clauses
+// is unsat (:88, W_FIXED / W_ADA1) and raises e to the memories' max_error terms (W_ADA2).
 // Lane l of the replica's NL lanes takes clauses l, l + NL, ...  Software-pipelined: the records of
 // clause c + 2 NL and the voltages / memories of clause c + NL are loaded before clause c's
 // arithmetic and stores (nothing phase 1 stores is read by another
 // clause: terms, memories and C are per clause and v is constant), so one wave per SIMD keeps
 // three clauses' LDS reads in flight instead of waiting on each clause's dependent load chain.
 template <typename T, int PK, int NL>
-__device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *rec4, const T *vL, T *tL, T *cmL, T *cL,
+__device__ __forceinline__ bool lane_clauses(const WArgs<T> &a, const int4 *rec4, const T *vL, T *tL, T *cmL, T *cL,
                                              int l, T h, T &e) {
     const T one = (T)1.0, halfc = (T)0.5, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
     bool uns = false;
-    if (l >= a.m) return __any(uns);  // (NL > m: the lanes without a clause)
+    if (l >= a.m) return false;  // (NL > m: the lanes without a clause)
     const int last = a.m - 1;
     typedef HIP_vector_type<T, 2> T2;  // a clause's (xs, xl): one 8- / 16-byte LDS access
     auto gather = [&](int c, const int4 &r4, WClause<T> &W) {  // clamped: always loadable
@@ -148,7 +148,18 @@ __device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *rec4
             reinterpret_cast<T2 *>(cmL)[c] = m2;
         }
     }
-    return __any(uns);  // this wave's; the caller combines a replica's waves
+    return uns;
+}
+
+// Phase 1, wave-uniform result: some clause of this wave is unsat (the caller combines a replica's
+// waves).  The ballot runs after every lane's share has returned: taken inside lane_clauses, the
+// lanes without a clause (m < NL) would vote among themselves on a divergent path and leave the
+// result -- and the step loop's exit -- different across the wave's lanes.
+template <typename T, int PK, int NL>
+__device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *rec4, const T *vL, T *tL, T *cmL, T *cL,
+                                             int l, T h, T &e) {
+    const bool u = lane_clauses<T, PK, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
+    return __any(u);
 }
 
 // Phase 2 for variable i: dv[i] as the reference's left fold of its terms (:33, :80).  The term
