@@ -75,6 +75,7 @@ struct odesat_solver {
     // memories in VGPRs, [oc_tr, oc_tr + oc_tl) in LDS.  oc_tr == 0: not available
     int oc_tr = 0, oc_tl = 0;
     uint64_t *oc_rec = nullptr;  // [tiles][512] slot-major clause records (onchip::make_rec)
+    int32_t *oc_tcp = nullptr;   // [ntp + 1] tile starts padded with m (static-index loads in k_onchip)
     int64_t oc_rec_bytes = 0;
     bool in_range = true;        // every replica's state is in ONCHIP's range (onchip.hip header)
     int64_t bytes = 0;
@@ -600,6 +601,12 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
     s->oc_rec_bytes = (int64_t)(rec.size() * sizeof(uint64_t));
     if ((rc = dmalloc(s, (void **)&s->oc_rec, rec.size() * sizeof(uint64_t)))) return rc;
     HIP_TRY(hipMemcpy(s->oc_rec, rec.data(), rec.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    // tile starts padded with m past the last tile, so the kernel reads tile j's start and end at
+    // static offsets (no clamp): a padded tile is empty (its lanes load clause m - 1, store nothing)
+    std::vector<int32_t> tcp((size_t)ntp + 1, (int32_t)s->m);
+    for (int t = 0; t <= nt; ++t) tcp[t] = tiles[t];
+    if ((rc = dmalloc(s, (void **)&s->oc_tcp, tcp.size() * 4))) return rc;
+    HIP_TRY(hipMemcpy(s->oc_tcp, tcp.data(), tcp.size() * 4, hipMemcpyHostToDevice));
     s->oc_tr = tr;
     s->oc_tl = std::max(0, nt - tr);
     return ODESAT_OK;
@@ -745,7 +752,7 @@ int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zet
     a.rec = s->oc_rec;
     a.rec_bytes = (uint32_t)s->oc_rec_bytes;
     a.lds = onchip::lds_map(s->n);
-    a.tc = s->res_tc;
+    a.tc = s->oc_tcp;
     a.v0 = (float *)s->v[0];
     a.v1 = (float *)s->v[1];
     a.c0 = (float *)s->c[0];
@@ -964,7 +971,7 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     for (auto e : s->pool) (void)hipEventDestroy(e);
     void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->pc, s->ps, s->empty, s->inc, s->v[0], s->v[1], s->c[0],
                     s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
-                    s->sat_step, s->steps_done, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec, s->wv_rec4, s->wv_vst};
+                    s->sat_step, s->steps_done, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec, s->oc_tcp, s->wv_rec4, s->wv_vst};
     for (void *p : ptrs) dfree(p);
     void *snaps[] = {s->snap_par, s->snap_sat, s->snap_done, s->snap_dt, s->ck_v, s->ck_c, s->ck_dt, s->ck_par,
                      s->ck_act, s->ck_sat, s->ck_done, s->ck_stop};

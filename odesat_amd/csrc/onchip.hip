@@ -236,22 +236,53 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
 }
 
 typedef const __attribute__((address_space(4))) int32_t cint32;
+// The replica's clause memories as a buffer resource (m float2 records): tile j's slot of lane l is
+// the byte offset 8 (tc[j] + l), checked against the range as a whole (the VGPR offset: the scalar
+// offset is not range-checked), so a slot past the replica's memories reads 0 and stores nothing.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mem_rsrc(float *base, int m) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, 8 * m, 0x00020000);
+}
 
-// Load (in) or store the register tiles' memories from / to the replica's clause memories.  The loads
-// are unconditional (an empty slot reads clause `mlast`'s memories, which nothing uses: its literals
-// point at the sink words, so its terms go to the dv sinks and its update is not stored), so the
-// compiler issues all of them back to back instead of one branch and one wait per tile.
+// Load the register tiles' memories.  Tile j's start is a scalar load at a static offset of the
+// padded tile table (a tile past the last one starts at m), so the compiler batches them into wide
+// scalar loads.  The loads are unconditional: a slot past the end of the memories reads 0 (buffer
+// range check), any other empty slot reads the next tile's clause -- neither is used, since an
+// empty slot's literals point at the sink words (its terms go to the dv sinks) and its update is
+// not stored.
 template <int TR, int... Js>
-__device__ __forceinline__ void mem_io(std::integer_sequence<int, Js...>, const cint32 *tc, int nt, float2 *CM,
-                                       float2 (&mr)[TR], int lane, bool in, int mlast) {
+__device__ __forceinline__ void mem_load(std::integer_sequence<int, Js...>, const cint32 *tc,
+                                         __amdgpu_buffer_rsrc_t rs, uint32_t lane8, float2 (&mr)[TR]) {
+    typedef int i2 __attribute__((ext_vector_type(2)));
     auto one = [&](auto J) {
         constexpr int j = decltype(J)::value;
-        const int c0 = tc[min(j, nt)], c1 = tc[min(j + 1, nt)];
-        const int c = c0 + lane;
-        if (in) mr[j] = CM[min(c, mlast)];
-        else if (c < c1) CM[c] = mr[j];
+        const i2 r = __builtin_amdgcn_raw_buffer_load_b64(rs, lane8 + 8u * (uint32_t)tc[j], 0, 0);
+        mr[j] = make_float2(__int_as_float(r.x), __int_as_float(r.y));
     };
     (one(std::integral_constant<int, Js>{}), ...);
+}
+
+// Store them back, 8 tiles at a time: the group's 9 tile bounds are loaded together (one wide
+// scalar load, no wait per tile); a lane whose slot of tile j holds no clause stores out of the
+// buffer's range, which drops the store.
+template <int TR, int... Gs>
+__device__ __forceinline__ void mem_store(std::integer_sequence<int, Gs...>, const cint32 *tc,
+                                          __amdgpu_buffer_rsrc_t rs, int lane, const float2 (&mr)[TR]) {
+    typedef int i2 __attribute__((ext_vector_type(2)));
+    auto group = [&](auto G) {
+        constexpr int j0 = decltype(G)::value * 8;
+        int b[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) b[k] = tc[j0 + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t vo = lane < b[k + 1] - b[k] ? 8u * (uint32_t)(b[k] + lane) : 0x80000000u;
+            i2 r;
+            r.x = __float_as_int(mr[j0 + k].x);
+            r.y = __float_as_int(mr[j0 + k].y);
+            __builtin_amdgcn_raw_buffer_store_b64(r, rs, vo, 0, 0);
+        }
+    };
+    (group(std::integral_constant<int, Gs>{}), ...);
 }
 
 // The kernel declares no static LDS, so dynamic LDS -- and the records' byte addresses -- start at 0.
@@ -290,9 +321,10 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     }
     const int mlast = a.m - 1;
     float2 mr[TR];
-    mem_io<TR>(std::make_integer_sequence<int, TR>{}, tc, a.ntiles, CM, mr, lane, true, mlast);
+    mem_load<TR>(std::make_integer_sequence<int, TR>{}, tc, mem_rsrc((p ? a.c1 : a.c0) + (size_t)g * a.m * 2, a.m),
+                 8u * (uint32_t)lane, mr);
     for (int t = 0; t < a.tl; ++t) {
-        const int c0 = tc[min(TR + t, a.ntiles)];
+        const int c0 = tc[TR + t];
         *lds_f2(mem_addr(a, t, lane)) = CM[min(c0 + lane, mlast)];  // (empty slots: as mem_io)
     }
     if (lane < 2) lds_st(UNS + 4u * lane, 0.0f);
@@ -329,9 +361,10 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         float2 *CMs = reinterpret_cast<float2 *>((q ? a.c1 : a.c0) + (size_t)g * a.m * 2);
         const cint32 *tcs = tc;
         asm volatile("" : "+s"(CMs), "+s"(tcs));
-        mem_io<TR>(std::make_integer_sequence<int, TR>{}, tcs, a.ntiles, CMs, mr, lane, false, 0);
+        static_assert(TR % 8 == 0, "register tiles are stored in groups of 8");
+        mem_store<TR>(std::make_integer_sequence<int, TR / 8>{}, tcs, mem_rsrc(reinterpret_cast<float *>(CMs), a.m), lane, mr);
         for (int t = 0; t < a.tl; ++t) {  // this lane's own LDS slots: no barrier needed
-            const int c0 = tc[min(TR + t, a.ntiles)], c1 = tc[min(TR + t + 1, a.ntiles)];
+            const int c0 = tc[TR + t], c1 = tc[TR + t + 1];
             const int c = c0 + lane;
             if (c < c1) CMs[c] = *lds_f2(mem_addr(a, t, lane));
         }

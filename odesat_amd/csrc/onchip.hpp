@@ -50,7 +50,8 @@ inline int tl_max(int64_t n) {
 struct Args {
     const uint64_t *rec; // [tiles][NTH] slot-major clause records (make_rec), padded with empty tiles
     uint32_t rec_bytes;
-    const int32_t *tc;   // [ntiles + 1] first internal clause of each tile (constant memory reads)
+    const int32_t *tc;   // first internal clause of each tile, [ntiles + 1] padded with m to at least
+                         // TR + tl + 1 entries (constant memory reads at static offsets)
     float *v0, *v1;      // voltages, [B][n] (par selects the buffer holding the current state)
     float *c0, *c1;      // clause memories, [B][m][2] (xs, xl), internal clause order
     uint8_t *par;        // [B] (flipped by an out-of-place launch)
