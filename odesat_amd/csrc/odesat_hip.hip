@@ -574,9 +574,13 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
         if (x == y || x == z || y == z) return ODESAT_OK;
     }
     const int tl_max = onchip::tl_max(s->n);
+    int live = nt;  // tiles up to the last one holding a clause (the tiling is padded to 4 for RESIDENT)
+    while (live > 0 && tiles[live] == tiles[live - 1]) --live;
     int tr = 0;
     for (int c : onchip::TR_CHOICES)
-        if (c >= nt) { tr = c; break; }
+        if (c >= live) { tr = c; break; }
+    // LDS tiles follow TR_MAX register tiles (their loop continues the 4-deep record ring, so it
+    // starts at a multiple of 4; nt is one)
     if (tr == 0 && nt - onchip::TR_MAX <= tl_max) tr = onchip::TR_MAX;
     if (tr == 0) return ODESAT_OK;
     // slot-major records, padded with empty tiles so every tile a pass touches exists; an empty
@@ -608,7 +612,7 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
     if ((rc = dmalloc(s, (void **)&s->oc_tcp, tcp.size() * 4))) return rc;
     HIP_TRY(hipMemcpy(s->oc_tcp, tcp.data(), tcp.size() * 4, hipMemcpyHostToDevice));
     s->oc_tr = tr;
-    s->oc_tl = std::max(0, nt - tr);
+    s->oc_tl = tr < live ? nt - tr : 0;
     return ODESAT_OK;
 }
 

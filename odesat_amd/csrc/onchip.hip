@@ -261,20 +261,21 @@ __device__ __forceinline__ void mem_load(std::integer_sequence<int, Js...>, cons
     (one(std::integral_constant<int, Js>{}), ...);
 }
 
-// Store them back, 8 tiles at a time: the group's 9 tile bounds are loaded together (one wide
-// scalar load, no wait per tile); a lane whose slot of tile j holds no clause stores out of the
-// buffer's range, which drops the store.
+// Store them back, 8 tiles at a time (the last group may be shorter): the group's tile bounds are
+// loaded together (one wide scalar load, no wait per tile); a lane whose slot of tile j holds no
+// clause stores out of the buffer's range, which drops the store.
 template <int TR, int... Gs>
 __device__ __forceinline__ void mem_store(std::integer_sequence<int, Gs...>, const cint32 *tc,
                                           __amdgpu_buffer_rsrc_t rs, int lane, const float2 (&mr)[TR]) {
     typedef int i2 __attribute__((ext_vector_type(2)));
     auto group = [&](auto G) {
         constexpr int j0 = decltype(G)::value * 8;
+        constexpr int cnt = TR - j0 < 8 ? TR - j0 : 8;
         int b[9];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) b[k] = tc[j0 + k];
+        for (int k = 0; k <= cnt; ++k) b[k] = tc[j0 + k];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < cnt; ++k) {
             const uint32_t vo = lane < b[k + 1] - b[k] ? 8u * (uint32_t)(b[k] + lane) : 0x80000000u;
             i2 r;
             r.x = __float_as_int(mr[j0 + k].x);
@@ -361,8 +362,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         float2 *CMs = reinterpret_cast<float2 *>((q ? a.c1 : a.c0) + (size_t)g * a.m * 2);
         const cint32 *tcs = tc;
         asm volatile("" : "+s"(CMs), "+s"(tcs));
-        static_assert(TR % 8 == 0, "register tiles are stored in groups of 8");
-        mem_store<TR>(std::make_integer_sequence<int, TR / 8>{}, tcs, mem_rsrc(reinterpret_cast<float *>(CMs), a.m), lane, mr);
+        mem_store<TR>(std::make_integer_sequence<int, (TR + 7) / 8>{}, tcs, mem_rsrc(reinterpret_cast<float *>(CMs), a.m), lane, mr);
         for (int t = 0; t < a.tl; ++t) {  // this lane's own LDS slots: no barrier needed
             const int c0 = tc[TR + t], c1 = tc[TR + t + 1];
             const int c = c0 + lane;
@@ -391,7 +391,9 @@ hipError_t launch(int tr, const Args &a, int G, size_t lds, hipStream_t stream) 
 #define ONCHIP_CASE(N) \
     case N: return launch_t<N>(a, G, lds, stream);
         ONCHIP_CASE(8) ONCHIP_CASE(16) ONCHIP_CASE(24) ONCHIP_CASE(32) ONCHIP_CASE(40) ONCHIP_CASE(48)
-        ONCHIP_CASE(56) ONCHIP_CASE(64) ONCHIP_CASE(72) ONCHIP_CASE(80) ONCHIP_CASE(88) ONCHIP_CASE(96)
+        ONCHIP_CASE(56) ONCHIP_CASE(64) ONCHIP_CASE(66) ONCHIP_CASE(68) ONCHIP_CASE(70) ONCHIP_CASE(72)
+        ONCHIP_CASE(74) ONCHIP_CASE(76) ONCHIP_CASE(78) ONCHIP_CASE(80) ONCHIP_CASE(82) ONCHIP_CASE(84)
+        ONCHIP_CASE(86) ONCHIP_CASE(88) ONCHIP_CASE(90) ONCHIP_CASE(92) ONCHIP_CASE(94) ONCHIP_CASE(96)
 #undef ONCHIP_CASE
         default: return hipErrorInvalidValue;
     }

@@ -65,10 +65,14 @@ struct Args {
     Lds lds;
 };
 
-// Register-tile counts compiled (template instantiations; VGPRs ~ 50 + 2 TR, ~243 at TR = 96).
-// Every launch runs all TR register tiles (the empty ones cost a barrier each), so the host picks
-// the smallest TR >= ntiles, else TR = 96 plus LDS tiles for the rest.
-constexpr int TR_CHOICES[] = {8, 16, 24, 32, 40, 48, 56, 64, 72, 80, 88, 96};
+// Register-tile counts compiled (template instantiations; VGPRs ~ 50 + 2 TR, ~245 at TR = 96).
+// Every launch runs all TR register tiles (an empty one costs as much as a full one: a barrier and
+// the whole tile code), so the host picks the smallest TR >= the tiles that hold clauses -- in steps
+// of 2 where real instances land (config 2: 90 tiles, k_onchip<90>) -- else TR = 96 plus LDS tiles
+// for the rest.  A branch that skipped the empty tiles instead costs every tile a join (register
+// copies and a vmcnt(0) wait on the record ring).
+constexpr int TR_CHOICES[] = {8, 16, 24, 32, 40, 48, 56, 64, 66, 68, 70, 72, 74, 76, 78, 80,
+                              82, 84, 86, 88, 90, 92, 94, 96};
 constexpr int TR_MAX = 96;
 
 // Record of one clause slot (8 bytes): lo = a0 | a1 << 16, hi = a2 | neg0 << 31 | neg1 << 30 |
