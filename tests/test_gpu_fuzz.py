@@ -1,0 +1,159 @@
+"""GPU fuzz parity: seeded random formulas of many shapes -- clause counts around the wave and tile
+widths (1, 63, 64, 65, 511, 512, 513 ...), tiny and unused variable sets, mixed clause widths,
+repeated variables in a clause, x and -x in one clause, empty and unit clauses -- run through EVERY
+algorithm and layout the solver can take for them, each checked bit for bit against the CPU oracle
+(system.rs:141-154 fixed steps and :111-139 adaptive steps, simulate's per-replica stop at the
+first allsat step, :156-239).
+
+The fixed fixtures of test_gpu_parity.py exercise each kernel path on a few shapes; a lane-count
+edge (k_wave with fewer clauses than lanes voting on a divergent path) slipped through them.  Here
+the shapes are drawn so that partial waves, partial tiles, one-clause tiles, single-wave replicas,
+ragged last workgroups and the trailing empty tiles of every path are hit.  Seeded: the same cases
+every run."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle.oracle import Oracle, init_voltages
+from odesat_amd import _lib, cnf
+from odesat_amd.system import ODESAT_STOP_EACH, Solver
+
+pytestmark = pytest.mark.gpu
+
+T_OF = {"f64": np.float64, "f32": np.float32}
+
+
+def same(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    if a.shape != b.shape:
+        return False
+    na, nb = np.isnan(a), np.isnan(b)
+    return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint64), b[~nb].view(np.uint64))
+
+
+def gen(seed):
+    """(name, n, clause_ptr, var, neg) of one drawn formula (0-based variables)."""
+    rng = np.random.default_rng(seed)
+    kind = ["k3", "k3", "k3", "k3dup", "mixed", "units"][seed % 6]
+    m = int(rng.choice([1, 2, 5, 31, 63, 64, 65, 127, 129, 200, 511, 512, 513, 1100, 2600]))
+    if kind == "k3":
+        n = int(rng.choice([3, 4, 7, 40, 64, 65, 300, 900])) if m > 1 else 3
+        n = max(n, 3)
+        var = np.stack([rng.choice(n, 3, replace=False) for _ in range(m)])
+        cp = np.arange(m + 1) * 3
+    elif kind == "k3dup":  # three literals, variables may repeat (x x y, x -x y)
+        n = int(rng.choice([2, 5, 33, 200]))
+        var = rng.integers(0, n, (m, 3))
+        cp = np.arange(m + 1) * 3
+    else:
+        n = int(rng.choice([1, 6, 50, 400])) if kind == "units" else int(rng.choice([5, 30, 150, 700]))
+        widths = rng.integers(1, 3 if kind == "units" else 7, m)
+        if kind == "mixed" and m > 3:
+            widths[rng.integers(0, m)] = 0  # one empty clause (never satisfied: no allsat)
+        cp = np.concatenate([[0], np.cumsum(widths)])
+        var = rng.integers(0, n, int(cp[-1]))
+    var = np.asarray(var, np.int64).reshape(-1)
+    neg = (rng.random(var.size) < 0.5).astype(np.uint8)
+    return f"{kind}-n{n}-m{m}", n, np.asarray(cp, np.int64), var, neg
+
+
+def variants(prec, uniform3, distinct):
+    """(label, env, algorithm) of every path the solver can take for such a formula."""
+    v = [("default", {}, None),
+         ("fused", {}, _lib.ODESAT_ALG_FUSED),
+         ("twopass", {}, _lib.ODESAT_ALG_TWOPASS),
+         ("fused-w8", {"ODESAT_GROUP_WIDTH": "8"}, _lib.ODESAT_ALG_FUSED),
+         ("resident-r1", {"ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "0"}, _lib.ODESAT_ALG_RESIDENT),
+         ("resident-narrow", {"ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "1"}, _lib.ODESAT_ALG_RESIDENT),
+         ("resident-r4", {"ODESAT_GROUP_WIDTH": "4"}, _lib.ODESAT_ALG_RESIDENT)]
+    if uniform3:
+        for team in ("1", "2", "4"):
+            v.append((f"wave-t{team}", {"ODESAT_WAVE": "1", "ODESAT_WAVE_TEAM": team}, _lib.ODESAT_ALG_RESIDENT))
+        if prec == "f32" and distinct:
+            v.append(("onchip", {"ODESAT_WAVE": "0", "ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "0"},
+                      _lib.ODESAT_ALG_ONCHIP))
+    return v
+
+
+COVERED = {}  # (variant label, algorithm that ran) -> cases checked
+
+
+def run_variant(f, B, prec, env, alg, adaptive, K, poll):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        with Solver(f, B, prec) as s:
+            if alg is not None:
+                try:
+                    s.set_algorithm(alg)
+                except _lib.OdesatError:
+                    return None  # not available for this formula / layout
+            s.init_state(9)
+            # fixed: dt 0.05; adaptive: the reference's initial dt 0.01 (system.rs:182)
+            r = s.simulate(adaptive=adaptive, dt=0.01 if adaptive else 0.05, tol=1e-3, zeta=0.01, max_steps=K,
+                           stop=ODESAT_STOP_EACH, poll_interval=poll)
+            return s.algorithm, r, s.get_state()
+    finally:
+        for k, x in old.items():
+            if x is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = x
+
+
+@pytest.mark.parametrize("seed", range(48))
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_fuzz_every_path_matches_oracle(seed, prec):
+    name, n, cp, var, neg = gen(seed)
+    f = cnf.CNFFormula.from_arrays(cp, var, neg, n)
+    o = Oracle(cp, var, neg, n, prec)
+    T = T_OF[prec]
+    m = len(cp) - 1
+    widths = np.diff(cp)
+    uniform3 = bool((widths == 3).all())
+    distinct = uniform3 and all(len(set(var[3 * c:3 * c + 3].tolist())) == 3 for c in range(m))
+    B = [1, 5, 67][seed % 3]
+    K = 40
+    for adaptive in (False, True):
+        ref = []
+        for b in range(B):
+            ov = init_voltages(9, b, 1, n)[0].astype(T)
+            oxs, oxl = o.init_short_term_memory(), np.ones(m, T)
+            if adaptive:
+                t, sat, _, h, _ = o.simulate(ov, oxs, oxl, tol=T(1e-3), dt=None, steps=K, zeta=T(0.01))
+            else:
+                t, sat, _, h, _ = o.simulate(ov, oxs, oxl, dt=T(0.05), steps=K, zeta=T(0.01))
+            ref.append((t, sat, ov, oxs, oxl))
+        ran = set()
+        for label, env, alg in variants(prec, uniform3, distinct):
+            out = run_variant(f, B, prec, env, alg, adaptive, K, poll=[3, 7, 40][seed % 3])
+            if out is None:
+                continue
+            galg, r, (gv, gxs, gxl) = out
+            ran.add((label, galg))
+            COVERED[(label, galg)] = COVERED.get((label, galg), 0) + 1
+            for b in range(B):
+                t, sat, ov, oxs, oxl = ref[b]
+                ctx = f"{name} {prec} {'adaptive' if adaptive else 'fixed'} {label} (alg {galg}) replica {b}"
+                assert r["steps_done"][b] == t, ctx
+                assert (r["first_sat_step"][b] >= 0) == sat, ctx
+                assert same(gv[b], ov) and same(gxs[b], oxs) and same(gxl[b], oxl), ctx
+        assert ("fused", _lib.ODESAT_ALG_FUSED) in ran
+
+
+def test_fuzz_covered_every_path():
+    """The cases above reached every kernel family: FUSED (W = 64 and 8), TWOPASS, the RESIDENT
+    tile kernels (512-lane, one-wave and R = 4 tiles), k_wave with teams of 1, 2 and 4 waves, and
+    ONCHIP."""
+    if not COVERED:
+        pytest.skip("run together with test_fuzz_every_path_matches_oracle")
+    need = [("fused", _lib.ODESAT_ALG_FUSED), ("twopass", _lib.ODESAT_ALG_TWOPASS),
+            ("fused-w8", _lib.ODESAT_ALG_FUSED), ("resident-r1", _lib.ODESAT_ALG_RESIDENT),
+            ("resident-narrow", _lib.ODESAT_ALG_RESIDENT), ("resident-r4", _lib.ODESAT_ALG_RESIDENT),
+            ("wave-t1", _lib.ODESAT_ALG_RESIDENT), ("wave-t2", _lib.ODESAT_ALG_RESIDENT),
+            ("wave-t4", _lib.ODESAT_ALG_RESIDENT), ("onchip", _lib.ODESAT_ALG_ONCHIP)]
+    print(sorted(COVERED.items()))
+    missing = [k for k in need if COVERED.get(k, 0) < 4]
+    assert not missing, (missing, COVERED)
