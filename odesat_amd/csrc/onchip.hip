@@ -40,6 +40,27 @@
 namespace onchip {
 namespace {
 
+// Diagnostic build only (-DONCHIP_STAMPS=1|2, scripts/build_variant.sh): per wave, s_memtime stamps
+// split each tile step into the barrier wait and the work before it (2: and the dv read-modify-write
+// at its start); the sums go to g_onchip_stamps, read by odesat_onchip_stamps.  Each stamp drains the
+// wave's LDS operations, so read the SHARES, never the build's run time.  In the product build
+// Stamps is empty and every stamp call vanishes.
+#ifdef ONCHIP_STAMPS
+struct Stamps {
+    uint64_t last, bar, work, rmw, tiles;
+};
+__device__ unsigned long long g_onchip_stamps[4096 * 16 * 4];
+__device__ __forceinline__ uint64_t memtime() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#else
+struct Stamps {};
+#endif
+
 struct Slot {  // one lane's literal record for one tile
     uint32_t lo, hi;
 };
@@ -145,12 +166,16 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
 // second half and tile t+2's first half -- independent, so they interleave -- while the writes
 // and the gathers drain.  The barrier then orders tile t's dv against tile t+1's.
 __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &slot3, float2 &mem1, Pend &P, Front &Fn,
-                                          Gath &Gn, int t, float h, float hh, uint32_t &cmax) {
+                                          Gath &Gn, int t, float h, float hh, uint32_t &cmax, Stamps &S) {
     const float o0 = lds_f(P.a0 + DVC), o1 = lds_f(P.a1 + DVC), o2 = lds_f(P.a2 + DVC);
     lds_st(P.a0 + DVC, o0 + P.d0);
     lds_st(P.a1 + DVC, o1 + P.d1);
     lds_st(P.a2 + DVC, o2 + P.d2);
     __builtin_amdgcn_sched_barrier(0);
+#if defined(ONCHIP_STAMPS) && ONCHIP_STAMPS == 2
+    const uint64_t t_rmw = memtime();
+    S.rmw += t_rmw - S.last;
+#endif
     Gath G3;
     gather(slot3, G3);
     slot3 = load_rec(R, t + 7);
@@ -158,8 +183,17 @@ __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &sl
     back(a, Fn, mem1, h, hh, P, cmax);  // P <- tile t+1's terms (tile t's were written above)
     front(Gn, Fn);                      // Fn <- tile t+2's first half
     __builtin_amdgcn_sched_barrier(0);  // a tile's work stays between its barriers
+#ifdef ONCHIP_STAMPS
+    const uint64_t t_pre = memtime();
+    S.work += t_pre - S.last;
+#endif
     __syncthreads();
     __builtin_amdgcn_sched_barrier(0);
+#ifdef ONCHIP_STAMPS
+    S.last = memtime();
+    S.bar += S.last - t_pre;
+    S.tiles += 1;
+#endif
     Gn = G3;
 }
 
@@ -175,13 +209,13 @@ __device__ __forceinline__ uint32_t mem_addr(const Args &a, int lt, int lane) {
 // the copies that merge mr[] there double its VGPR footprint.
 template <int TR, int T>
 __device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&mr)[TR], Slot (&ring)[4], Pend &P,
-                                         Front &Fn, Gath &Gn, float h, float hh, int lane, uint32_t &cmax) {
+                                         Front &Fn, Gath &Gn, float h, float hh, int lane, uint32_t &cmax, Stamps &S) {
     if constexpr (T + 1 < TR) {
-        tile_step(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, cmax);
+        tile_step(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, cmax, S);
     } else {  // tile TR is the first LDS tile (if any)
         float2 m = make_float2(0.0f, 0.0f);
         if (a.tl > 0) m = *lds_f2(mem_addr(a, 0, lane));
-        tile_step(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, cmax);
+        tile_step(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, cmax, S);
         if (a.tl > 0) *lds_f2(mem_addr(a, 0, lane)) = m;
     }
 }
@@ -189,13 +223,13 @@ __device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&
 template <int TR, int... Ts>
 __device__ __forceinline__ void reg_tiles(std::integer_sequence<int, Ts...>, const Args &a, const Recs &R,
                                           float2 (&mr)[TR], Slot (&ring)[4], Pend &P, Front &Fn, Gath &Gn, float h,
-                                          float hh, int lane, uint32_t &cmax) {
-    (reg_tile<TR, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax), ...);
+                                          float hh, int lane, uint32_t &cmax, Stamps &S) {
+    (reg_tile<TR, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S), ...);
 }
 
 // One RHS pass + memory update over every tile; ends with a barrier (dv complete).
 template <int TR>
-__device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, int lane, uint32_t &cmax) {
+__device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, int lane, uint32_t &cmax, Stamps &S) {
     Recs R;
     R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec, 0, (int)a.rec_bytes, 0x00020000);
     R.voff = (uint32_t)lane * 8u;
@@ -219,7 +253,7 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
     front(G0, F0);
     front(G1, Fn);
     back(a, F0, mr[0], h, hh, P, cmax);
-    reg_tiles<TR>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax);
+    reg_tiles<TR>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S);
     // LDS tiles [TR, TR + tl): tl is a multiple of 4 (the host pads the tiling)
     const int NT = TR + a.tl;
     const int last = a.tl - 1;
@@ -229,7 +263,7 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
             const int t = t0 + u;
             const uint32_t ma = mem_addr(a, min(t + 1 - TR, last), lane);
             float2 m = *lds_f2(ma);
-            tile_step(a, R, ring[(u + 3) % 4], m, P, Fn, Gn, t, h, hh, cmax);
+            tile_step(a, R, ring[(u + 3) % 4], m, P, Fn, Gn, t, h, hh, cmax, S);
             *lds_f2(ma) = m;
         }
     }
@@ -332,9 +366,13 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     __syncthreads();
 
     const float h = a.dt, hh = 0.5f * a.dt;
+    Stamps S{};
     for (int k = 0; k < a.nsteps; ++k) {  // euler_step_fixed (system.rs:141-154)
         uint32_t cmax = 0u;
-        pass<TR>(a, mr, h, lane, cmax);
+#ifdef ONCHIP_STAMPS
+        S.last = memtime();
+#endif
+        pass<TR>(a, mr, h, lane, cmax, S);
         if (!(__uint_as_float(cmax) < 0.5f)) lds_st(UNS + 4u * (k & 1), 1.0f);
         for (int i = lane; i < a.n; i += NTH) {  // :96 (h dv = (h/2) dv2), dv restarts at 0 (:33)
             const float d2 = lds_f(4u * i + DVC);
@@ -369,6 +407,15 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
             if (c < c1) CMs[c] = *lds_f2(mem_addr(a, t, lane));
         }
     }
+#ifdef ONCHIP_STAMPS
+    if ((lane & 63) == 0 && g < 4096) {
+        unsigned long long *o = g_onchip_stamps + ((size_t)g * 16 + lane / 64) * 4;
+        o[0] = S.bar;
+        o[1] = S.work;
+        o[2] = S.rmw;
+        o[3] = S.tiles;
+    }
+#endif
     if (lane == 0) {
         if (a.oop) a.par[g] = (uint8_t)q;
         a.act[g] = (uint8_t)act;
@@ -400,3 +447,12 @@ hipError_t launch(int tr, const Args &a, int G, size_t lds, hipStream_t stream) 
 }
 
 }  // namespace onchip
+
+#ifdef ONCHIP_STAMPS
+// Diagnostic build only: copy out the per-(replica, wave) stamp sums {barrier wait, work, dv RMW,
+// tiles} of the last launches (replicas < 4096, 16 wave slots each).
+extern "C" int odesat_onchip_stamps(unsigned long long *out, int count) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(onchip::g_onchip_stamps), sizeof(unsigned long long) * (size_t)count, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
