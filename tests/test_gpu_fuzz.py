@@ -157,3 +157,103 @@ def test_fuzz_covered_every_path():
     print(sorted(COVERED.items()))
     missing = [k for k in need if COVERED.get(k, 0) < 4]
     assert not missing, (missing, COVERED)
+
+
+# ------------------------------------------------------------- one instance across ranks -------
+PART_ENVS = [{}, {"ODESAT_PART_TERMS": "slot"}, {"ODESAT_PART_TERMS": "ell"}, {"ODESAT_PART_PACK": "0"},
+             {"ODESAT_PART_K3": "0"}, {"ODESAT_PART_XCD": "1"}]
+
+
+@pytest.mark.parametrize("seed", range(0, 48, 2))
+def test_fuzz_partition_matches_oracle(seed):
+    """The partitioned single-replica kernels (csrc/partition.hip, config 5's path) on the fuzzed
+    shapes: VARIABLES at world 1-4 (ranks of one process sharing the device, the all-gather done
+    in-process) and CLAUSES at world 1, every term layout / record / kernel / placement choice,
+    against the oracle's f32 fixed steps (system.rs:141-154) bit for bit, sat steps included."""
+    import torch
+
+    from odesat_amd.partition import CLAUSES, VARIABLES, LocalComm, PartitionedSolver
+
+    name, n, cp, var, neg = gen(seed)
+    m = len(cp) - 1
+    T = np.float32
+    o = Oracle(cp, var, neg, n, "f32")
+    steps, dt, zeta = 25, T(0.05), T(0.01)
+    v = init_voltages(5, 0, 1, n)[0].astype(T)
+    xs, xl = o.init_short_term_memory(), np.ones(m, T)
+    init = (v.copy(), xs.copy(), xl.copy())
+    sats = [o.euler_step_fixed(v, xs, xl, dt, zeta) for _ in range(steps)]
+    exp_sat = next((k for k, s in enumerate(sats) if s), -1)
+    cases = [(VARIABLES, w) for w in (1, 2, 3, 4) if w <= n] + [(CLAUSES, 1)]
+    for env in PART_ENVS[seed // 2 % len(PART_ENVS):][:2]:
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            for mode, world in cases:
+                parts = [PartitionedSolver(cp, var, neg, n, mode, comm=LocalComm(r, world)) for r in range(world)]
+                for p in parts:
+                    p.set_state(*init)
+                for _ in range(steps):
+                    for p in parts:
+                        p.rhs(float(dt), float(zeta), False)
+                    if mode == VARIABLES:
+                        g = torch.cat([p.out for p in parts])
+                        for p in parts:
+                            p.v.copy_(g)
+                    for p in parts:
+                        p.post(float(dt))
+                ctx = f"{name} mode {mode} world {world} env {env}"
+                for p in parts:
+                    st = p.status(False)
+                    gv, gxs, gxl, loc = p.get_state()
+                    assert st["steps_done"] == steps and st["first_sat_step"] == exp_sat, ctx
+                    assert same(gv.astype(T), v), ctx
+                    assert same(gxs.astype(T), xs[loc]) and same(gxl.astype(T), xl[loc]), ctx
+                    p.close()
+        finally:
+            for k, x in old.items():
+                if x is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = x
+
+
+# --------------------------------------------------------------------- the discrete search -----
+@pytest.mark.parametrize("seed", range(1, 48, 2))
+def test_fuzz_stoch_matches_oracle(seed):
+    """stoch.rs's search (csrc/stoch.hip) on the fuzzed shapes, both kernel paths (the one-wave LDS
+    kernel at the workgroup widths the solver picks, and the three-kernel HBM path): v, xl, the sat
+    step and the steps taken bit for bit against oracle/stoch_oracle.c.  Variables that occur in no
+    clause are renamed away first (the reference panics on them, stoch.rs:70)."""
+    from odesat_amd.stoch import StochSearch
+
+    name, n, cp, var, neg = gen(seed)
+    used = np.unique(var)
+    if len(used) == 0:
+        pytest.skip("no literal")
+    remap = np.full(n, -1, np.int64)
+    remap[used] = np.arange(len(used))
+    var, n = remap[var], len(used)
+    o = Oracle(cp, var, neg, n, "f64")
+    f = cnf.CNFFormula.from_arrays(cp, var, neg, n)
+    B, steps, rs = [1, 7, 70][seed % 3], 120, 3 + seed
+    for path in ("wave", "hbm"):
+        old = os.environ.get("ODESAT_STOCH_WAVE")
+        if path == "hbm":
+            os.environ["ODESAT_STOCH_WAVE"] = "0"
+        try:
+            with StochSearch(f, B) as s:
+                r = s.search(rs, steps, replica0=11)
+                gv, gxl = s.get_state()
+        finally:
+            if old is None:
+                os.environ.pop("ODESAT_STOCH_WAVE", None)
+            else:
+                os.environ["ODESAT_STOCH_WAVE"] = old
+        for b in range(B):
+            v = np.zeros(n, np.uint8)
+            xl = np.ones(len(cp) - 1, np.uint64)
+            t, sat = o.stoch_search(v, xl, rs, 11 + b, steps)
+            ctx = f"{name} {path} replica {b}"
+            assert np.array_equal(gv[b], v.astype(bool)) and np.array_equal(gxl[b], xl), ctx
+            assert r["steps_done"][b] == t and r["first_sat_step"][b] == (t - 1 if sat else -1), ctx
