@@ -261,10 +261,13 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int t = t0 + u;
-            const uint32_t ma = mem_addr(a, min(t + 1 - TR, last), lane);
+            // the step's second half works on tile t + 1; after the last tile there is none, and
+            // its (discarded) update must not land on the last tile's memories
+            const int lt = t + 1 - TR;
+            const uint32_t ma = mem_addr(a, min(lt, last), lane);
             float2 m = *lds_f2(ma);
             tile_step(a, R, ring[(u + 3) % 4], m, P, Fn, Gn, t, h, hh, cmax, S);
-            *lds_f2(ma) = m;
+            if (lt <= last) *lds_f2(ma) = m;
         }
     }
 }

@@ -74,6 +74,9 @@ def local_topology(cp, var, neg, n: int, mode: int, rank: int, world: int, order
         owner = np.repeat(np.arange(m, dtype=np.int64), lens_all)
         touch = np.zeros(m, bool)
         touch[owner[(var >= v0) & (var < v1)]] = True
+        # a clause with no literal touches no variable, but it is never satisfied (system.rs:43-57
+        # leaves its C at infinity): rank 0 holds it, so its unsat flag reaches the stop check
+        touch[lens_all == 0] = rank == 0
         local = np.flatnonzero(touch).astype(np.int64)
     else:
         raise ValueError("mode must be CLAUSES or VARIABLES")

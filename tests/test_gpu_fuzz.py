@@ -21,6 +21,13 @@ from odesat_amd.system import ODESAT_STOP_EACH, Solver
 
 pytestmark = pytest.mark.gpu
 
+NSEED = int(os.environ.get("ODESAT_FUZZ_SEEDS", "48"))  # a longer hunt: ODESAT_FUZZ_SEEDS=400
+# seeds the 400-seed hunt failed on before their fixes, kept in every run: ONCHIP with the tiles
+# spilling into LDS and a clause in the last one (253, 258, 282), and the VARIABLES partition of a
+# formula with an empty clause (76, 112, 202)
+PATH_SEEDS = sorted(set(range(NSEED)) | {253, 258, 282})
+PART_SEEDS = sorted(set(range(0, NSEED, 2)) | {76, 112, 202})
+
 T_OF = {"f64": np.float64, "f32": np.float32}
 
 
@@ -103,7 +110,7 @@ def run_variant(f, B, prec, env, alg, adaptive, K, poll):
                 os.environ[k] = x
 
 
-@pytest.mark.parametrize("seed", range(48))
+@pytest.mark.parametrize("seed", PATH_SEEDS)
 @pytest.mark.parametrize("prec", ["f32", "f64"])
 def test_fuzz_every_path_matches_oracle(seed, prec):
     name, n, cp, var, neg = gen(seed)
@@ -164,7 +171,7 @@ PART_ENVS = [{}, {"ODESAT_PART_TERMS": "slot"}, {"ODESAT_PART_TERMS": "ell"}, {"
              {"ODESAT_PART_K3": "0"}, {"ODESAT_PART_XCD": "1"}]
 
 
-@pytest.mark.parametrize("seed", range(0, 48, 2))
+@pytest.mark.parametrize("seed", PART_SEEDS)
 def test_fuzz_partition_matches_oracle(seed):
     """The partitioned single-replica kernels (csrc/partition.hip, config 5's path) on the fuzzed
     shapes: VARIABLES at world 1-4 (ranks of one process sharing the device, the all-gather done
@@ -219,7 +226,7 @@ def test_fuzz_partition_matches_oracle(seed):
 
 
 # --------------------------------------------------------------------- the discrete search -----
-@pytest.mark.parametrize("seed", range(1, 48, 2))
+@pytest.mark.parametrize("seed", range(1, NSEED, 2))
 def test_fuzz_stoch_matches_oracle(seed):
     """stoch.rs's search (csrc/stoch.hip) on the fuzzed shapes, both kernel paths (the one-wave LDS
     kernel at the workgroup widths the solver picks, and the three-kernel HBM path): v, xl, the sat
