@@ -264,3 +264,72 @@ def test_fuzz_stoch_matches_oracle(seed):
             ctx = f"{name} {path} replica {b}"
             assert np.array_equal(gv[b], v.astype(bool)) and np.array_equal(gxl[b], xl), ctx
             assert r["steps_done"][b] == t and r["first_sat_step"][b] == (t - 1 if sat else -1), ctx
+
+
+# --------------------------------------------------------------- inter mode and forced steps ---
+@pytest.mark.parametrize("seed", range(0, NSEED, 3))
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_fuzz_stop_policies_agree(seed, prec):
+    """STOP_ANY (simulate_inter, system.rs:241-359: every replica stops at the first step any replica
+    is allsat -- the persistent kernels run multi-step launches and replay from a snapshot when the
+    stop fell inside one) and STOP_NONE (every replica takes every step), fixed and adaptive steps,
+    on every path: bit-identical to FUSED, which for fixed steps under STOP_ANY is held to the
+    oracle's simulate_inter (the winner's stop step and every replica's state)."""
+    from odesat_amd.system import ODESAT_STOP_ANY, ODESAT_STOP_NONE
+
+    name, n, cp, var, neg = gen(seed)
+    f = cnf.CNFFormula.from_arrays(cp, var, neg, n)
+    m = len(cp) - 1
+    widths = np.diff(cp)
+    uniform3 = bool((widths == 3).all())
+    distinct = uniform3 and all(len(set(var[3 * c:3 * c + 3].tolist())) == 3 for c in range(m))
+    B = [2, 9, 70][seed % 3]
+    K = 60
+    poll = [5, 13, 60][(seed // 3) % 3]
+    for stop in (ODESAT_STOP_ANY, ODESAT_STOP_NONE):
+        for adaptive in (False, True):
+            def run(env, alg):
+                old = {k: os.environ.get(k) for k in env}
+                os.environ.update(env)
+                try:
+                    with Solver(f, B, prec) as s:
+                        if alg is not None:
+                            try:
+                                s.set_algorithm(alg)
+                            except _lib.OdesatError:
+                                return None
+                        s.init_state(13)
+                        r = s.simulate(adaptive=adaptive, dt=0.01 if adaptive else 0.05, tol=1e-3, zeta=0.01,
+                                       max_steps=K, stop=stop, poll_interval=poll)
+                        return s.algorithm, r, s.get_state()
+                finally:
+                    for k, x in old.items():
+                        if x is None:
+                            os.environ.pop(k, None)
+                        else:
+                            os.environ[k] = x
+
+            base = run({}, _lib.ODESAT_ALG_FUSED)
+            _, rb, sb = base
+            if stop == ODESAT_STOP_ANY and not adaptive:
+                T = T_OF[prec]
+                o = Oracle(cp, var, neg, n, prec)
+                v = init_voltages(13, 0, B, n).astype(T)
+                xs = np.tile(o.init_short_term_memory(), (B, 1))
+                xl = np.ones((B, m), T)
+                t, win, _, _ = o.simulate_inter(v, xs, xl, dt=T(0.05), steps=K, zeta=T(0.01))
+                assert rb["steps_run"] == t, name
+                for b in range(B):
+                    assert same(sb[0][b], v[b]) and same(sb[1][b], xs[b]) and same(sb[2][b], xl[b]), (name, b)
+            for label, env, alg in variants(prec, uniform3, distinct):
+                out = run(env, alg)
+                if out is None:
+                    continue
+                galg, r, st = out
+                ctx = f"{name} {prec} stop {stop} {'adaptive' if adaptive else 'fixed'} {label} (alg {galg})"
+                assert r["steps_run"] == rb["steps_run"], ctx
+                assert np.array_equal(r["first_sat_step"], rb["first_sat_step"]), ctx
+                assert np.array_equal(r["steps_done"], rb["steps_done"]), ctx
+                assert same(r["dt"], rb["dt"]), ctx
+                for x, y in zip(st, sb):
+                    assert same(x, y), ctx
