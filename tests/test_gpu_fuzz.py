@@ -333,3 +333,67 @@ def test_fuzz_stop_policies_agree(seed, prec):
                 assert same(r["dt"], rb["dt"]), ctx
                 for x, y in zip(st, sb):
                     assert same(x, y), ctx
+
+
+# ------------------------------------------------------------------ caller-supplied states -----
+@pytest.mark.parametrize("seed", range(1, NSEED, 3))
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+def test_fuzz_caller_states_match_oracle(seed, prec):
+    """The reference integrates whatever State it is handed (system.rs:156: `state: &mut State`).
+    Caller states through odesat_set_state: voltages outside [-1, 1], memories outside their clamps,
+    and exact lattice values (v in {-1, 0, 1}: ties in the min / second-min scan and the rigidity term
+    firing, system.rs:73-80) -- on every path (ONCHIP takes only in-range states and runs such a
+    call's first step on RESIDENT), fixed and adaptive, against the oracle bit for bit."""
+    name, n, cp, var, neg = gen(seed)
+    f = cnf.CNFFormula.from_arrays(cp, var, neg, n)
+    T = T_OF[prec]
+    o = Oracle(cp, var, neg, n, prec)
+    m = len(cp) - 1
+    widths = np.diff(cp)
+    uniform3 = bool((widths == 3).all())
+    distinct = uniform3 and all(len(set(var[3 * c:3 * c + 3].tolist())) == 3 for c in range(m))
+    rng = np.random.default_rng(1000 + seed)
+    B, K = [3, 8, 40][seed % 3], 30
+    v = rng.uniform(-1.5, 1.5, (B, n))
+    xs = rng.uniform(-0.2, 1.2, (B, m))
+    xl = rng.uniform(0.5, 50.0, (B, m))
+    lat = rng.random(B) < 0.5  # lattice replicas
+    v[lat] = rng.integers(-1, 2, (int(lat.sum()), n))
+    xs[lat] = rng.choice([0.001, 0.5, 0.999], (int(lat.sum()), m))
+    xl[lat] = rng.choice([1.0, 7.0], (int(lat.sum()), m))
+    v, xs, xl = (a.astype(T).astype(np.float64) for a in (v, xs, xl))  # the precision's own values
+    for adaptive in (False, True):
+        ref = []
+        for b in range(B):
+            ov, oxs, oxl = v[b].astype(T), xs[b].astype(T), xl[b].astype(T)
+            if adaptive:
+                t, sat, _, _, _ = o.simulate(ov, oxs, oxl, tol=T(1e-3), dt=None, steps=K, zeta=T(0.01))
+            else:
+                t, sat, _, _, _ = o.simulate(ov, oxs, oxl, dt=T(0.05), steps=K, zeta=T(0.01))
+            ref.append((t, sat, ov, oxs, oxl))
+        for label, env, alg in variants(prec, uniform3, distinct):
+            old = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            try:
+                with Solver(f, B, prec) as s:
+                    if alg is not None:
+                        try:
+                            s.set_algorithm(alg)
+                        except _lib.OdesatError:
+                            continue
+                    s.set_state(v, xs, xl)
+                    r = s.simulate(adaptive=adaptive, dt=0.01 if adaptive else 0.05, tol=1e-3, zeta=0.01,
+                                   max_steps=K, stop=ODESAT_STOP_EACH, poll_interval=[4, 9, 30][seed % 3])
+                    galg = s.algorithm
+                    gv, gxs, gxl = s.get_state()
+            finally:
+                for k, x in old.items():
+                    if x is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = x
+            for b in range(B):
+                t, sat, ov, oxs, oxl = ref[b]
+                ctx = f"{name} {prec} {'adaptive' if adaptive else 'fixed'} {label} (alg {galg}) replica {b}"
+                assert r["steps_done"][b] == t and (r["first_sat_step"][b] >= 0) == sat, ctx
+                assert same(gv[b], ov) and same(gxs[b], oxs) and same(gxl[b], oxl), ctx
