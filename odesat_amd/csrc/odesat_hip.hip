@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -75,7 +76,7 @@ struct odesat_solver {
     // memories in VGPRs, [oc_tr, oc_tr + oc_tl) in LDS.  oc_tr == 0: not available
     int oc_tr = 0, oc_tl = 0;
     uint64_t *oc_rec = nullptr;  // [tiles][512] slot-major clause records (onchip::make_rec)
-    int32_t *oc_tcp = nullptr;   // [ntp + 1] tile starts padded with m (static-index loads in k_onchip)
+    int32_t *oc_tcp = nullptr;   // [ntp * 8 + 1] wave starts (t * 8 + w) padded with m (static-index loads in k_onchip)
     int64_t oc_rec_bytes = 0;
     bool in_range = true;        // every replica's state is in ONCHIP's range (onchip.hip header)
     int64_t bytes = 0;
@@ -520,21 +521,93 @@ int small_instance_width(const odesat_cnf *f, int64_t n, int64_t batch, int devi
     return R;
 }
 
-bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, std::vector<int32_t> &perm,
-                 std::vector<int32_t> &tc, std::vector<uint8_t> &code) {
+// Wave-paired tiles (ONCHIP, onchip.hip: one barrier per PAIR of tiles).  Tiles 2i and 2i+1 form
+// one barrier interval, and slots [64w, 64w + 64) of a tile are wave w's.  LDS operations of one
+// wave complete in issue order, so a clause may sit in the interval's second tile after a clause
+// it shares a variable with in the first tile when both are in the same wave; across waves the
+// order still needs the barrier after the pair.  Greedy in the reference's clause order: clause c
+// goes to the first tile after the tiles of its variables' last clauses where every one of those
+// in the same interval is in one wave w, and w has room (c then takes w); a clause with none there
+// takes the least-filled wave.  Each tile stays var-disjoint and every variable's tiles increase in
+// clause order, so the tiling is also a RESIDENT tiling.  Config 2: 91 tiles in 46 intervals
+// (plain greedy: 90 tiles, 90 barriers).
+constexpr int PAIR_WAVES = 8, PAIR_WAVE_CAP = 64;
+
+void pair_tiles(const odesat_cnf *f, int64_t n, std::vector<int32_t> &tile_of, std::vector<int8_t> &wave_of,
+                std::vector<int32_t> &fill) {
+    const int64_t m = f->nclauses();
+    std::vector<int32_t> lastt((size_t)n, -1);
+    std::vector<int8_t> lastw((size_t)n, -1);
+    std::vector<std::array<int32_t, PAIR_WAVES>> wf;  // per tile, per wave fill
+    tile_of.assign((size_t)m, 0);
+    wave_of.assign((size_t)m, 0);
+    for (int64_t c = 0; c < m; ++c) {
+        const int64_t b = f->clause_ptr[c], e = f->clause_ptr[c + 1];
+        int32_t t = 0;
+        for (int64_t sl = b; sl < e; ++sl) t = std::max(t, lastt[f->var[sl]] + 1);
+        int w = -1;
+        for (;;) {
+            while ((int32_t)wf.size() <= t) wf.push_back({});
+            int want = -1;
+            bool split = false;
+            for (int64_t sl = b; sl < e; ++sl) {  // last clauses of c's variables in t's interval
+                const int32_t lt = lastt[f->var[sl]];
+                if (lt >= 0 && lt / 2 == t / 2) {
+                    const int lw = lastw[f->var[sl]];
+                    if (want >= 0 && want != lw) split = true;
+                    want = lw;
+                }
+            }
+            if (split) {  // in two waves: only the next interval orders c after both
+                t = (t / 2 + 1) * 2;
+                continue;
+            }
+            if (want >= 0) {
+                if (wf[t][want] < PAIR_WAVE_CAP) { w = want; break; }
+                ++t;
+                continue;
+            }
+            for (int k = 0; k < PAIR_WAVES; ++k)
+                if (wf[t][k] < PAIR_WAVE_CAP && (w < 0 || wf[t][k] < wf[t][w])) w = k;
+            if (w >= 0) break;
+            ++t;
+        }
+        wf[t][w] += 1;
+        tile_of[c] = t;
+        wave_of[c] = (int8_t)w;
+        for (int64_t sl = b; sl < e; ++sl) {
+            lastt[f->var[sl]] = t;
+            lastw[f->var[sl]] = (int8_t)w;
+        }
+    }
+    fill.assign(wf.size(), 0);
+    for (size_t t = 0; t < wf.size(); ++t)
+        for (int k = 0; k < PAIR_WAVES; ++k) fill[t] += wf[t][k];
+}
+
+// wst (pairs only): [ntiles * 8 + 1] internal clause of wave w's first slot in tile t at t * 8 + w;
+// a tile's clauses are stored wave by wave, so wave w of tile t holds wst[t*8+w+1] - wst[t*8+w].
+bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, bool pairs, std::vector<int32_t> &perm,
+                 std::vector<int32_t> &tc, std::vector<uint8_t> &code, std::vector<int32_t> &wst) {
     const int64_t m = f->nclauses();
     std::vector<int32_t> last((size_t)n, -1), tile_of((size_t)m), fill;
-    int32_t first_open = 0;  // every tile before it is full
-    for (int64_t c = 0; c < m; ++c) {
-        int32_t t = 0;
-        for (int64_t sl = f->clause_ptr[c]; sl < f->clause_ptr[c + 1]; ++sl) t = std::max(t, last[f->var[sl]] + 1);
-        t = std::max(t, first_open);
-        while (t < (int32_t)fill.size() && fill[t] >= cap) ++t;
-        if (t == (int32_t)fill.size()) fill.push_back(0);
-        fill[t] += 1;
-        while (first_open < (int32_t)fill.size() && fill[first_open] >= cap) ++first_open;
-        tile_of[c] = t;
-        for (int64_t sl = f->clause_ptr[c]; sl < f->clause_ptr[c + 1]; ++sl) last[f->var[sl]] = t;
+    std::vector<int8_t> wave_of;
+    wst.clear();
+    if (pairs) {
+        pair_tiles(f, n, tile_of, wave_of, fill);
+    } else {
+        int32_t first_open = 0;  // every tile before it is full
+        for (int64_t c = 0; c < m; ++c) {
+            int32_t t = 0;
+            for (int64_t sl = f->clause_ptr[c]; sl < f->clause_ptr[c + 1]; ++sl) t = std::max(t, last[f->var[sl]] + 1);
+            t = std::max(t, first_open);
+            while (t < (int32_t)fill.size() && fill[t] >= cap) ++t;
+            if (t == (int32_t)fill.size()) fill.push_back(0);
+            fill[t] += 1;
+            while (first_open < (int32_t)fill.size() && fill[first_open] >= cap) ++first_open;
+            tile_of[c] = t;
+            for (int64_t sl = f->clause_ptr[c]; sl < f->clause_ptr[c + 1]; ++sl) last[f->var[sl]] = t;
+        }
     }
     // a var-disjoint tile holds at most n slots and `cap` clauses: fall back to FUSED only when the
     // tiling is far from that bound (e.g. one variable in every clause)
@@ -543,11 +616,25 @@ bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, std::v
     if (nt > 8 * bound + 16) return false;
     tc.assign((size_t)nt + 1, 0);
     for (int64_t t = 0; t < nt; ++t) tc[t + 1] = tc[t] + fill[t];
-    std::vector<int32_t> pos(tc.begin(), tc.end() - 1);
     perm.assign((size_t)m, 0);
-    for (int64_t c = 0; c < m; ++c) perm[pos[tile_of[c]]++] = (int32_t)c;  // original order inside a tile
     code.assign((size_t)m, 0);  // indexed by ORIGINAL clause here; remapped below
-    if (k3) {
+    if (pairs) {  // wave by wave inside a tile; the bank layout deals each wave's clauses to its half-waves
+        wst.assign((size_t)nt * PAIR_WAVES + 1, 0);
+        for (int64_t c = 0; c < m; ++c) wst[(size_t)tile_of[c] * PAIR_WAVES + wave_of[c] + 1] += 1;
+        for (size_t i = 1; i < wst.size(); ++i) wst[i] += wst[i - 1];
+        std::vector<int32_t> pos(wst.begin(), wst.end() - 1);
+        for (int64_t c = 0; c < m; ++c) perm[pos[(size_t)tile_of[c] * PAIR_WAVES + wave_of[c]]++] = (int32_t)c;
+        if (k3)
+            for (size_t g = 0; g + 1 < wst.size(); ++g) {
+                std::vector<int32_t> cl(perm.begin() + wst[g], perm.begin() + wst[g + 1]);
+                bank_layout(f, R, cl, code);
+                std::copy(cl.begin(), cl.end(), perm.begin() + wst[g]);
+            }
+    } else {
+        std::vector<int32_t> pos(tc.begin(), tc.end() - 1);
+        for (int64_t c = 0; c < m; ++c) perm[pos[tile_of[c]]++] = (int32_t)c;  // original order inside a tile
+    }
+    if (k3 && !pairs) {
         for (int64_t t = 0; t < nt; ++t) {
             std::vector<int32_t> cl(perm.begin() + tc[t], perm.begin() + tc[t + 1]);
             bank_layout(f, R, cl, code);
@@ -562,13 +649,14 @@ bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, std::v
 
 // ONCHIP eligibility and slot-major records (onchip.hpp).  tiles = the padded tile starts, lits =
 // the internal-order literals (var << 1 | neg).
-int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std::vector<int32_t> &lits) {
+int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std::vector<int32_t> &wst,
+                 const std::vector<int32_t> &lits) {
     if (s->res_R != 1 || s->res_narrow || s->res_wave || s->dtype != ODESAT_F32 || s->uniform_k != 3 || s->n > onchip::MAX_N)
         return ODESAT_OK;
     if (const char *ev = std::getenv("ODESAT_ONCHIP"))
         if (std::atoi(ev) == 0) return ODESAT_OK;
     const int nt = (int)tiles.size() - 1;
-    if (nt == 0 || s->m == 0) return ODESAT_OK;
+    if (nt == 0 || s->m == 0 || wst.empty()) return ODESAT_OK;  // k_onchip runs wave-paired tiles only
     for (int64_t k = 0; k < s->m; ++k) {  // three distinct variables per clause (independent dv updates)
         const int32_t x = lits[3 * k] >> 1, y = lits[3 * k + 1] >> 1, z = lits[3 * k + 2] >> 1;
         if (x == y || x == z || y == z) return ODESAT_OK;
@@ -583,15 +671,22 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
     // starts at a multiple of 4; nt is one)
     if (tr == 0 && nt - onchip::TR_MAX <= tl_max) tr = onchip::TR_MAX;
     if (tr == 0) return ODESAT_OK;
+    // wave starts (build_tiles): wave w of tile t holds internal clauses [ws[t*8+w], ws[t*8+w+1]),
+    // padded with m past the last tile, so the kernel reads a tile's wave bounds at static offsets
+    // (a padded tile is empty)
+    const int W8 = onchip::WAVES;
+    const int ntp = std::max(nt, tr) + 8;
+    std::vector<int32_t> ws((size_t)ntp * W8 + 1, (int32_t)s->m);
+    std::copy(wst.begin(), wst.end() - 1, ws.begin());
     // slot-major records, padded with empty tiles so every tile a pass touches exists; an empty
     // slot of lane l points all three literals at sink word n + l % 32 (v = 1.0 there)
-    const int ntp = std::max(nt, tr) + 8;
     std::vector<uint64_t> rec((size_t)ntp * onchip::NTH);
     for (int t = 0; t < ntp; ++t)
         for (int l = 0; l < onchip::NTH; ++l) {
-            const int32_t k = t < nt ? tiles[t] + l : -1;
+            const size_t g = (size_t)t * W8 + l / 64;
+            const int32_t k = ws[g] + l % 64;
             uint64_t r;
-            if (k >= 0 && k < tiles[t + 1]) {
+            if (k < ws[g + 1]) {
                 const int32_t *q = &lits[3 * (size_t)k];
                 r = onchip::make_rec(4u * (uint32_t)(q[0] >> 1), 4u * (uint32_t)(q[1] >> 1), 4u * (uint32_t)(q[2] >> 1),
                                      q[0] & 1, q[1] & 1, q[2] & 1);
@@ -605,12 +700,8 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
     s->oc_rec_bytes = (int64_t)(rec.size() * sizeof(uint64_t));
     if ((rc = dmalloc(s, (void **)&s->oc_rec, rec.size() * sizeof(uint64_t)))) return rc;
     HIP_TRY(hipMemcpy(s->oc_rec, rec.data(), rec.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-    // tile starts padded with m past the last tile, so the kernel reads tile j's start and end at
-    // static offsets (no clamp): a padded tile is empty (its lanes load clause m - 1, store nothing)
-    std::vector<int32_t> tcp((size_t)ntp + 1, (int32_t)s->m);
-    for (int t = 0; t <= nt; ++t) tcp[t] = tiles[t];
-    if ((rc = dmalloc(s, (void **)&s->oc_tcp, tcp.size() * 4))) return rc;
-    HIP_TRY(hipMemcpy(s->oc_tcp, tcp.data(), tcp.size() * 4, hipMemcpyHostToDevice));
+    if ((rc = dmalloc(s, (void **)&s->oc_tcp, ws.size() * 4))) return rc;
+    HIP_TRY(hipMemcpy(s->oc_tcp, ws.data(), ws.size() * 4, hipMemcpyHostToDevice));
     s->oc_tr = tr;
     s->oc_tl = tr < live ? nt - tr : 0;
     return ODESAT_OK;
@@ -1079,15 +1170,21 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         else s->res_narrow = 4 * tile_count(f, n, RES_NARROW) <= 5 * tile_count(f, n, ResShape<1>::NL);
     }
     // the internal clause order: var-disjoint tiles for RESIDENT, else the file order
-    std::vector<int32_t> perm, tiles;
+    std::vector<int32_t> perm, tiles, wst;
     std::vector<uint8_t> lorder;  // per internal clause: literal order code (kP3), 0 = file order
+    // wave-paired tiles where ONCHIP may run (onchip_setup's conditions; k_onchip needs them);
+    // ODESAT_ONCHIP_PAIRS=0: plain tiles (RESIDENT)
+    bool pairs = res_r == 1 && !s->res_narrow && !s->res_wave && s->dtype == ODESAT_F32 && s->uniform_k == 3 &&
+                 n <= onchip::MAX_N;
+    if (const char *ev = std::getenv("ODESAT_ONCHIP")) pairs = pairs && std::atoi(ev) != 0;
+    if (const char *ev = std::getenv("ODESAT_ONCHIP_PAIRS")) pairs = pairs && std::atoi(ev) != 0;
     const int cap = s->res_narrow ? RES_NARROW : res_capacity(res_r);
     if (s->res_wave) {  // no tiles: the file order, one pseudo-tile
         perm.resize(m);
         for (int64_t c = 0; c < m; ++c) perm[c] = (int32_t)c;
         tiles = {0, (int32_t)m};
         lorder.assign(m, 0);
-    } else if (res_r > 0 && !build_tiles(f, n, cap, res_r, s->uniform_k == 3, perm, tiles, lorder)) {
+    } else if (res_r > 0 && !build_tiles(f, n, cap, res_r, s->uniform_k == 3, pairs, perm, tiles, lorder, wst)) {
         res_r = 0;
     }
     if (res_r != 1) s->res_narrow = false;
@@ -1215,7 +1312,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
                 return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
             s->res_ada = true;  // wave_lds_bytes(adaptive) fits by selection
         }
-        if ((rc = onchip_setup(s, tiles, lits))) return bail(rc);
+        if ((rc = onchip_setup(s, tiles, wst, lits))) return bail(rc);
         if (s->oc_tr > 0) s->alg = ODESAT_ALG_ONCHIP;
     }
     // state (double-buffered)

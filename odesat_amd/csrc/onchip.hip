@@ -166,7 +166,7 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
 // second half and tile t+2's first half -- independent, so they interleave -- while the writes
 // and the gathers drain.  The barrier then orders tile t's dv against tile t+1's.
 __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &slot3, float2 &mem1, Pend &P, Front &Fn,
-                                          Gath &Gn, int t, float h, float hh, uint32_t &cmax, Stamps &S) {
+                                          Gath &Gn, int t, float h, float hh, uint32_t &cmax, Stamps &S, bool bar) {
     const float o0 = lds_f(P.a0 + DVC), o1 = lds_f(P.a1 + DVC), o2 = lds_f(P.a2 + DVC);
     lds_st(P.a0 + DVC, o0 + P.d0);
     lds_st(P.a1 + DVC, o1 + P.d1);
@@ -187,7 +187,7 @@ __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &sl
     const uint64_t t_pre = memtime();
     S.work += t_pre - S.last;
 #endif
-    __syncthreads();
+    if (bar) __syncthreads();  // static: only after the second tile of a pair
     __builtin_amdgcn_sched_barrier(0);
 #ifdef ONCHIP_STAMPS
     S.last = memtime();
@@ -210,12 +210,13 @@ __device__ __forceinline__ uint32_t mem_addr(const Args &a, int lt, int lane) {
 template <int TR, int T>
 __device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&mr)[TR], Slot (&ring)[4], Pend &P,
                                          Front &Fn, Gath &Gn, float h, float hh, int lane, uint32_t &cmax, Stamps &S) {
+    constexpr bool bar = (T & 1) != 0;  // wave-paired tiles: a barrier after the second of a pair
     if constexpr (T + 1 < TR) {
-        tile_step(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, cmax, S);
+        tile_step(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, cmax, S, bar);
     } else {  // tile TR is the first LDS tile (if any)
         float2 m = make_float2(0.0f, 0.0f);
         if (a.tl > 0) m = *lds_f2(mem_addr(a, 0, lane));
-        tile_step(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, cmax, S);
+        tile_step(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, cmax, S, bar);
         if (a.tl > 0) *lds_f2(mem_addr(a, 0, lane)) = m;
     }
 }
@@ -266,7 +267,7 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
             const int lt = t + 1 - TR;
             const uint32_t ma = mem_addr(a, min(lt, last), lane);
             float2 m = *lds_f2(ma);
-            tile_step(a, R, ring[(u + 3) % 4], m, P, Fn, Gn, t, h, hh, cmax, S);
+            tile_step(a, R, ring[(u + 3) % 4], m, P, Fn, Gn, t, h, hh, cmax, S, (u & 1) != 0);  // TR is even
             if (lt <= last) *lds_f2(ma) = m;
         }
     }
@@ -280,40 +281,43 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mem_rsrc(float *base, int m) {
     return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, 8 * m, 0x00020000);
 }
 
-// Load the register tiles' memories.  Tile j's start is a scalar load at a static offset of the
-// padded tile table (a tile past the last one starts at m), so the compiler batches them into wide
-// scalar loads.  The loads are unconditional: a slot past the end of the memories reads 0 (buffer
+// Load the register tiles' memories.  The start of this wave's clauses in tile j is a scalar load
+// at a static offset of the padded wave table (tcw = tc + wave; a tile past the last one starts at
+// m), so the compiler batches them into wide scalar loads.  The loads are unconditional: a slot past the end of the memories reads 0 (buffer
 // range check), any other empty slot reads the next tile's clause -- neither is used, since an
 // empty slot's literals point at the sink words (its terms go to the dv sinks) and its update is
 // not stored.
 template <int TR, int... Js>
-__device__ __forceinline__ void mem_load(std::integer_sequence<int, Js...>, const cint32 *tc,
+__device__ __forceinline__ void mem_load(std::integer_sequence<int, Js...>, const cint32 *tcw,
                                          __amdgpu_buffer_rsrc_t rs, uint32_t lane8, float2 (&mr)[TR]) {
     typedef int i2 __attribute__((ext_vector_type(2)));
     auto one = [&](auto J) {
         constexpr int j = decltype(J)::value;
-        const i2 r = __builtin_amdgcn_raw_buffer_load_b64(rs, lane8 + 8u * (uint32_t)tc[j], 0, 0);
+        const i2 r = __builtin_amdgcn_raw_buffer_load_b64(rs, lane8 + 8u * (uint32_t)tcw[j * WAVES], 0, 0);
         mr[j] = make_float2(__int_as_float(r.x), __int_as_float(r.y));
     };
     (one(std::integral_constant<int, Js>{}), ...);
 }
 
-// Store them back, 8 tiles at a time (the last group may be shorter): the group's tile bounds are
-// loaded together (one wide scalar load, no wait per tile); a lane whose slot of tile j holds no
-// clause stores out of the buffer's range, which drops the store.
+// Store them back, 8 tiles at a time (the last group may be shorter): the group's wave bounds are
+// loaded together (scalar loads, no wait per tile); a lane whose slot of tile j holds no clause
+// stores out of the buffer's range, which drops the store.
 template <int TR, int... Gs>
-__device__ __forceinline__ void mem_store(std::integer_sequence<int, Gs...>, const cint32 *tc,
+__device__ __forceinline__ void mem_store(std::integer_sequence<int, Gs...>, const cint32 *tcw,
                                           __amdgpu_buffer_rsrc_t rs, int lane, const float2 (&mr)[TR]) {
     typedef int i2 __attribute__((ext_vector_type(2)));
     auto group = [&](auto G) {
         constexpr int j0 = decltype(G)::value * 8;
         constexpr int cnt = TR - j0 < 8 ? TR - j0 : 8;
-        int b[9];
-#pragma unroll
-        for (int k = 0; k <= cnt; ++k) b[k] = tc[j0 + k];
+        int b[8], e[8];
 #pragma unroll
         for (int k = 0; k < cnt; ++k) {
-            const uint32_t vo = lane < b[k + 1] - b[k] ? 8u * (uint32_t)(b[k] + lane) : 0x80000000u;
+            b[k] = tcw[(j0 + k) * WAVES];
+            e[k] = tcw[(j0 + k) * WAVES + 1];
+        }
+#pragma unroll
+        for (int k = 0; k < cnt; ++k) {
+            const uint32_t vo = lane < e[k] - b[k] ? 8u * (uint32_t)(b[k] + lane) : 0x80000000u;
             i2 r;
             r.x = __float_as_int(mr[j0 + k].x);
             r.y = __float_as_int(mr[j0 + k].y);
@@ -327,6 +331,7 @@ __device__ __forceinline__ void mem_store(std::integer_sequence<int, Gs...>, con
 template <int TR>
 __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     const int g = blockIdx.x, lane = threadIdx.x;
+    const int wl = lane & 63;  // slot of this lane in its wave's share of a tile
     int act = a.act[g];
     if (!act) return;  // frozen replica (uniform)
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
@@ -339,7 +344,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     const int n2 = a.n + SINKS;
     const uint32_t UNS = DVC + 4u * (uint32_t)n2;  // two unsat flags
     int64_t sat = a.sat_step[g], done = a.steps_done[g];
-    const cint32 *tc = (const cint32 *)a.tc;
+    const cint32 *tcw = (const cint32 *)a.tc + __builtin_amdgcn_readfirstlane(lane >> 6);  // this wave's starts
 
     {   // v (sinks = 1.0) into LDS, dv = 0 (:33): the loads of a pass issued together, then the stores
         constexpr int U = 16;
@@ -359,11 +364,11 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     }
     const int mlast = a.m - 1;
     float2 mr[TR];
-    mem_load<TR>(std::make_integer_sequence<int, TR>{}, tc, mem_rsrc((p ? a.c1 : a.c0) + (size_t)g * a.m * 2, a.m),
-                 8u * (uint32_t)lane, mr);
+    mem_load<TR>(std::make_integer_sequence<int, TR>{}, tcw, mem_rsrc((p ? a.c1 : a.c0) + (size_t)g * a.m * 2, a.m),
+                 8u * (uint32_t)wl, mr);
     for (int t = 0; t < a.tl; ++t) {
-        const int c0 = tc[TR + t];
-        *lds_f2(mem_addr(a, t, lane)) = CM[min(c0 + lane, mlast)];  // (empty slots: as mem_io)
+        const int c0 = tcw[(TR + t) * WAVES];
+        *lds_f2(mem_addr(a, t, lane)) = CM[min(c0 + wl, mlast)];  // (empty slots: as mem_io)
     }
     if (lane < 2) lds_st(UNS + 4u * lane, 0.0f);
     __syncthreads();
@@ -401,12 +406,12 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     {   // opaque copies: the store addresses are recomputed here instead of being kept live (two
         // VGPRs per tile) across the step loop from the loads above
         float2 *CMs = reinterpret_cast<float2 *>((q ? a.c1 : a.c0) + (size_t)g * a.m * 2);
-        const cint32 *tcs = tc;
+        const cint32 *tcs = tcw;
         asm volatile("" : "+s"(CMs), "+s"(tcs));
-        mem_store<TR>(std::make_integer_sequence<int, (TR + 7) / 8>{}, tcs, mem_rsrc(reinterpret_cast<float *>(CMs), a.m), lane, mr);
+        mem_store<TR>(std::make_integer_sequence<int, (TR + 7) / 8>{}, tcs, mem_rsrc(reinterpret_cast<float *>(CMs), a.m), wl, mr);
         for (int t = 0; t < a.tl; ++t) {  // this lane's own LDS slots: no barrier needed
-            const int c0 = tc[TR + t], c1 = tc[TR + t + 1];
-            const int c = c0 + lane;
+            const int c0 = tcw[(TR + t) * WAVES], c1 = tcw[(TR + t) * WAVES + 1];
+            const int c = c0 + wl;
             if (c < c1) CMs[c] = *lds_f2(mem_addr(a, t, lane));
         }
     }

@@ -16,6 +16,7 @@
 namespace onchip {
 
 constexpr int NTH = 512;           // threads per workgroup = tile capacity in clauses
+constexpr int WAVES = NTH / 64;    // slots [64 w, 64 w + 64) of a tile are wave w's
 constexpr int TILE_LDS = NTH * 8;  // LDS bytes of one LDS-resident tile of memories (float2 per lane)
 constexpr int SINKS = 32;          // sink words after v and after dv (empty slots of lane l use l % 32)
 constexpr uint32_t DVC = 65532;    // LDS byte offset of dv[0] from v[0]: the ds instructions' 16-bit
@@ -50,8 +51,9 @@ inline int tl_max(int64_t n) {
 struct Args {
     const uint64_t *rec; // [tiles][NTH] slot-major clause records (make_rec), padded with empty tiles
     uint32_t rec_bytes;
-    const int32_t *tc;   // first internal clause of each tile, [ntiles + 1] padded with m to at least
-                         // TR + tl + 1 entries (constant memory reads at static offsets)
+    const int32_t *tc;   // wave starts: wave w of tile t holds internal clauses [tc[8t+w], tc[8t+w+1]) in
+                         // its lanes 0.. (the rest of its slots are empty); padded with m to at least
+                         // 8 (TR + tl) + 1 entries (constant memory reads at static offsets)
     float *v0, *v1;      // voltages, [B][n] (par selects the buffer holding the current state)
     float *c0, *c1;      // clause memories, [B][m][2] (xs, xl), internal clause order
     uint8_t *par;        // [B] (flipped by an out-of-place launch)
