@@ -78,6 +78,7 @@ struct odesat_solver {
     uint64_t *oc_rec = nullptr;  // [tiles][512] slot-major clause records (onchip::make_rec)
     int32_t *oc_tcp = nullptr;   // [ntp * 8 + 1] wave starts (t * 8 + w) padded with m (static-index loads in k_onchip)
     int64_t oc_rec_bytes = 0;
+    int oc_off = 0;  // pair offset of the wave-paired tiles (pair_tiles): barrier after tile t iff t + off is odd
     bool in_range = true;        // every replica's state is in ONCHIP's range (onchip.hip header)
     int64_t bytes = 0;
     // steps run since the last fresh odesat_simulate: odesat_simulate_continue numbers its steps from
@@ -521,19 +522,20 @@ int small_instance_width(const odesat_cnf *f, int64_t n, int64_t batch, int devi
     return R;
 }
 
-// Wave-paired tiles (ONCHIP, onchip.hip: one barrier per PAIR of tiles).  Tiles 2i and 2i+1 form
-// one barrier interval, and slots [64w, 64w + 64) of a tile are wave w's.  LDS operations of one
+// Wave-paired tiles (ONCHIP, onchip.hip: one barrier per PAIR of tiles).  Tiles 2i - off and
+// 2i + 1 - off form one barrier interval (off = 0 or 1: with 1, tile 0 is an interval alone), and slots [64w, 64w + 64) of a tile are wave w's.  LDS operations of one
 // wave complete in issue order, so a clause may sit in the interval's second tile after a clause
 // it shares a variable with in the first tile when both are in the same wave; across waves the
 // order still needs the barrier after the pair.  Greedy in the reference's clause order: clause c
 // goes to the first tile after the tiles of its variables' last clauses where every one of those
 // in the same interval is in one wave w, and w has room (c then takes w); a clause with none there
 // takes the least-filled wave.  Each tile stays var-disjoint and every variable's tiles increase in
-// clause order, so the tiling is also a RESIDENT tiling.  Config 2: 91 tiles in 46 intervals
-// (plain greedy: 90 tiles, 90 barriers).
+// clause order, so the tiling is also a RESIDENT tiling.  Config 2: 91 tiles in 46 intervals at
+// off = 0, 90 in 46 at off = 1 (plain greedy: 90 tiles, 90 barriers); build_tiles keeps the offset
+// with fewer tiles.
 constexpr int PAIR_WAVES = 8, PAIR_WAVE_CAP = 64;
 
-void pair_tiles(const odesat_cnf *f, int64_t n, std::vector<int32_t> &tile_of, std::vector<int8_t> &wave_of,
+void pair_tiles(const odesat_cnf *f, int64_t n, int off, std::vector<int32_t> &tile_of, std::vector<int8_t> &wave_of,
                 std::vector<int32_t> &fill) {
     const int64_t m = f->nclauses();
     std::vector<int32_t> lastt((size_t)n, -1);
@@ -552,14 +554,14 @@ void pair_tiles(const odesat_cnf *f, int64_t n, std::vector<int32_t> &tile_of, s
             bool split = false;
             for (int64_t sl = b; sl < e; ++sl) {  // last clauses of c's variables in t's interval
                 const int32_t lt = lastt[f->var[sl]];
-                if (lt >= 0 && lt / 2 == t / 2) {
+                if (lt >= 0 && (lt + off) / 2 == (t + off) / 2) {
                     const int lw = lastw[f->var[sl]];
                     if (want >= 0 && want != lw) split = true;
                     want = lw;
                 }
             }
             if (split) {  // in two waves: only the next interval orders c after both
-                t = (t / 2 + 1) * 2;
+                t = ((t + off) / 2 + 1) * 2 - off;
                 continue;
             }
             if (want >= 0) {
@@ -583,18 +585,28 @@ void pair_tiles(const odesat_cnf *f, int64_t n, std::vector<int32_t> &tile_of, s
     fill.assign(wf.size(), 0);
     for (size_t t = 0; t < wf.size(); ++t)
         for (int k = 0; k < PAIR_WAVES; ++k) fill[t] += wf[t][k];
+    while (!fill.empty() && fill.back() == 0) fill.pop_back();
 }
 
 // wst (pairs only): [ntiles * 8 + 1] internal clause of wave w's first slot in tile t at t * 8 + w;
 // a tile's clauses are stored wave by wave, so wave w of tile t holds wst[t*8+w+1] - wst[t*8+w].
 bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, bool pairs, std::vector<int32_t> &perm,
-                 std::vector<int32_t> &tc, std::vector<uint8_t> &code, std::vector<int32_t> &wst) {
+                 std::vector<int32_t> &tc, std::vector<uint8_t> &code, std::vector<int32_t> &wst, int &pair_off) {
     const int64_t m = f->nclauses();
     std::vector<int32_t> last((size_t)n, -1), tile_of((size_t)m), fill;
     std::vector<int8_t> wave_of;
     wst.clear();
     if (pairs) {
-        pair_tiles(f, n, tile_of, wave_of, fill);
+        std::vector<int32_t> t1, f1;
+        std::vector<int8_t> w1;
+        pair_tiles(f, n, 0, tile_of, wave_of, fill);
+        pair_tiles(f, n, 1, t1, w1, f1);
+        pair_off = f1.size() < fill.size() ? 1 : 0;
+        if (pair_off) {
+            tile_of.swap(t1);
+            wave_of.swap(w1);
+            fill.swap(f1);
+        }
     } else {
         int32_t first_open = 0;  // every tile before it is full
         for (int64_t c = 0; c < m; ++c) {
@@ -868,7 +880,7 @@ int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zet
     a.xl_max = 1e4f * (float)s->m;  // system.rs:95, as (T)1e4 * (T)m
     {
         Timed tm(s, 0);
-        HIP_TRY(onchip::launch(s->oc_tr, a, s->G, onchip::lds_bytes(s->n, s->oc_tl), s->stream));
+        HIP_TRY(onchip::launch(s->oc_tr, s->oc_off, a, s->G, onchip::lds_bytes(s->n, s->oc_tl), s->stream));
     }
     return ODESAT_OK;
 }
@@ -1184,7 +1196,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         for (int64_t c = 0; c < m; ++c) perm[c] = (int32_t)c;
         tiles = {0, (int32_t)m};
         lorder.assign(m, 0);
-    } else if (res_r > 0 && !build_tiles(f, n, cap, res_r, s->uniform_k == 3, pairs, perm, tiles, lorder, wst)) {
+    } else if (res_r > 0 && !build_tiles(f, n, cap, res_r, s->uniform_k == 3, pairs, perm, tiles, lorder, wst, s->oc_off)) {
         res_r = 0;
     }
     if (res_r != 1) s->res_narrow = false;

@@ -207,10 +207,10 @@ __device__ __forceinline__ uint32_t mem_addr(const Args &a, int lt, int lane) {
 // Register tile T of the pass (static T, so mr[] stays in VGPRs).  All TR register tiles run
 // (tiles past the last one are empty): an early exit would join TR paths after the sequence, and
 // the copies that merge mr[] there double its VGPR footprint.
-template <int TR, int T>
+template <int TR, int OFF, int T>
 __device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&mr)[TR], Slot (&ring)[4], Pend &P,
                                          Front &Fn, Gath &Gn, float h, float hh, int lane, uint32_t &cmax, Stamps &S) {
-    constexpr bool bar = (T & 1) != 0;  // wave-paired tiles: a barrier after the second of a pair
+    constexpr bool bar = ((T + OFF) & 1) != 0;  // wave-paired tiles: a barrier after the second of a pair
     if constexpr (T + 1 < TR) {
         tile_step(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, cmax, S, bar);
     } else {  // tile TR is the first LDS tile (if any)
@@ -221,15 +221,15 @@ __device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&
     }
 }
 
-template <int TR, int... Ts>
+template <int TR, int OFF, int... Ts>
 __device__ __forceinline__ void reg_tiles(std::integer_sequence<int, Ts...>, const Args &a, const Recs &R,
                                           float2 (&mr)[TR], Slot (&ring)[4], Pend &P, Front &Fn, Gath &Gn, float h,
                                           float hh, int lane, uint32_t &cmax, Stamps &S) {
-    (reg_tile<TR, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S), ...);
+    (reg_tile<TR, OFF, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S), ...);
 }
 
 // One RHS pass + memory update over every tile; ends with a barrier (dv complete).
-template <int TR>
+template <int TR, int OFF>
 __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, int lane, uint32_t &cmax, Stamps &S) {
     Recs R;
     R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec, 0, (int)a.rec_bytes, 0x00020000);
@@ -254,7 +254,7 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
     front(G0, F0);
     front(G1, Fn);
     back(a, F0, mr[0], h, hh, P, cmax);
-    reg_tiles<TR>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S);
+    reg_tiles<TR, OFF>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S);
     // LDS tiles [TR, TR + tl): tl is a multiple of 4 (the host pads the tiling)
     const int NT = TR + a.tl;
     const int last = a.tl - 1;
@@ -267,10 +267,11 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
             const int lt = t + 1 - TR;
             const uint32_t ma = mem_addr(a, min(lt, last), lane);
             float2 m = *lds_f2(ma);
-            tile_step(a, R, ring[(u + 3) % 4], m, P, Fn, Gn, t, h, hh, cmax, S, (u & 1) != 0);  // TR is even
+            tile_step(a, R, ring[(u + 3) % 4], m, P, Fn, Gn, t, h, hh, cmax, S, ((u + OFF) & 1) != 0);  // TR is even
             if (lt <= last) *lds_f2(ma) = m;
         }
     }
+    if constexpr (OFF == 1) __syncthreads();  // the last tile (TR + tl - 1, odd) ends no pair
 }
 
 typedef const __attribute__((address_space(4))) int32_t cint32;
@@ -328,7 +329,7 @@ __device__ __forceinline__ void mem_store(std::integer_sequence<int, Gs...>, con
 }
 
 // The kernel declares no static LDS, so dynamic LDS -- and the records' byte addresses -- start at 0.
-template <int TR>
+template <int TR, int OFF>
 __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     const int g = blockIdx.x, lane = threadIdx.x;
     const int wl = lane & 63;  // slot of this lane in its wave's share of a tile
@@ -380,7 +381,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
 #ifdef ONCHIP_STAMPS
         S.last = memtime();
 #endif
-        pass<TR>(a, mr, h, lane, cmax, S);
+        pass<TR, OFF>(a, mr, h, lane, cmax, S);
         if (!(__uint_as_float(cmax) < 0.5f)) lds_st(UNS + 4u * (k & 1), 1.0f);
         for (int i = lane; i < a.n; i += NTH) {  // :96 (h dv = (h/2) dv2), dv restarts at 0 (:33)
             const float d2 = lds_f(4u * i + DVC);
@@ -432,19 +433,19 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     }
 }
 
-template <int TR> hipError_t launch_t(const Args &a, int G, size_t lds, hipStream_t stream) {
-    hipError_t e = odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_onchip<TR>), (int)LDS_MAX);
+template <int TR, int OFF> hipError_t launch_t(const Args &a, int G, size_t lds, hipStream_t stream) {
+    hipError_t e = odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_onchip<TR, OFF>), (int)LDS_MAX);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_onchip<TR>), dim3((unsigned)G), dim3(NTH), lds, stream, a);
+    hipLaunchKernelGGL((k_onchip<TR, OFF>), dim3((unsigned)G), dim3(NTH), lds, stream, a);
     return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch(int tr, const Args &a, int G, size_t lds, hipStream_t stream) {
+hipError_t launch(int tr, int off, const Args &a, int G, size_t lds, hipStream_t stream) {
     switch (tr) {
 #define ONCHIP_CASE(N) \
-    case N: return launch_t<N>(a, G, lds, stream);
+    case N: return off ? launch_t<N, 1>(a, G, lds, stream) : launch_t<N, 0>(a, G, lds, stream);
         ONCHIP_CASE(8) ONCHIP_CASE(16) ONCHIP_CASE(24) ONCHIP_CASE(32) ONCHIP_CASE(40) ONCHIP_CASE(48)
         ONCHIP_CASE(56) ONCHIP_CASE(64) ONCHIP_CASE(66) ONCHIP_CASE(68) ONCHIP_CASE(70) ONCHIP_CASE(72)
         ONCHIP_CASE(74) ONCHIP_CASE(76) ONCHIP_CASE(78) ONCHIP_CASE(80) ONCHIP_CASE(82) ONCHIP_CASE(84)

@@ -85,7 +85,8 @@ inline uint64_t make_rec(uint32_t a0, uint32_t a1, uint32_t a2, bool n0, bool n1
     return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-// Launch over replicas [0, G) on `stream`; tr must be one of TR_CHOICES.
-hipError_t launch(int tr, const Args &a, int G, size_t lds, hipStream_t stream);
+// Launch over replicas [0, G) on `stream`; tr must be one of TR_CHOICES, off (0 / 1) the pair offset
+// of the wave-paired tiles (a barrier after tile t iff t + off is odd).
+hipError_t launch(int tr, int off, const Args &a, int G, size_t lds, hipStream_t stream);
 
 }  // namespace onchip
