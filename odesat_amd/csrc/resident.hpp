@@ -243,6 +243,9 @@ __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> 
     res_clause3<T, R, PK>(a, x, CM, t + 1, S, Q, on, h, uns, e, CMr != CM);  // Q.ok = false past the last tile
     res_apply3<T, R>(x, P);
     res_load3<T, R, PK>(a, x, CMr, t + 1 + RES_DEPTH, S);
+#ifdef RES_TIMING_PAIRS  // timing-only diagnostic build (results race): a barrier after odd tiles only
+    if (t & 1)
+#endif
     __syncthreads();
     P = Q;
 }
