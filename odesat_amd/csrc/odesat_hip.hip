@@ -1907,3 +1907,23 @@ extern "C" int64_t odesat_clause_kernel_bytes(const odesat_solver *s) {
     const int64_t per = s->alg == ODESAT_ALG_TWOPASS ? s->n + 4 * s->m : 2 * s->n + 4 * s->m;
     return (int64_t)s->B * per * (int64_t)s->tsize;
 }
+
+// Test hook (not part of include/odesat.h): the wave-paired tiling the solver would build for a
+// 0-based formula (pair_tiles, offset off): tile and wave of every clause, and the tile count.
+// tests/test_tiling.py checks its invariants on the CPU -- a race it let through would not show
+// reliably on the GPU.
+extern "C" int odesat_debug_pair_tiles(const odesat_cnf *f, int off, int32_t *tile_of, int8_t *wave_of,
+                                       int32_t *ntiles) {
+    if (!f || !tile_of || !wave_of || !ntiles || (off != 0 && off != 1))
+        return fail(ODESAT_EINVAL, "odesat_debug_pair_tiles: bad argument");
+    const int64_t n = f->varnum;
+    for (int64_t v : f->var)
+        if (v < 0 || v >= n) return fail(ODESAT_EINVAL, "odesat_debug_pair_tiles: variables must be 0-based below varnum");
+    std::vector<int32_t> t, fill;
+    std::vector<int8_t> w;
+    pair_tiles(f, n, off, t, w, fill);
+    std::copy(t.begin(), t.end(), tile_of);
+    std::copy(w.begin(), w.end(), wave_of);
+    *ntiles = (int32_t)fill.size();
+    return ODESAT_OK;
+}
