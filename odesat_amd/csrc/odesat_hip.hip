@@ -1211,6 +1211,10 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     }
     s->LW = lw;
     s->VEC = 1;
+    // ODESAT_VEC=2/4 (tuning, FUSED / TWOPASS at LW = 64): contiguous replicas per lane, W = 64 VEC
+    if (const char *ev = std::getenv("ODESAT_VEC"))
+        if (res_r == 0 && lw == 64 && (std::atoi(ev) == 2 || (std::atoi(ev) == 4 && s->dtype == ODESAT_F32)))
+            s->VEC = std::atoi(ev);
     if (const char *ev = std::getenv("ODESAT_RB")) s->rb = std::atoi(ev) == 8 ? 8 : 4;
     s->W = s->LW * s->VEC;
     s->Bp = (batch + s->W - 1) / s->W * s->W;
