@@ -602,6 +602,8 @@ bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, bool p
         pair_tiles(f, n, 0, tile_of, wave_of, fill);
         pair_tiles(f, n, 1, t1, w1, f1);
         pair_off = f1.size() < fill.size() ? 1 : 0;
+        if (const char *ev = std::getenv("ODESAT_PAIR_OFF"))  // tests: force the offset
+            if (std::atoi(ev) == 0 || std::atoi(ev) == 1) pair_off = std::atoi(ev);
         if (pair_off) {
             tile_of.swap(t1);
             wave_of.swap(w1);

@@ -308,9 +308,13 @@ def test_f32_tracks_f64_on_short_horizon():
 
 
 # ---------------------------------------------------------------- full size (BASELINE config 2) ---
-def test_config2_full_size_subset_bitexact_and_properties():
+@pytest.mark.parametrize("pair_off", [None, "0"])
+def test_config2_full_size_subset_bitexact_and_properties(monkeypatch, pair_off):
     """n=10k, m=42k, B=1024 f32 for 12 steps: replicas {0, 517, 1023} bit-exact vs the oracle's f32
-    restatement; every replica: v in [-1,1], xs in [eps, 1-eps], xl in [1, 1e4 m], finite."""
+    restatement; every replica: v in [-1,1], xs in [eps, 1-eps], xl in [1, 1e4 m], finite.  The
+    solver's wave-paired tiles (k_onchip<90, 1>) and the other pair offset (91 tiles: k_onchip<92, 0>)."""
+    if pair_off is not None:
+        monkeypatch.setenv("ODESAT_PAIR_OFF", pair_off)
     c = wl.CONFIGS["config2"]
     var, neg = wl.random_ksat(c["n"], c["m"], 3, c["seed"])
     cp, v_, n_ = wl.formula_arrays(var, neg)
@@ -502,10 +506,14 @@ def _instance(n, m, seed):
 
 
 @pytest.mark.parametrize("stop", ["each", "any", "none"])
-def test_onchip_lds_tiles_match_resident_and_oracle(stop):
+@pytest.mark.parametrize("pair_off", [None, "0", "1"])
+def test_onchip_lds_tiles_match_resident_and_oracle(stop, monkeypatch, pair_off):
     """n=6000, m=33000 (ratio 5.5): 116 tiles, so ONCHIP keeps 96 tiles' memories in VGPRs and 20
     in LDS.  ONCHIP == RESIDENT (HBM-streamed memories) bit for bit on every stop policy, and
-    replica 0 == the oracle's f32 restatement."""
+    replica 0 == the oracle's f32 restatement -- with the wave-paired tiles at either pair offset
+    (ODESAT_PAIR_OFF; None = the solver's choice)."""
+    if pair_off is not None:
+        monkeypatch.setenv("ODESAT_PAIR_OFF", pair_off)
     from odesat_amd import _lib
     f, (cp, v_, n_) = _instance(6000, 33000, 5)
     pol = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[stop]
