@@ -275,6 +275,32 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
 }
 
 typedef const __attribute__((address_space(4))) int32_t cint32;
+
+// The state moves through HBM once per launch, read once and written once: non-temporal (aux nt),
+// so the launch's 770 MB stream (config 2, B = 1024) does not evict the clause records every CU
+// re-reads from L2 at the next round's first pass.  ONCHIP_STATE_AUX=0: default policy (A/B).
+#ifndef ONCHIP_STATE_AUX
+#define ONCHIP_STATE_AUX 2
+#endif
+template <typename P> __device__ __forceinline__ P ld_state(const P *p) {
+    if constexpr (ONCHIP_STATE_AUX != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <typename P> __device__ __forceinline__ void st_state(P *p, P x) {
+    if constexpr (ONCHIP_STATE_AUX != 0) __builtin_nontemporal_store(x, p);
+    else *p = x;
+}
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2 ld_state(const float2 *p) {
+    const f2v x = ld_state(reinterpret_cast<const f2v *>(p));
+    return make_float2(x.x, x.y);
+}
+__device__ __forceinline__ void st_state(float2 *p, float2 x) {
+    f2v y;
+    y.x = x.x;
+    y.y = x.y;
+    st_state(reinterpret_cast<f2v *>(p), y);
+}
 // The replica's clause memories as a buffer resource (m float2 records): tile j's slot of lane l is
 // the byte offset 8 (tc[j] + l), checked against the range as a whole (the VGPR offset: the scalar
 // offset is not range-checked), so a slot past the replica's memories reads 0 and stores nothing.
@@ -294,7 +320,7 @@ __device__ __forceinline__ void mem_load(std::integer_sequence<int, Js...>, cons
     typedef int i2 __attribute__((ext_vector_type(2)));
     auto one = [&](auto J) {
         constexpr int j = decltype(J)::value;
-        const i2 r = __builtin_amdgcn_raw_buffer_load_b64(rs, lane8 + 8u * (uint32_t)tcw[j * WAVES], 0, 0);
+        const i2 r = __builtin_amdgcn_raw_buffer_load_b64(rs, lane8 + 8u * (uint32_t)tcw[j * WAVES], 0, ONCHIP_STATE_AUX);
         mr[j] = make_float2(__int_as_float(r.x), __int_as_float(r.y));
     };
     (one(std::integral_constant<int, Js>{}), ...);
@@ -322,7 +348,7 @@ __device__ __forceinline__ void mem_store(std::integer_sequence<int, Gs...>, con
             i2 r;
             r.x = __float_as_int(mr[j0 + k].x);
             r.y = __float_as_int(mr[j0 + k].y);
-            __builtin_amdgcn_raw_buffer_store_b64(r, rs, vo, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(r, rs, vo, 0, ONCHIP_STATE_AUX);
         }
     };
     (group(std::integral_constant<int, Gs>{}), ...);
@@ -352,7 +378,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         for (int i0 = lane; i0 < n2; i0 += NTH * U) {
             float x[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) x[u] = V[min(i0 + u * NTH, a.n - 1)];
+            for (int u = 0; u < U; ++u) x[u] = ld_state(&V[min(i0 + u * NTH, a.n - 1)]);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int i = i0 + u * NTH;
@@ -369,7 +395,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                  8u * (uint32_t)wl, mr);
     for (int t = 0; t < a.tl; ++t) {
         const int c0 = tcw[(TR + t) * WAVES];
-        *lds_f2(mem_addr(a, t, lane)) = CM[min(c0 + wl, mlast)];  // (empty slots: as mem_io)
+        *lds_f2(mem_addr(a, t, lane)) = ld_state(&CM[min(c0 + wl, mlast)]);  // (empty slots: as mem_io)
     }
     if (lane < 2) lds_st(UNS + 4u * lane, 0.0f);
     __syncthreads();
@@ -403,7 +429,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     }
 
     float *Vo = (q ? a.v1 : a.v0) + (size_t)g * a.n;
-    for (int i = lane; i < a.n; i += NTH) Vo[i] = lds_f(4u * i);  // written by this lane in the last update
+    for (int i = lane; i < a.n; i += NTH) st_state(&Vo[i], lds_f(4u * i));  // written by this lane in the last update
     {   // opaque copies: the store addresses are recomputed here instead of being kept live (two
         // VGPRs per tile) across the step loop from the loads above
         float2 *CMs = reinterpret_cast<float2 *>((q ? a.c1 : a.c0) + (size_t)g * a.m * 2);
@@ -413,7 +439,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         for (int t = 0; t < a.tl; ++t) {  // this lane's own LDS slots: no barrier needed
             const int c0 = tcw[(TR + t) * WAVES], c1 = tcw[(TR + t) * WAVES + 1];
             const int c = c0 + wl;
-            if (c < c1) CMs[c] = *lds_f2(mem_addr(a, t, lane));
+            if (c < c1) st_state(&CMs[c], *lds_f2(mem_addr(a, t, lane)));
         }
     }
 #ifdef ONCHIP_STAMPS
