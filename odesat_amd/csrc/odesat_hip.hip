@@ -596,6 +596,7 @@ bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, bool p
     std::vector<int32_t> last((size_t)n, -1), tile_of((size_t)m), fill;
     std::vector<int8_t> wave_of;
     wst.clear();
+    pairs = pairs && cap == PAIR_WAVES * PAIR_WAVE_CAP;  // one replica per 512-lane workgroup only
     if (pairs) {
         std::vector<int32_t> t1, f1;
         std::vector<int8_t> w1;
