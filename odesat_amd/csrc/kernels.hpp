@@ -469,8 +469,16 @@ __device__ __forceinline__ void stream_rows3(const KArgs<T> &a, const Bufs<T> &b
 // literals (random k-SAT) -- RB incidences per batch, all their loads issued before the first use.
 // K == 0: mixed clause widths, one incidence at a time.
 // ------------------------------------------------------------------------------------------------
+#ifndef KSTEP_WAVES_PER_EU  // tuning: minimum waves per SIMD the compiler must leave room for (0 = its choice)
+#define KSTEP_WAVES_PER_EU 0
+#endif
+#if KSTEP_WAVES_PER_EU > 0
+#define KSTEP_ATTR __attribute__((amdgpu_waves_per_eu(KSTEP_WAVES_PER_EU)))
+#else
+#define KSTEP_ATTR
+#endif
 template <typename T, int LW, int VEC, int MODE, int K, int RB = 4>
-__global__ __launch_bounds__(256) void k_step(KArgs<T> a) {
+__global__ __launch_bounds__(256) KSTEP_ATTR void k_step(KArgs<T> a) {
     using G_ = Geo<LW, VEC>;
     constexpr int W = G_::W, IPR = G_::IPR;
     static_assert(K == 0 || K == 3, "incidence records are laid out for 3-SAT");
