@@ -5,7 +5,9 @@
 // Same clause tiles as the RESIDENT kernel (resident.hpp): no two clauses of a
 // tile share a variable and every variable's tiles increase in the reference's clause order, so
 // the lanes of a tile add their terms straight into dv (LDS) and every dv[i] is the reference's
-// left fold over (clause, literal), bit for bit.  What changes is where the clause memories live:
+// left fold over (clause, literal), bit for bit.  The tiles are wave-paired (odesat_hip.hip
+// pair_tiles): a barrier follows every second tile only, and a clause that depends on a clause of
+// the same pair sits in the same wave, whose LDS operations complete in issue order.  What changes is where the clause memories live:
 // lane l owns clause slot l of every tile, so its memories form a per-lane array indexed by the
 // tile number.  The first TR tiles keep theirs in VGPRs (the tile sequence is expanded at compile
 // time, so the index is static), the remaining tiles in LDS next to v and dv.  A step then moves
@@ -161,10 +163,11 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
 // One tile step.  In flight: P = tile t's dv terms, Fn = tile t+1's first half, Gn = tile t+2's
 // gathered voltages, ring = the records of tiles t+3 .. t+6.  The critical chain of a step is tile
 // t's dv read-modify-write (:80; three distinct variables per clause, so the updates are
-// independent) between two barriers: its reads go out first and the writes right after they
-// return.  The voltage gathers of tile t+3 follow (v is constant during a pass), then tile t+1's
-// second half and tile t+2's first half -- independent, so they interleave -- while the writes
-// and the gathers drain.  The barrier then orders tile t's dv against tile t+1's.
+// independent): its reads go out first and the writes right after they return.  The voltage
+// gathers of tile t+3 follow (v is constant during a pass), then tile t+1's second half and tile
+// t+2's first half -- independent, so they interleave -- while the writes and the gathers drain.
+// After the second tile of a pair (bar), the barrier orders the pair's dv updates against the next
+// pair's; inside a pair the same-wave order suffices (see the header).
 __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &slot3, float2 &mem1, Pend &P, Front &Fn,
                                           Gath &Gn, int t, float h, float hh, uint32_t &cmax, Stamps &S, bool bar) {
     const float o0 = lds_f(P.a0 + DVC), o1 = lds_f(P.a1 + DVC), o2 = lds_f(P.a2 + DVC);
