@@ -242,23 +242,30 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
         for (int j = 0; j < TW; ++j) r = r || unsL[w * TW + j] != 0;
         return r;
     };
+    // Barriers per step (TW > 1): team_any's (phase 1's terms and memories before the fold, and the
+    // unsat vote), and the step's closing __syncthreads_or (the fold's voltages before the next
+    // step's phase 1, and whether any team still steps); adaptive adds two (the half step's
+    // voltages before the second clause pass, its terms before the second fold) and one for the
+    // error fold.  The bookkeeping only needs uns, so it runs before the closing barrier.
     for (int k = 0; k < a.nsteps; ++k) {
         const int step = a.step0 + k;
         const T h = dtr;
         T e = (T)0.0;
         bool uns = false;
+        const int act0 = act;  // this step's participation; the bookkeeping below may clear act
+        bool go = false;
         if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
-            if (act) uns = wave_clauses<T, W_FIXED, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
+            if (act0) uns = wave_clauses<T, W_FIXED, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
             uns = team_any(uns);
-            team_sync<TW>();
-            if (act)
+            if (TW == 1) team_sync<TW>();  // (TW > 1: team_any's barrier ordered phase 1's stores)
+            if (act0)
                 for (int i = l; i < a.n; i += NL) vL[i] = dmin(dmax(vL[i] + h * wave_fold(vst, tL, i), (T)-1.0), (T)1.0);
-            team_sync<TW>();
         } else {  // euler_step (:111-139)
-            if (act) uns = wave_clauses<T, W_ADA1, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
+            if (act0) uns = wave_clauses<T, W_ADA1, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
             uns = team_any(uns);
-            team_sync<TW>();
-            const bool go = act && uns;  // an allsat replica takes no step (:122)
+            if (TW == 1) team_sync<TW>();
+            if (l == 0) errL[w] = 0;  // last read before the previous step's closing barrier
+            go = act0 && uns;  // an allsat replica takes no step (:122)
             const T half = (T)0.5 * h;
             if (go)
                 for (int i = l; i < a.n; i += NL) {
@@ -275,16 +282,9 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
                     e = dmax(e, dabs(vfL[i] - vn));  // :101-108
                     vL[i] = vn;
                 }
-            if (l == 0) errL[w] = 0;
-            team_sync<TW>();
             if (go) atomicMax(&errL[w], tobits(e));
-            team_sync<TW>();
-            if (go) {
-                const T error = frombits(errL[w]);  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
-                dtr = dmax(dmin(dtr * dsqrt((T)a.tol / error), (T)1e3), (T)0.0078125);
-            }
         }
-        if (act) {
+        if (act0) {
             done += 1;
             if (!uns) {  // allsat: the fixed step was still taken (:148-152); adaptive took none
                 if (sat < 0) sat = step;
@@ -292,7 +292,12 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
                 if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
             }
         }
+        if (TW == 1) team_sync<TW>();
         if (TW == 1 ? !act : !__syncthreads_or(act)) break;  // uniform per wave / per workgroup
+        if (ADAPTIVE && go) {  // (a stepping team stays active, so it reaches this after the barrier)
+            const T error = frombits(errL[w]);  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
+            dtr = dmax(dmin(dtr * dsqrt((T)a.tol / error), (T)1e3), (T)0.0078125);
+        }
     }
     team_sync<TW>();
     if (!live) return;
