@@ -1146,6 +1146,14 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         const char *ev = std::getenv("ODESAT_WAVE");
         const size_t topo = wave_topo_bytes(n, m), rep = wave_lds_bytes(n, m, L, s->tsize, true);
         s->wv_wpw = topo + 4 * rep <= RES_LDS_MAX ? 4 : (topo + 2 * rep <= RES_LDS_MAX ? 2 : 1);
+        // ... and no more than leaves every CU a workgroup: a small batch spreads over the chip one
+        // replica per workgroup, each then a team of up to 16 waves (B = 256 on 256 CUs: WPW 4 -> 1)
+        {
+            int cus = 256;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
+                cus = 256;
+            while (s->wv_wpw > 1 && (batch + s->wv_wpw - 1) / s->wv_wpw < cus) s->wv_wpw /= 2;
+        }
         s->res_wave = ev ? (std::atoi(ev) != 0 && topo + rep <= RES_LDS_MAX) : topo + 2 * rep <= RES_LDS_MAX;
         // waves per replica: LDS holds one workgroup (wv_wpw replicas) per CU, so a replica of one
         // wave leaves a lone wave on each SIMD, which issues a VALU instruction every 4 cycles.  A

@@ -3,7 +3,7 @@
 # product library vs expt/lib$VAR.so, alternated.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-one() { timeout -k 10 300 python scripts/bench_configs.py --configs config3,config3f --steps 200 --warmup 20 --no-cpu 2>/dev/null | python3 -c "
+one() { timeout -k 10 300 python scripts/bench_configs.py --configs config3,config3f ${CFG3_ARGS:-} --steps 200 --warmup 20 --no-cpu 2>/dev/null | python3 -c "
 import sys,json
 for line in sys.stdin:
     d=json.loads(line); print(d['config'] if 'config' in d else '', d.get('algorithm'), round(d['replica_steps_per_s']/1e6,2), 'M', round(d['ms_per_step'],5))"; }
