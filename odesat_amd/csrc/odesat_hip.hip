@@ -1898,6 +1898,16 @@ extern "C" int odesat_profile_enable(odesat_solver *s, int enable) {
         s->prof_ms[k] = 0;
         s->prof_n[k] = 0;
     }
+    // events for the launches to come, created (and recorded once) here rather than inside a call
+    if (s->profile) {
+        while (s->pool.size() < 8) {
+            hipEvent_t e = nullptr;
+            HIP_TRY(hipEventCreate(&e));
+            s->pool.push_back(e);
+        }
+        for (hipEvent_t e : s->pool) HIP_TRY(hipEventRecord(e, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+    }
     return ODESAT_OK;
 }
 
