@@ -67,7 +67,8 @@ struct odesat_solver {
     int4 *wv_rec4 = nullptr;  // [m] k_wave: literal | variable-major term position << 16, per literal
     int32_t *wv_vst = nullptr;  // [n+1] k_wave: first term position of each variable
     int wv_wpw = 1;             // k_wave: replicas per workgroup sharing the LDS topology
-    int wv_tw = 1;              // k_wave: waves per replica (2 when one per replica leaves SIMDs idle)
+    int wv_tw = 1;              // k_wave: waves per replica, fixed steps
+    int wv_tw_ada = 1;          // ... adaptive steps (four barriers per step instead of two: at most 4)
     bool res_ada = false; // adaptive steps fit in LDS too (else they run FUSED on the same layout)
     int res_ntiles = 0;
     int32_t *res_tc = nullptr, *cmap = nullptr;
@@ -782,7 +783,7 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
         return adaptive ? launch_wave_k<T, true, WPW, TW>(s, a) : launch_wave_k<T, false, WPW, TW>(s, a);
     };
     // (replicas per workgroup, waves per replica): at most 16 waves per workgroup
-    switch (s->wv_wpw * 100 + s->wv_tw) {
+    switch (s->wv_wpw * 100 + (adaptive ? s->wv_tw_ada : s->wv_tw)) {
         case 401: return go(IC<4>{}, IC<1>{});
         case 402: return go(IC<4>{}, IC<2>{});
         case 404: return go(IC<4>{}, IC<4>{});
@@ -1164,9 +1165,13 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         // 26 / 14 ms at TW = 4.  ODESAT_WAVE_TEAM = 1/2/4/8/16 overrides (if the shape exists).
         s->wv_tw = 16 / s->wv_wpw;
         while (s->wv_tw > 1 && 32 * (int64_t)s->wv_tw > m) s->wv_tw /= 2;
+        // adaptive steps order their phases with four barriers, fixed ones with two: a wide team pays
+        // twice as many (config 3, B = 256, one replica per workgroup: adaptive 42.4 M replica-steps/s
+        // at TW = 4 vs 35.7 M at 16; fixed 80.2 M at 4 vs 91.7 M at 16)
+        s->wv_tw_ada = std::min(s->wv_tw, 4);
         if (const char *et = std::getenv("ODESAT_WAVE_TEAM")) {
             const int t = std::atoi(et);
-            if ((t == 1 || t == 2 || t == 4 || t == 8 || t == 16) && t * s->wv_wpw <= 16) s->wv_tw = t;
+            if ((t == 1 || t == 2 || t == 4 || t == 8 || t == 16) && t * s->wv_wpw <= 16) s->wv_tw = s->wv_tw_ada = t;
         }
     }
     if (s->res_wave) {
