@@ -24,6 +24,8 @@ SPEC = {
     "config3": dict(adaptive=True, batch=1024, cpu_replicas=8, cpu_steps=400),
     "config4": dict(adaptive=False, batch=1024, cpu_replicas=1, cpu_steps=30),
     "config3f": dict(adaptive=False, batch=1024, cpu_replicas=8, cpu_steps=400, base="config3"),
+    # the reference's default mode (solve / batch without -s) on the headline instance
+    "config2a": dict(adaptive=True, batch=1024, cpu_replicas=4, cpu_steps=100, base="config2"),
 }
 
 
