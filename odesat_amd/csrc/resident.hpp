@@ -50,13 +50,14 @@ template <typename T> struct RArgs {
     double tol;
 };
 
-// Pass kinds: P_FIXED one fixed step in place; P_ADA1 full + first half candidates to scratch;
-// P_ADA2 second half in place + max_error against the full-step candidate.
+// Pass kinds: P_FIXED one fixed step in place; P_ADA1 each clause's C to scratch (the memories stay
+// y); P_ADA2 recomputes the full-step and first-half candidates from y and that C, then the second
+// half in place + max_error against the full-step candidate.
 enum Pass : int { P_FIXED = 0, P_ADA1 = 1, P_ADA2 = 2 };
 
 template <typename T, int R> struct ResCtx {
     T *vL, *dvL, *vfL;  // LDS
-    T *cf, *ch;         // this group's adaptive scratch memories
+    T *cf, *ch;         // this group's adaptive scratch: cf holds each clause's first-pass C
     int r, lc;          // this lane's replica and clause-lane index
 };
 
@@ -88,8 +89,22 @@ __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> 
     // ring's back-edge but measured 4% slower)
     ld.lit = *at(a.cl4, (uint32_t)cc);
     const uint32_t ci = (uint32_t)(cc * R + x.r) * 2u;  // 32-bit offsets from the group's base
-    ld.mem = ldv<T, 2>(at(PK == P_ADA2 ? (const T *)x.ch : CM, ci));
-    if (PK == P_ADA2) ld.full = ldv<T, 2>(at((const T *)x.cf, ci));
+    ld.mem = ldv<T, 2>(at(CM, ci));  // (adaptive: y's memories, untouched until the second pass stores)
+    if (PK == P_ADA2) ld.full.e[0] = *at((const T *)x.cf, ci / 2u);  // the first pass's C
+}
+
+// The adaptive step's candidates for one clause's memories from y's memories and the first pass's
+// C (system.rs:84-85, :124-128): the full-step clone f and the first half step hh.
+template <typename T>
+__device__ __forceinline__ void res_ada_mems(const RArgs<T> &a, const Vec<T, 2> &y, T C1, T h, Vec<T, 2> &f,
+                                             Vec<T, 2> &hh) {
+    const T one = (T)1.0, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001, half = (T)0.5 * h;
+    const T dxs = (T)20.0 * (y.e[0] + eps) * (C1 - (T)0.25);  // :84
+    const T dxl = (T)5.0 * (C1 - (T)0.05);                    // :85
+    f.e[0] = dmin(dmax(y.e[0] + h * dxs, eps), xs_hi);  // full-step clone (:124-125)
+    f.e[1] = dmin(dmax(y.e[1] + h * dxl, one), a.xl_max);
+    hh.e[0] = dmin(dmax(y.e[0] + half * dxs, eps), xs_hi);  // first half step (:128)
+    hh.e[1] = dmin(dmax(y.e[1] + half * dxl, one), a.xl_max);
 }
 
 // Memory update of one clause (system.rs:84-85, 94-95 / :124-132); returns the max_error terms.
@@ -113,14 +128,10 @@ __device__ __forceinline__ T res_mem_update(const RArgs<T> &a, const ResCtx<T, R
         o.e[1] = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
         stv<T, 2>(at(CM, ci), o);
     } else if (PK == P_ADA1) {
-        const T half = (T)0.5 * h;
-        Vec<T, 2> f, hh;
-        f.e[0] = dmin(dmax(xs_m + h * dxs, eps), xs_hi);  // full-step clone (:124-125)
-        f.e[1] = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
-        hh.e[0] = dmin(dmax(xs_m + half * dxs, eps), xs_hi);  // first half step (:128)
-        hh.e[1] = dmin(dmax(xl_m + half * dxl, one), a.xl_max);
-        stv<T, 2>(at(x.cf, ci), f);
-        stv<T, 2>(at(x.ch, ci), hh);
+        // only C: the second pass recomputes the full-step clone and the first half step from it
+        // and y's memories (res_ada_mems) -- the same expressions, so the same bits -- which moves
+        // 12 bytes per clause less through HBM than storing both candidates
+        *at(x.cf, ci / 2u) = C;
     } else {
         const T half = (T)0.5 * h;  // second half step (:130) and max_error terms (:132)
         Vec<T, 2> o;
@@ -162,7 +173,9 @@ __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R
         minsec(val[j], mn, sec);
     }
     const T C = halfc * mn;  // :60
-    const T xs_m = ld.mem.e[0], xl_m = ld.mem.e[1];
+    Vec<T, 2> mem = ld.mem, full{};
+    if (PK == P_ADA2) res_ada_mems(a, ld.mem, ld.full.e[0], h, full, mem);  // mem <- the first half step
+    const T xs_m = mem.e[0], xl_m = mem.e[1];
     const T tt = xl_m * xs_m;
     const T tr = (one + a.zeta * xl_m) * (one - xs_m);
 #pragma unroll
@@ -180,7 +193,7 @@ __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R
         }
     }
     if (PK != P_ADA2) uns = uns || (on && !(C < (T)0.25));  // :88
-    e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, (uint32_t)(c * R + x.r) * 2u, C, ld.mem, ld.full, on, h, copy));
+    e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, (uint32_t)(c * R + x.r) * 2u, C, mem, full, on, h, copy));
 }
 
 // :80 for one clause: dv[i_j] += d_j for j = 0, 1, 2 in order.  The three reads are issued
@@ -207,9 +220,9 @@ __device__ __forceinline__ void res_clause_any(const RArgs<T> &a, const ResCtx<T
     if (c >= ldc(a.tc, t + 1)) return;
     const int s0 = a.cptr[c], s1 = a.cptr[c + 1];
     const uint32_t ci = (uint32_t)(c * R + x.r) * 2u;
-    const Vec<T, 2> mem = ldv<T, 2>((PK == P_ADA2 ? x.ch : CMr) + ci);
+    Vec<T, 2> mem = ldv<T, 2>(CMr + ci);
     Vec<T, 2> full{};
-    if (PK == P_ADA2) full = ldv<T, 2>(x.cf + ci);
+    if (PK == P_ADA2) res_ada_mems(a, Vec<T, 2>(mem), x.cf[ci / 2u], h, full, mem);
     T mn = inf_v<T>(), sec = inf_v<T>();
     for (int s = s0; s < s1; ++s) {
         const int lit = a.lits[s];
