@@ -75,6 +75,35 @@ template <typename T> struct TileLoad {
     bool ok;
 };
 
+// The clause memories stream through HBM once per pass; RES_NT=1 (experiment) moves them with
+// non-temporal accesses so they do not evict the clause records every CU re-reads from L2.
+#ifndef RES_NT
+#define RES_NT 0
+#endif
+template <typename T> __device__ __forceinline__ Vec<T, 2> res_ldm(const T *p) {
+    if constexpr (RES_NT != 0) {
+        typedef T t2 __attribute__((ext_vector_type(2)));
+        const t2 x = __builtin_nontemporal_load(reinterpret_cast<const t2 *>(p));
+        Vec<T, 2> r;
+        r.e[0] = x.x;
+        r.e[1] = x.y;
+        return r;
+    } else {
+        return ldv<T, 2>(p);
+    }
+}
+template <typename T> __device__ __forceinline__ void res_stm(T *p, const Vec<T, 2> &v) {
+    if constexpr (RES_NT != 0) {
+        typedef T t2 __attribute__((ext_vector_type(2)));
+        t2 x;
+        x.x = v.e[0];
+        x.y = v.e[1];
+        __builtin_nontemporal_store(x, reinterpret_cast<t2 *>(p));
+    } else {
+        stv<T, 2>(p, v);
+    }
+}
+
 // Loads of tile t (t >= ntiles: nothing to do, a valid address is read).  Unconditional, so the
 // ring's loads stay in flight across iterations (no control flow for the wait counters to merge).
 template <typename T, int R, int PK>
@@ -89,7 +118,7 @@ __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> 
     // ring's back-edge but measured 4% slower)
     ld.lit = *at(a.cl4, (uint32_t)cc);
     const uint32_t ci = (uint32_t)(cc * R + x.r) * 2u;  // 32-bit offsets from the group's base
-    ld.mem = ldv<T, 2>(at(CM, ci));  // (adaptive: y's memories, untouched until the second pass stores)
+    ld.mem = res_ldm<T>(at(CM, ci));  // (adaptive: y's memories, untouched until the second pass stores)
     if (PK == P_ADA2) ld.full.e[0] = *at((const T *)x.cf, ci / 2u);  // the first pass's C
 }
 
@@ -126,7 +155,7 @@ __device__ __forceinline__ T res_mem_update(const RArgs<T> &a, const ResCtx<T, R
         Vec<T, 2> o;
         o.e[0] = dmin(dmax(xs_m + h * dxs, eps), xs_hi);
         o.e[1] = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
-        stv<T, 2>(at(CM, ci), o);
+        res_stm<T>(at(CM, ci), o);
     } else if (PK == P_ADA1) {
         // only C: the second pass recomputes the full-step clone and the first half step from it
         // and y's memories (res_ada_mems) -- the same expressions, so the same bits -- which moves
