@@ -11,9 +11,28 @@ ranks are already there.  Each rank steps its own B replicas (global replica ind
 no collective in the data path -- weak scaling; barrier + max-over-ranks timing via
 torch.distributed (RCCL).
 
+Beside the headline, the same JSON line carries one object per further leg, each timed
+the same way (barrier + device sync around K steps, max over ranks) with its own roofline:
+  f64            config 2, B=1024, fixed step in the reference's own precision (the CLI default dtype)
+  adaptive       config 2, B=1024, adaptive step tol 1e-3 (the reference's default mode, system.rs:111-139)
+  inter          config 2 under STOP_ANY (simulate_inter)
+  inter_config4  config 4 (n=50k, m=210k), B=1024 per rank, the sharded inter protocol
+                 (sharding.run_inter: lock-step chunks, MIN all-reduce of the stop step, rollback) --
+                 BASELINE configs[3]; weak scaling; in-run digest: rank 0 re-integrates the first
+                 replicas of every rank on its own GPU and compares state hashes bit for bit
+  partition_config5  config 5 (n=1M, m=4.2M), ONE replica partitioned over the ranks, HIP-graph
+                 stepped, RCCL collective per step -- BASELINE configs[4]; strong scaling; three
+                 partitions (CLAUSES all-reduce = the north star's design, CLAUSES_RS reduce-scatter +
+                 all-gather, VARIABLES all-gather); in-run digest against a world-1 run on rank 0
+                 (VARIABLES bit-exact, the CLAUSES forms within their stated tolerance)
+  extra_batch    config 2 at B=256 (BASELINE configs[1])
+  ab_hbm_streaming  the HBM-streaming kernel (k_resident) on the headline workload
+
 Rank 0 prints ONE JSON line (see DESIGN.md §6 for every field).
 """
 import argparse
+import glob
+import hashlib
 import json
 import os
 import socket
@@ -28,6 +47,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD (SIMD-32),
 # at the 2.4 GHz max clock (MI355X_MICROARCH.md, wave scheduling / chip-level parameters)
 VALU_PEAK_GINST = 1024 * 2.4e9 / 2 / 1e9
+LEGS = ("f64", "adaptive", "inter", "config4", "config5", "extra", "ab")
+CLAUSES_TOL = 1e-5       # the CLAUSES partitions' stated tolerance against a world-1 run
+DIGEST_REPLICAS = 4      # inter_config4: replicas per rank re-integrated by rank 0
 
 
 def parse():
@@ -43,22 +65,67 @@ def parse():
     p.add_argument("--cpu-steps", type=int, default=300)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--profile-dir", default=os.path.join(ROOT, "profiles"),
-                   help="directory of profile_<kernel>.json: the dominant kernel's PMC HBM bytes and VALU "
-                        "instructions as fixed-per-launch + per-step fits (scripts/make_profile_json.py)")
+                   help="directory of profile_*.json: PMC HBM bytes and VALU instructions of a kernel on a "
+                        "workload as fixed-per-launch + per-step fits (scripts/make_profile_json.py)")
     p.add_argument("--alg", default="auto", choices=["auto", "onchip", "resident", "fused", "twopass"],
                    help="force an algorithm (A/B); auto = the solver's default")
     p.add_argument("--extra-batch", type=int, default=256, help="also time this B (configs[1]); 0 = off")
+    p.add_argument("--skip", default="", help="comma-separated legs to leave out: " + ",".join(LEGS))
+    p.add_argument("--only", default="", help="comma-separated legs to run (with the headline), others skipped")
     p.add_argument("--no-ab", action="store_true",
                    help="skip the in-run A/B line of the HBM-streaming kernel (k_resident) on the same workload")
     p.add_argument("--no-inter", action="store_true", help="skip the inter-mode (STOP_ANY) line")
-    return p.parse_args()
+    p.add_argument("--config5-graph", type=int, default=0,
+                   help="steps per captured HIP graph in partition_config5 (0 = all timed steps in one graph)")
+    args = p.parse_args()
+    skip = {x for x in args.skip.split(",") if x}
+    if args.only:
+        skip |= set(LEGS) - {x for x in args.only.split(",") if x}
+    if args.no_ab:
+        skip.add("ab")
+    if args.no_inter:
+        skip.add("inter")
+    if not args.extra_batch:
+        skip.add("extra")
+    bad = skip - set(LEGS)
+    if bad:
+        p.error(f"unknown legs {sorted(bad)}")
+    args.skip_legs = skip
+    return args
+
+
+def visible_gpus():
+    """GPUs this process could use, counted WITHOUT a HIP call (the parent of the rank processes must
+    not initialise the GPU): the KFD topology's GPU nodes whose render node is present and accessible,
+    narrowed by ROCR/HIP/CUDA_VISIBLE_DEVICES.  None when the topology is unreadable."""
+    nodes = sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"))
+    if not nodes:
+        return None
+    count = 0
+    for f in nodes:
+        try:
+            props = dict(line.split()[:2] for line in open(f) if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) <= 0:
+            continue  # a CPU node
+        dev = f"/dev/dri/renderD{props.get('drm_render_minor', '-1')}"
+        if os.path.exists(dev) and os.access(dev, os.R_OK | os.W_OK):
+            count += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None and v.strip() != "":
+            count = min(count, len([x for x in v.split(",") if x.strip() != ""]))
+    return count
 
 
 def spawn_ranks(args):
     """`--gpus N` without a launcher: start N ranks (one per GPU) under torch.distributed.run and exit
     with its status.  Started as a child process before this process touches the GPU."""
-    import torch
-    ndev = torch.cuda.device_count()  # counts devices without initialising HIP
+    ndev = visible_gpus()
+    if ndev is None:  # no KFD topology to read: torch's count (HIP-free when amdsmi answers)
+        import torch
+        ndev = torch.cuda.device_count()
     if args.gpus > ndev:
         sys.exit(f"bench.py: --gpus {args.gpus} but only {ndev} GPU(s) are visible")
     with socket.socket() as sk:
@@ -81,7 +148,6 @@ def dist_setup(args):
         ndev = torch.cuda.device_count()
         # RCCL ("nccl") on GPU boxes, one rank per GPU; ODESAT_DIST_BACKEND=gloo rehearses N ranks on
         # fewer GPUs (RCCL refuses two ranks on one device): ranks then share devices round-robin.
-        # Only host scalars cross ranks (odesat_amd/sharding.py).
         backend = os.environ.get("ODESAT_DIST_BACKEND") or ("nccl" if ndev > 0 else "gloo")
         if backend == "nccl":
             if local >= ndev:
@@ -91,6 +157,8 @@ def dist_setup(args):
         else:
             devices = min(world, max(1, ndev))
             local %= max(1, ndev)
+            if ndev > 0:
+                torch.cuda.set_device(local)
         td.init_process_group(backend=backend)
         dist = td
     elif args.gpus != 1:
@@ -100,8 +168,10 @@ def dist_setup(args):
 
 def barrier_sync(dist, solver, local):
     """Device sync (the solver's stream carries all of its work) + barrier across ranks.  At N = 1
-    torch is never imported, so the process holds exactly one HIP runtime, the library's."""
-    solver.synchronize()
+    the headline legs never import torch before the config-5 leg, so the process holds one HIP
+    runtime, torch's (odesat_amd/_lib.py)."""
+    if solver is not None:
+        solver.synchronize()
     if dist is not None:
         import torch
         if torch.cuda.is_available():
@@ -109,16 +179,17 @@ def barrier_sync(dist, solver, local):
         dist.barrier()
 
 
-def time_gpu(solver, steps, warmup, dist, local, profile, stop):
+def time_gpu(solver, steps, warmup, dist, local, profile, stop, adaptive=False):
     """Warmup, then `steps` steps (one persistent launch; STOP_ANY may end earlier) between barrier +
     sync pairs."""
     from odesat_amd.system import ODESAT_STOP_NONE
+    kw = dict(adaptive=adaptive, dt=0.01, tol=1e-3, stop=stop)
     if warmup:
-        solver.simulate(dt=0.01, max_steps=warmup, stop=stop, poll_interval=warmup)
+        solver.simulate(max_steps=warmup, poll_interval=warmup, **kw)
     solver.profile(profile)
     barrier_sync(dist, solver, local)
     t0 = time.perf_counter()
-    r = solver.simulate(dt=0.01, max_steps=steps, stop=stop, poll_interval=steps)
+    r = solver.simulate(max_steps=steps, poll_interval=steps, **kw)
     barrier_sync(dist, solver, local)
     t1 = time.perf_counter()
     ms, launches = solver.profile_read() if profile else (None, None)
@@ -156,16 +227,103 @@ def cpu_baseline(cp, var, neg, n, m, replicas, steps, threads=1):
                       f"({dt:.1f} s)"}
 
 
-def load_profile(profile_dir, short, B, dtype, config):
+def load_profile(profile_dir, short, B, dtype, config, mode="fixed"):
     """PMC fits of one kernel on this workload (scripts/make_profile_json.py), or None."""
-    path = os.path.join(profile_dir, f"profile_{short}.json")
-    if not os.path.exists(path):
-        return None
-    with open(path) as fh:
-        pj = json.load(fh)
-    if pj.get("batch") != B or pj.get("dtype") != dtype or pj.get("config") != config:
-        return None
-    return pj
+    for path in sorted(glob.glob(os.path.join(profile_dir, "profile_*.json"))):
+        try:
+            with open(path) as fh:
+                pj = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if (pj.get("kernel") == short and pj.get("batch") == B and pj.get("dtype") == dtype
+                and pj.get("config") == config and pj.get("mode", "fixed") == mode):
+            pj["file"] = os.path.relpath(path, ROOT)
+            return pj
+    return None
+
+
+def state_digest(v, xs, xl):
+    """64-bit digest of replica states (the bits of the f64 copies of the device state)."""
+    import numpy as np
+    h = hashlib.sha256()
+    for a in (v, xs, xl):
+        h.update(np.ascontiguousarray(a, np.float64).tobytes())
+    return int.from_bytes(h.digest()[:8], "little", signed=True)
+
+
+def gather_ints(dist, x):
+    """[x of rank 0, ..., x of rank world-1] (int64 all-gather); [x] without a process group."""
+    if dist is None:
+        return [int(x)]
+    import torch
+    from odesat_amd.sharding import _device
+    dev = _device(dist)
+    t = torch.tensor([int(x)], dtype=torch.int64, device=dev)
+    out = torch.zeros(dist.get_world_size(), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(out, t)
+    return [int(y) for y in out.cpu().tolist()]
+
+
+KERNELS = {
+    "k_resident": "k_resident (persistent; v in LDS, clause memories streamed through HBM every step)",
+    "k_onchip": "k_onchip (persistent; the whole replica state on one CU: v/dv in LDS, clause memories in VGPRs)",
+    "k_wave": "k_wave (persistent; small instances, one replica per wave team, the state in LDS)",
+    "k_step": "k_step (FUSED: one launch per step; lane = (variable, replica), clause terms folded in clause order)",
+    "k_clause_u": "k_clause_u (TWOPASS clause pass)",
+}
+
+
+def roofline(args, short, ms, launches, clause_bytes_step, batch=None, dtype=None, config=None, mode="fixed",
+             steps=None):
+    """Dominant kernel (`short`, as odesat_step_kernel names it).  HBM side: algorithmic bytes per
+    launch ((8n + 16m) B per fp32 replica-step -- v, xs, xl read and written once; 3x
+    for an adaptive step -- x the replica-steps of one launch) / its mean launch time (HIP events on
+    the solver's stream), and the PMC HBM bytes of a launch of this size (profile fit: fixed +
+    per-step bytes).  k_onchip keeps the state on the CU, so HBM does not bound it: its roofline is
+    VALU issue -- PMC VALU instructions of a launch of this size / the launch time, against 1024
+    SIMDs x one wave64 instruction per 2 cycles at 2.4 GHz."""
+    batch = batch or args.batch
+    dtype = dtype or args.dtype
+    config = config or args.config
+    steps = steps or args.steps
+    kernel = KERNELS.get(short, short)
+    nlaunch = int(launches[0])
+    per_launch_s = ms[0] / 1e3 / nlaunch
+    steps_per_launch = steps / nlaunch
+    per_launch_bytes = clause_bytes_step * steps_per_launch
+    hbm_alg = per_launch_bytes / per_launch_s / 1e9
+    pj = load_profile(args.profile_dir, short, batch, dtype, config, mode)
+    traffic = valu = None
+    if pj is not None:
+        traffic = pj["hbm_bytes_fixed"] + pj["hbm_bytes_per_step"] * steps_per_launch
+        if "valu_insts_per_step" in pj:
+            valu = pj["valu_insts_fixed"] + pj["valu_insts_per_step"] * steps_per_launch
+    r = {"kernel": kernel, "traffic": traffic, "mean_launch_us": per_launch_s * 1e6, "launches": nlaunch,
+         "steps_per_launch": steps_per_launch, "algorithmic_bytes_per_launch": per_launch_bytes,
+         "profile": pj["file"] if pj else None}
+    hbm = {"achieved": hbm_alg, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_alg / HBM_PEAK_GBS}
+    if short == "k_onchip" and valu is not None:
+        achieved = valu / per_launch_s / 1e9
+        r.update({"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_GINST,
+                  "unit": "G VALU wave-instructions/s", "frac": achieved / VALU_PEAK_GINST,
+                  "valu_insts_per_launch": valu, "hbm_algorithmic": hbm,
+                  "note": "k_onchip keeps v, dv and the clause memories on the CU for a whole launch: HBM "
+                          "moves the state once per launch (traffic), so the HBM-algorithmic rate exceeds "
+                          "the HBM peak and the binding resource is the CU's VALU issue (plus LDS/barrier "
+                          "latency; DESIGN.md §4.0).  ab_hbm_streaming is the HBM-bound kernel on the same "
+                          "workload."})
+    else:
+        r.update({"bound": "hbm", **hbm})
+    return r
+
+
+def formula_of(config):
+    from odesat_amd import cnf
+    from odesat_amd import workloads as wl
+    c = wl.CONFIGS[config]
+    var, neg = wl.random_ksat(c["n"], c["m"], c["k"], c["seed"])
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    return c, cp, v_, n_, cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
 
 
 def main():
@@ -173,105 +331,78 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         spawn_ranks(args)
     world, rank, local, dist, devices = dist_setup(args)
+    legs = [x for x in LEGS if x not in args.skip_legs]
 
-    from odesat_amd import cnf
-    from odesat_amd import workloads as wl
+    from odesat_amd import _lib
     from odesat_amd.sharding import max_over_ranks, shard_range
     from odesat_amd.system import ODESAT_STOP_ANY, ODESAT_STOP_NONE, Solver
 
-    c = wl.CONFIGS[args.config]
+    c, cp, v_, n_, f = formula_of(args.config)
     n, m = c["n"], c["m"]
-    var, neg = wl.random_ksat(n, m, c["k"], c["seed"])
-    cp, v_, n_ = wl.formula_arrays(var, neg)
-    f = cnf.CNFFormula.from_arrays(cp, v_, n_, n)
     B = args.batch
 
-    def run_batch(batch, profile, alg_name=None, stop=ODESAT_STOP_NONE):
-        from odesat_amd import _lib
-        s = Solver(f, batch, args.dtype, device=local)
+    def run_batch(batch, profile, alg_name=None, stop=ODESAT_STOP_NONE, dtype=None, adaptive=False, formula=None):
+        s = Solver(formula or f, batch, dtype or args.dtype, device=local)
         if args.chunk:
             s.set_chunk_replicas(args.chunk)
         alg_name = alg_name or args.alg
         if alg_name != "auto":
             s.set_algorithm(getattr(_lib, "ODESAT_ALG_" + alg_name.upper()))
         s.init_state(42, replica0=shard_range(rank, world, batch)[0])
-        wall, ms, launches, ran = time_gpu(s, args.steps, args.warmup, dist, local, profile, stop)
-        bytes_step = s.clause_kernel_bytes()
-        alg = s.algorithm
+        wall, ms, launches, ran = time_gpu(s, args.steps, args.warmup, dist, local, profile, stop, adaptive)
+        bytes_step = s.clause_kernel_bytes() * (3 if adaptive else 1)
+        kern = s.step_kernel(adaptive)
         s.close()
-        return wall, ms, launches, bytes_step, alg, ran
+        return wall, ms, launches, bytes_step, kern, ran
 
-    def roofline(alg, ms, launches, clause_bytes_step):
-        """Dominant kernel.  HBM side: algorithmic bytes per launch ((8n + 16m) B per
-        fp32 replica-step -- v, xs, xl read and written once -- x the replica-steps of one launch) / its
-        mean launch time (HIP events on the solver's stream), and the PMC HBM bytes of a launch of this
-        size (profile fit: fixed + per-step bytes).  k_onchip keeps the state on the CU, so HBM does not
-        bound it: its roofline is VALU issue -- PMC VALU instructions of a launch of this size / the
-        launch time, against 1024 SIMDs x one wave64 instruction per 2 cycles at 2.4 GHz."""
-        from odesat_amd._lib import ODESAT_ALG_ONCHIP, ODESAT_ALG_RESIDENT
-        kernel = {ODESAT_ALG_RESIDENT: "k_resident (persistent; v in LDS, clause memories streamed through HBM "
-                                       "every step)",
-                  ODESAT_ALG_ONCHIP: "k_onchip (persistent; the whole replica state on one CU: v/dv in LDS, "
-                                     "clause memories in VGPRs)"}.get(alg, "k_step (fused RHS + Euler update)")
-        short = kernel.split(" ")[0]
-        nlaunch = int(launches[0])
-        per_launch_s = ms[0] / 1e3 / nlaunch
-        steps_per_launch = args.steps / nlaunch
-        per_launch_bytes = clause_bytes_step * steps_per_launch
-        hbm_alg = per_launch_bytes / per_launch_s / 1e9
-        pj = load_profile(args.profile_dir, short, B, args.dtype, args.config)
-        traffic = valu = None
-        if pj is not None:
-            traffic = pj["hbm_bytes_fixed"] + pj["hbm_bytes_per_step"] * steps_per_launch
-            if "valu_insts_per_step" in pj:
-                valu = pj["valu_insts_fixed"] + pj["valu_insts_per_step"] * steps_per_launch
-        r = {"kernel": kernel, "traffic": traffic, "mean_launch_us": per_launch_s * 1e6, "launches": nlaunch,
-             "steps_per_launch": steps_per_launch, "algorithmic_bytes_per_launch": per_launch_bytes}
-        hbm = {"achieved": hbm_alg, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_alg / HBM_PEAK_GBS}
-        if alg == ODESAT_ALG_ONCHIP and valu is not None:
-            achieved = valu / per_launch_s / 1e9
-            r.update({"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_GINST,
-                      "unit": "G VALU wave-instructions/s", "frac": achieved / VALU_PEAK_GINST,
-                      "valu_insts_per_launch": valu, "hbm_algorithmic": hbm,
-                      "note": "k_onchip keeps v, dv and the clause memories on the CU for a whole launch: HBM "
-                              "moves the state once per launch (traffic), so the HBM-algorithmic rate exceeds "
-                              "the HBM peak and the binding resource is the CU's VALU issue (plus LDS/barrier "
-                              "latency; DESIGN.md §4.0).  ab_hbm_streaming is the HBM-bound kernel on the same "
-                              "workload."})
-        else:
-            r.update({"bound": "hbm", **hbm})
-        return r
-
-    from odesat_amd._lib import ODESAT_ALG_ONCHIP
-    wall, ms, launches, clause_bytes_step, alg, _ = run_batch(B, True)
+    # ------------------------------------------------------------------------------ headline ---
+    wall, ms, launches, clause_bytes_step, kern, _ = run_batch(B, True)
     wall_max = max_over_ranks(dist, wall)
-    total_replica_steps = B * world * args.steps
-    value = total_replica_steps / wall_max
+    value = B * world * args.steps / wall_max
     ms_per_step = wall_max * 1e3 / args.steps
-    roof = roofline(alg, ms, launches, clause_bytes_step)
+    roof = roofline(args, kern, ms, launches, clause_bytes_step)
     tsize = 4 if args.dtype == "f32" else 8
     step_bytes = B * (2 * n + 4 * m) * tsize  # algorithmic per GPU-step: v, xs, xl read + written once
+    res = {}
 
-    ab = None
-    if alg == ODESAT_ALG_ONCHIP and not args.no_ab:
-        w3, ms3, l3, b3, a3, _ = run_batch(B, True, "resident")
-        w3 = max_over_ranks(dist, w3)
-        ab = {"value": B * world * args.steps / w3, "ms_per_step": w3 * 1e3 / args.steps,
-              "roofline": roofline(a3, ms3, l3, b3)}
+    def simple_leg(name, **kw):
+        w, ms_, l_, b_, a_, ran = run_batch(B, True, **kw)
+        w = max_over_ranks(dist, w)
+        mode = "adaptive" if kw.get("adaptive") else "fixed"
+        res[name] = {"value": B * world * ran / w, "unit": "replica-steps/s", "ms_per_step": w * 1e3 / ran,
+                     "steps_run": ran, "dtype": "fp64" if kw.get("dtype") == "f64" else "fp32",
+                     "step": "adaptive tol 1e-3 (per-replica dt)" if kw.get("adaptive") else "fixed dt 0.01",
+                     "batch_per_gpu": B, "kernel": a_,
+                     "roofline": roofline(args, a_, ms_, l_, b_, dtype=kw.get("dtype"), mode=mode, steps=ran)}
 
-    inter = None
-    if not args.no_inter:  # simulate_inter (STOP_ANY): multi-step launches with replay at the stop step
+    if "f64" in legs and args.config == "config2" and args.dtype == "f32":
+        simple_leg("f64", dtype="f64")
+    if "adaptive" in legs and args.config == "config2":
+        simple_leg("adaptive", adaptive=True)
+
+    if "inter" in legs:  # simulate_inter (STOP_ANY): multi-step launches with replay at the stop step
         ri = run_batch(B, False, stop=ODESAT_STOP_ANY)
         wi, ran = max_over_ranks(dist, ri[0]), ri[5]  # a stop before `steps` ends the run early
-        inter = {"value": B * world * ran / wi, "ms_per_step": wi * 1e3 / ran, "steps_run": ran,
-                 "vs_stop_none": (B * world * ran / wi) / value}
+        res["inter"] = {"value": B * world * ran / wi, "ms_per_step": wi * 1e3 / ran, "steps_run": ran,
+                        "vs_stop_none": (B * world * ran / wi) / value}
 
-    extra = None
-    if args.extra_batch and args.extra_batch != B:
+    if "config4" in legs:
+        res["inter_config4"] = config4_leg(args, world, rank, local, dist)
+
+    # ------------------------------------------ config 5: one instance partitioned over the ranks ---
+    if "config5" in legs:
+        res["partition_config5"] = config5_leg(args, world, rank, local, dist)
+
+    if "extra" in legs and args.extra_batch != B:
         w2 = max_over_ranks(dist, run_batch(args.extra_batch, False)[0])
-        extra = {"batch_per_gpu": args.extra_batch,
-                 "value": args.extra_batch * world * args.steps / w2,
-                 "ms_per_step": w2 * 1e3 / args.steps}
+        res["extra_batch"] = {"batch_per_gpu": args.extra_batch, "value": args.extra_batch * world * args.steps / w2,
+                              "ms_per_step": w2 * 1e3 / args.steps}
+
+    if "ab" in legs and kern == "k_onchip":
+        w3, ms3, l3, b3, a3, _ = run_batch(B, True, "resident")
+        w3 = max_over_ranks(dist, w3)
+        res["ab_hbm_streaming"] = {"value": B * world * args.steps / w3, "ms_per_step": w3 * 1e3 / args.steps,
+                                   "roofline": roofline(args, a3, ms3, l3, b3)}
 
     cpu = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -304,13 +435,202 @@ def main():
             "step_algorithmic_GBps": step_bytes * args.steps / wall / 1e9,
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
-            "inter": inter,
-            "extra_batch": extra,
-            "ab_hbm_streaming": ab,
+            **res,
         }
         print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def config4_leg(args, world, rank, local, dist, solver_cls=None, config="config4", batch=1024):
+    """BASELINE configs[3]: inter mode on n = 50k, m = 210k, B = `batch` replicas per rank (global
+    replica index rank * batch + b), sharded with no collective on the data path; the ranks agree on
+    the stop step through sharding.run_inter (lock-step chunks from a device checkpoint, one int64
+    MIN all-reduce per chunk, rollback of ranks that ran past it).  Timed like the headline; then the
+    same steps without the protocol (STOP_NONE) for its overhead.  Digest: rank 0 re-integrates the
+    first DIGEST_REPLICAS replicas of every rank in a batch of their own and compares state hashes.
+    solver_cls / config / batch: tests drive the same code with a host stand-in on a small instance."""
+    from odesat_amd.sharding import INTER_LOCKSTEP_CHUNK, NO_SAT, max_over_ranks, run_inter, shard_range
+    from odesat_amd.system import ODESAT_STOP_NONE
+    if solver_cls is None:
+        from odesat_amd.system import Solver as solver_cls
+    c4, _, _, _, f4 = formula_of(config)
+    r0 = shard_range(rank, world, batch)[0]
+    kw = dict(dt=0.01, poll_interval=64)
+    with solver_cls(f4, batch, "f32", device=local) as s:
+        s.init_state(42, replica0=r0)
+        if args.warmup:
+            s.simulate(max_steps=args.warmup, stop=ODESAT_STOP_NONE, **kw)
+        s.init_state(42, replica0=r0)  # the timed run starts at step 0 of the inter protocol
+        s.profile(True)
+        barrier_sync(dist, s, local)
+        t0 = time.perf_counter()
+        (wstep, wrep), ran = run_inter(dist, s, r0, max_steps=args.steps, chunk=INTER_LOCKSTEP_CHUNK, **kw)
+        barrier_sync(dist, s, local)
+        w_inter = max_over_ranks(dist, time.perf_counter() - t0)
+        ms4, l4 = s.profile_read()
+        s.profile(False)
+        kern4 = s.step_kernel()
+        b4 = s.clause_kernel_bytes()
+        q = min(DIGEST_REPLICAS, batch)
+        digests = gather_ints(dist, state_digest(*s.get_state(0, q)))
+        # the same steps without the stop protocol (STOP_NONE, one run): the protocol's overhead
+        s.init_state(42, replica0=r0)
+        barrier_sync(dist, s, local)
+        t0 = time.perf_counter()
+        s.simulate(max_steps=ran, stop=ODESAT_STOP_NONE, **kw)
+        barrier_sync(dist, s, local)
+        w_none = max_over_ranks(dist, time.perf_counter() - t0)
+    digest = None
+    if rank == 0:  # every replica on every rank ran exactly `ran` steps (the inter stop included)
+        ok = []
+        with solver_cls(f4, q, "f32", device=local) as chk:
+            for r in range(world):
+                chk.init_state(42, replica0=shard_range(r, world, batch)[0])
+                chk.simulate(max_steps=ran, stop=ODESAT_STOP_NONE, **kw)
+                ok.append(state_digest(*chk.get_state()) == digests[r])
+        digest = {"match": all(ok), "ranks_checked": world, "replicas_per_rank": q,
+                  "method": "rank 0 re-integrates the first replicas of every rank (global indices r*B ..) for "
+                            "the steps the protocol ran, on its own GPU, in a batch of their own; sha256 of the "
+                            "f64 copy of the state (v, xs, xl) equal bit for bit"}
+    return {
+        "value": batch * world * ran / w_inter, "unit": "replica-steps/s", "ms_per_step": w_inter * 1e3 / ran,
+        "steps_run": ran, "batch_per_gpu": batch, "global_batch": batch * world, "scaling": "weak",
+        "workload": f"{config}: random 3-SAT n={c4['n']} m={c4['m']} seed={c4['seed']}, inter mode, fixed dt "
+                    f"0.01, f32; sharding.run_inter over {dist.get_backend() if dist else 'one rank'} (chunks of "
+                    f"{INTER_LOCKSTEP_CHUNK} steps from a device checkpoint, MIN all-reduce of the stop step, "
+                    "rollback)",
+        "winner": None if wstep == NO_SAT else {"step": wstep, "replica": wrep},
+        "stop_none_value": batch * world * ran / w_none, "stop_protocol_overhead": w_inter / w_none - 1.0,
+        "kernel": kern4,
+        "roofline": roofline(args, kern4, ms4, l4, b4, batch=batch, dtype="f32", config=config, steps=ran),
+        "digest": digest}
+
+
+def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5"):
+    """BASELINE configs[4]: one replica of n = 1M, m = 4.2M partitioned over the ranks (strong
+    scaling), every partition.  A step = the rank's kernels + its collective(s) over
+    RCCL, captured in one HIP graph per timed run (gloo, host-staged, runs eagerly).  Digest: every
+    partition's final voltages against a world-1 VARIABLES run of the same steps on rank 0.
+    part_cls / config: tests drive the same code with a host stand-in on a small instance."""
+    import numpy as np
+    import torch
+
+    from odesat_amd import workloads as wl
+    from odesat_amd.partition import CLAUSES, CLAUSES_RS, VARIABLES, LocalComm, TorchComm, default_zeta
+    from odesat_amd.sharding import max_over_ranks
+    if part_cls is None:
+        from odesat_amd.partition import PartitionedSolver as part_cls
+
+    gpu = torch.cuda.is_available()
+    if gpu:
+        torch.cuda.set_device(local)
+
+    def sync():
+        if gpu:
+            torch.cuda.synchronize(local)
+        if dist is not None:
+            dist.barrier()
+
+    c = wl.CONFIGS[config]
+    n, m = c["n"], c["m"]
+    var, neg = wl.random_ksat(n, m, c["k"], c["seed"])
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    del var, neg
+    v0 = wl.init_voltages(42, 0, 1, n)[0]
+    xs0 = np.where(n_.reshape(m, 3).any(axis=1), 1.0, -1.0)  # system.rs:361-372 (every clause has 3 literals)
+    xl0 = np.ones(m)
+    zeta = default_zeta(n, m)
+    dt = 0.01
+    total = args.warmup + args.steps
+    comm = TorchComm(dist) if dist is not None else LocalComm()
+    out = {"workload": f"{config}: random 3-SAT n={n} m={m} seed={c['seed']}, ONE replica, fixed dt 0.01, f32, "
+                       f"partitioned over {world} rank(s)", "scaling": "strong", "unit": "steps/s",
+           "backend": dist.get_backend() if dist is not None else None}
+    finals = {}
+    for name, mode in (("clauses", CLAUSES), ("clauses_rs", CLAUSES_RS), ("variables", VARIABLES)):
+        t0 = time.perf_counter()
+        ps = part_cls(cp, v_, n_, n, mode, comm=comm, device=local)
+        setup = time.perf_counter() - t0
+        ps.set_state(v0, xs0, xl0)
+        for _ in range(args.warmup):
+            ps.step(dt, zeta, stop=False)
+        g = None
+        if ps.capturable():
+            gsteps = args.config5_graph or args.steps
+            if args.steps % gsteps:
+                raise SystemExit("bench.py: --steps must be a multiple of --config5-graph")
+            g = ps.graph(gsteps, dt, zeta, stop=False)  # captured, not run
+        if gpu:  # HIP events on the stream the partition's kernels and collectives run on
+            stream = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        sync()
+        t0 = time.perf_counter()
+        if gpu:
+            e0.record(stream)
+        if g is not None:
+            for _ in range(args.steps // gsteps):
+                g.replay()
+        else:
+            for _ in range(args.steps):
+                ps.step(dt, zeta, stop=False)
+        if gpu:
+            e1.record(stream)
+        sync()
+        t1 = time.perf_counter()
+        wall = max_over_ranks(dist, t1 - t0)
+        gpu_ms = e0.elapsed_time(e1) if gpu else (t1 - t0) * 1e3
+        st = ps.status(stop=False)
+        assert st["steps_done"] == total, "a partitioned step was skipped"
+        finals[name] = ps.get_state()[0] if rank == 0 else None
+        mloc = len(ps.topo["clauses"])
+        # SURVEY.md §8d per rank and step: v read + written (8n) and the local memories read + written
+        # (16 mloc); the exchanged bytes on top
+        alg_bytes = 8 * n + 16 * mloc
+        per_step_s = gpu_ms / 1e3 / args.steps
+        achieved = alg_bytes / per_step_s / 1e9
+        out[name] = {
+            "value": args.steps / wall, "ms_per_step": wall * 1e3 / args.steps,
+            "collective": {"clauses": "all_reduce", "clauses_rs": "reduce_scatter + all_gather",
+                           "variables": "all_gather"}[name],
+            "exchange_bytes_per_rank": ps.exchange_bytes(), "local_clauses_rank0": mloc,
+            "graph_steps": gsteps if g is not None else 0, "setup_s": setup,
+            "roofline": {"bound": "hbm", "kernel": "k_part_clause3 + k_part_var (+ collective), per step",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "algorithmic_bytes_per_step": alg_bytes, "gpu_ms_per_step": per_step_s * 1e3,
+                         "traffic": None,
+                         "note": "bytes = SURVEY.md §8d (v and the rank's clause memories read and written once); "
+                                 "the step is bound by 12.6M/world random 4-byte gathers and the term hand-off, "
+                                 "not streaming: see DESIGN.md §5.1 for the measured random-access ceiling"}}
+        ps.close()
+        del ps, g
+        if gpu:
+            torch.cuda.empty_cache()
+    digest = None
+    if rank == 0:
+        if world == 1:
+            ref = finals["variables"]
+        else:  # the same steps at world 1 on this GPU: the reference trajectory
+            ps = part_cls(cp, v_, n_, n, VARIABLES, comm=LocalComm(), device=local)
+            ps.set_state(v0, xs0, xl0)
+            if ps.capturable():
+                ps.graph(total, dt, zeta, stop=False).replay()
+            else:
+                for _ in range(total):
+                    ps.step(dt, zeta, stop=False)
+            ref = ps.get_state()[0]
+            ps.close()
+            del ps
+            if gpu:
+                torch.cuda.empty_cache()
+        diffs = {k: float(np.max(np.abs(finals[k] - ref))) for k in finals}
+        digest = {"reference": "world-1 VARIABLES run of the same warmup + timed steps (bit-exact to the oracle's "
+                               "f32 restatement, tests/test_gpu_configs.py)", "steps": total,
+                  "max_abs_v_diff": diffs, "variables_bit_exact": diffs["variables"] == 0.0,
+                  "clauses_within_tol": diffs["clauses"] <= CLAUSES_TOL,
+                  "clauses_rs_within_tol": diffs["clauses_rs"] <= CLAUSES_TOL, "tol": CLAUSES_TOL}
+    out["digest"] = digest
+    return out
 
 
 if __name__ == "__main__":

@@ -290,6 +290,9 @@ int odesat_set_algorithm(odesat_solver *s, int alg);
 /* The algorithm odesat_simulate uses (ODESAT_ALG_*), and the solver's replica group width. */
 int odesat_get_algorithm(const odesat_solver *s);
 int odesat_group_width(const odesat_solver *s);
+/* The step kernel odesat_simulate launches for fixed (adaptive = 0) or adaptive steps: "k_onchip",
+ * "k_resident", "k_wave", "k_step" (FUSED) or "k_clause_u" (TWOPASS); NULL for a null solver. */
+const char *odesat_step_kernel(const odesat_solver *s, int adaptive);
 
 /* --------------------------------------------- one instance across GPUs ------- */
 
@@ -306,6 +309,14 @@ int odesat_group_width(const odesat_solver *s);
  *                          its unsat count (out[S]); the caller all-gathers the world blocks of
  *                          S + 1 floats, which are the next step's voltages (variable i at
  *                          i + i / S).  Bit-exact for any world size.
+ *   ODESAT_PART_CLAUSES_RS rank r holds a slice of the clauses, as CLAUSES, and v in VARIABLES'
+ *                          gathered layout (block = S, full range v0 = 0, v1 = n).  odesat_part_rhs
+ *                          (apply = 2) writes the partial dv of every variable at out[i + i / S] and
+ *                          the rank's unsat count in every block's flag slot; the caller
+ *                          reduce-scatters (sum) out onto its block of S + 1 floats, calls
+ *                          odesat_part_reduce_apply, and all-gathers the send blocks into v.  The
+ *                          all-reduce split into its two halves; tolerance parity
+ *                          as CLAUSES (bit-exact at world = 1).
  * world = the number of ranks.  Local topology: clause_ptr[mloc + 1], var[L], neg[L] of the local clauses in the reference's clause
  * order; var_ptr[v1 - v0 + 1] / inc_slot[] = for each variable of [v0, v1), its local literal slots
  * in clause-then-literal order; block = S (VARIABLES) or 0 (CLAUSES, plain v[n]).  m = the global
@@ -313,6 +324,7 @@ int odesat_group_width(const odesat_solver *s);
  * `stream` is a hipStream_t (NULL = the default stream). */
 #define ODESAT_PART_CLAUSES 0
 #define ODESAT_PART_VARIABLES 1
+#define ODESAT_PART_CLAUSES_RS 2
 typedef struct odesat_part odesat_part;
 int odesat_part_create(int device, int world, int64_t n, int64_t m, int64_t mloc, const int64_t *clause_ptr,
                        const int64_t *var, const uint8_t *neg, int64_t v0, int64_t v1,
@@ -323,7 +335,7 @@ int64_t odesat_part_device_bytes(const odesat_part *p);
 /* the local clauses' memories, in local clause order (f64 host arrays of mloc) */
 int odesat_part_set_memories(odesat_part *p, const double *xs, const double *xl);
 int odesat_part_get_memories(odesat_part *p, double *xs, double *xl);
-/* Enqueue one right-hand side + memory update; apply = 0 (CLAUSES) or 1 (VARIABLES).  Before it,
+/* Enqueue one right-hand side + memory update; apply = 0 (CLAUSES), 1 (VARIABLES) or 2 (CLAUSES_RS).  Before it,
  * the previous step's global unsat count (read from v's flag slots or out[n]) is folded into the
  * replica's bookkeeping; stop = 1: the first allsat step freezes the replica (simulate,
  * system.rs:193) and later steps are no-ops, so callers may poll at any interval. */
@@ -331,6 +343,11 @@ int odesat_part_rhs(odesat_part *p, const float *v, float *out, double dt, doubl
                     int stop, void *stream);
 /* CLAUSES: v[i] = clamp(v[i] + dt * dvsum[i]) after the all-reduce (system.rs:96) */
 int odesat_part_apply(odesat_part *p, float *v, const float *dvsum, double dt, void *stream);
+/* CLAUSES_RS: after the reduce-scatter, rank `rank`'s voltages (v[i + rank], i in its block) take the
+ * summed dv of `block` (S + 1 floats, the last the summed unsat count) into `send` (S + 1 floats:
+ * the updated voltages, then that count), the all-gather's input (system.rs:96). */
+int odesat_part_reduce_apply(odesat_part *p, const float *v, const float *block, float *send, int rank,
+                             double dt, void *stream);
 /* Restart the bookkeeping (steps done 0, no sat step, not frozen). */
 int odesat_part_reset(odesat_part *p, void *stream);
 /* Fold the last step's unsat count and read the bookkeeping (synchronises `stream`). */

@@ -17,7 +17,7 @@ ODESAT_F32, ODESAT_F64 = 0, 1
 ODESAT_STOP_EACH, ODESAT_STOP_ANY, ODESAT_STOP_NONE = 0, 1, 2
 ODESAT_SCHED_AUTO, ODESAT_SCHED_STEP_MAJOR, ODESAT_SCHED_CHUNK_MAJOR = 0, 1, 2
 ODESAT_ALG_FUSED, ODESAT_ALG_TWOPASS, ODESAT_ALG_RESIDENT, ODESAT_ALG_ONCHIP = 0, 1, 2, 3
-ODESAT_PART_CLAUSES, ODESAT_PART_VARIABLES = 0, 1
+ODESAT_PART_CLAUSES, ODESAT_PART_VARIABLES, ODESAT_PART_CLAUSES_RS = 0, 1, 2
 ODESAT_STEP_VARIABLE_ELIMINATION, ODESAT_STEP_BLOCKED_CLAUSE, ODESAT_UNSET = 0, 1, 2
 
 
@@ -101,6 +101,7 @@ SIGNATURES = {
     "odesat_set_algorithm": (C.c_int, [_P, C.c_int]),
     "odesat_get_algorithm": (C.c_int, [_P]),
     "odesat_group_width": (C.c_int, [_P]),
+    "odesat_step_kernel": (C.c_char_p, [_P, C.c_int]),
     "odesat_part_create": (C.c_int, [C.c_int, C.c_int, _i64, _i64, _i64, _i64p, _i64p, _u8p, _i64, _i64, _i64p,
                                      _i64p, _i64, C.POINTER(_P)]),
     "odesat_part_destroy": (None, [_P]),
@@ -109,6 +110,7 @@ SIGNATURES = {
     "odesat_part_get_memories": (C.c_int, [_P, _dp, _dp]),
     "odesat_part_rhs": (C.c_int, [_P, _P, _P, C.c_double, C.c_double, C.c_int, C.c_int, _P]),
     "odesat_part_apply": (C.c_int, [_P, _P, _P, C.c_double, _P]),
+    "odesat_part_reduce_apply": (C.c_int, [_P, _P, _P, _P, C.c_int, C.c_double, _P]),
     "odesat_part_reset": (C.c_int, [_P, _P]),
     "odesat_part_status": (C.c_int, [_P, _P, _P, C.c_int, C.c_int, _P, _i64p, _i64p, C.POINTER(C.c_int32)]),
 }

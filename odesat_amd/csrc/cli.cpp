@@ -255,7 +255,10 @@ void run_shard(const Opts &o, const odesat_cnf *norm, Shard &sh, int nshards, Ba
     }
     // inter over several shards
     const int64_t total = bounded ? o.steps : INT64_MAX;
-    const int64_t k_lock = o.has_steps ? std::min<int64_t>(chunk, 256) : std::min<int64_t>(chunk, 256);
+    // lock-step chunk: steps between the shards' stop agreements (each chunk starts from a device
+    // checkpoint).  The same value is sharding.run_inter's default (odesat_amd/sharding.py).
+    constexpr int64_t INTER_LOCKSTEP_CHUNK = 256;
+    const int64_t k_lock = std::min<int64_t>(chunk, INTER_LOCKSTEP_CHUNK);
     for (int64_t t = 0; t < total;) {
         const int64_t k = std::min(k_lock, total - t);
         p.max_steps = k;

@@ -1423,6 +1423,16 @@ extern "C" int odesat_get_algorithm(const odesat_solver *s) {
 
 extern "C" int odesat_group_width(const odesat_solver *s) { return s ? s->W : fail(ODESAT_EINVAL, "null solver"); }
 
+// the dispatch of simulate_impl / simulate_resident, named
+extern "C" const char *odesat_step_kernel(const odesat_solver *s, int adaptive) {
+    if (!s) return nullptr;
+    if ((s->alg == ODESAT_ALG_RESIDENT || s->alg == ODESAT_ALG_ONCHIP) && (!adaptive || s->res_ada)) {
+        if (s->alg == ODESAT_ALG_ONCHIP && !adaptive) return "k_onchip";
+        return s->res_wave ? "k_wave" : "k_resident";
+    }
+    return s->alg == ODESAT_ALG_TWOPASS ? "k_clause_u" : "k_step";
+}
+
 extern "C" int odesat_set_state(odesat_solver *s, int64_t r0, int64_t count, const double *v, const double *xs,
                                 const double *xl) {
     int rc;
@@ -1432,6 +1442,7 @@ extern "C" int odesat_set_state(odesat_solver *s, int64_t r0, int64_t count, con
     if ((rc = upload_items(s, s->c, xs, s->m, 2, 0, r0, count))) return rc;
     if ((rc = upload_items(s, s->c, xl, s->m, 2, 1, r0, count))) return rc;
     if ((rc = reset_replicas(s, r0, count))) return rc;
+    if ((rc = set_stop(s, INT_MAX))) return rc;  // a new state ends the run (and a STOP_ANY stop)
     auto within = [](const double *x, int64_t cnt, double lo, double hi) {
         if (!x) return true;
         for (int64_t i = 0; i < cnt; ++i)
@@ -1450,6 +1461,7 @@ extern "C" int odesat_init_state(odesat_solver *s, uint64_t seed, int64_t replic
     if ((rc = check_solver(s))) return rc;
     if ((rc = init_dispatch(s, seed, replica0, false))) return rc;
     if ((rc = reset_replicas(s, 0, s->Bp))) return rc;
+    if ((rc = set_stop(s, INT_MAX))) return rc;  // a new state ends the run (and a STOP_ANY stop)
     s->in_range = true;  // v in [-1, 1), xs = +-1, xl = 1
     s->t_base = 0;
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1556,7 +1568,7 @@ static int finish_simulate(odesat_solver *s, const odesat_params *p, bool adapti
     // after it were no-ops
     if (p->stop == ODESAT_STOP_ANY && *s->h_stop != INT_MAX)
         t_run = std::max<int64_t>(0, std::min<int64_t>(t_run, (int64_t)*s->h_stop - s->t_base + 1));
-    s->in_range = true;  // every replica that stepped took a clamped step
+    if (t_run > 0) s->in_range = true;  // every replica that stepped took a clamped step
     s->t_base += t_run;
     if (steps_run) *steps_run = t_run;
     if (first_sat_step) std::memcpy(first_sat_step, s->h_sat, s->B * 8);

@@ -15,8 +15,14 @@
 //              their updated voltages plus its unsat flag into a send block; the ranks
 //              all-gather the blocks, which form the next step's voltage array.  Bit-exact for any
 //              world size, and the exchange is half an all-reduce's bytes.
-// Gathered voltage layout (VARIABLES): world blocks of (S voltages, 1 unsat flag), so variable i
-// sits at i + i / S.  CLAUSES uses a plain v[n] (stride 0).
+//   CLAUSES_RS rank r owns a slice of the clauses, as CLAUSES, but the all-reduce is split into its
+//              two halves (SURVEY.md §8e's alternative): the partial dv of every variable is written
+//              in the gathered layout below and reduce-scattered (sum) onto the ranks' variable
+//              blocks; each rank updates its own block of voltages, and an all-gather of the blocks
+//              rebuilds v.  Same bytes as a ring all-reduce, with the voltage update done once per
+//              variable instead of on every rank; tolerance parity as CLAUSES (bit-exact at world 1).
+// Gathered voltage layout (VARIABLES, CLAUSES_RS): world blocks of (S voltages, 1 unsat flag), so
+// variable i sits at i + i / S.  CLAUSES uses a plain v[n] (stride 0).
 //
 // Arithmetic: the reference's expressions in the reference's order (system.rs:43-96), f32, with
 // the rigidity term -- identical to the oracle's f32 restatement for any state.
@@ -229,7 +235,10 @@ __global__ __launch_bounds__(256) void k_part_clause3(const void *__restrict__ l
 // ([chunk][j][64], padded to the chunk's largest degree): SLOT layout reads the slot there and
 // gathers its term, ELL layout reads the term itself there (the clause kernel put it there), both
 // coalesced.  CLAUSES (apply == 0): out[i] = partial dv[i].  VARIABLES (apply == 1): out[i - v0] =
-// the updated voltage (:96), v[i + voff] being variable i in the gathered layout.
+// the updated voltage (:96), v[i + voff] being variable i in the gathered layout.  CLAUSES_RS
+// (apply == 2): out[i + i / S] = partial dv[i], and block 0's unsat flag (out[S], set by the clause
+// kernel) is copied to the other world - 1 blocks' flag slots, so the reduce-scatter hands every
+// rank the global count.
 // REGION (RG > 0 regions, a multiple of 8): block b runs region x + 8 g (x = b % 8) with bpr blocks
 // per region, so every region's variables are folded on one residue class of blockIdx mod 8.
 template <bool ELL, bool REGION>
@@ -237,7 +246,10 @@ __global__ __launch_bounds__(256) void k_part_var(const int32_t *__restrict__ cs
                                                   const int32_t *__restrict__ islot, const float *__restrict__ w,
                                                   const float *__restrict__ v, int32_t voff, int32_t v0, int32_t v1,
                                                   float dt, int apply, float *__restrict__ out,
-                                                  const PartStat *__restrict__ st, int32_t RG, int32_t bpr) {
+                                                  const PartStat *__restrict__ st, int32_t RG, int32_t bpr,
+                                                  int32_t S, int32_t world) {
+    if (apply == 2 && blockIdx.x == 0 && (int32_t)threadIdx.x < world - 1)
+        out[(int64_t)(threadIdx.x + 1) * (S + 1) + S] = out[S];  // the clause kernel has finished
     int32_t k;
     if (REGION) {
         const int32_t nv = v1 - v0, x = (int32_t)(blockIdx.x % 8), kk = (int32_t)(blockIdx.x / 8);
@@ -251,9 +263,10 @@ __global__ __launch_bounds__(256) void k_part_var(const int32_t *__restrict__ cs
     }
     const int32_t i = v0 + k;
     if (i >= v1) return;
+    const int32_t oi = apply == 2 ? i + i / S : i;
     if (st->frozen) {  // the replica stopped: v is re-sent unchanged, no dv
-        if (apply) out[k] = v[i + voff];
-        else out[i] = 0.0f;
+        if (apply == 1) out[k] = v[i + voff];
+        else out[oi] = 0.0f;
         return;
     }
     const int32_t base = cstart[k >> 6] + (k & 63);
@@ -280,8 +293,8 @@ __global__ __launch_bounds__(256) void k_part_var(const int32_t *__restrict__ cs
                 if (j0 + u < d) dv += t[u];
         }
     }
-    if (apply) out[k] = fminf(fmaxf(v[i + voff] + dt * dv, -1.0f), 1.0f);
-    else out[i] = dv;
+    if (apply == 1) out[k] = fminf(fmaxf(v[i + voff] + dt * dv, -1.0f), 1.0f);
+    else out[oi] = dv;
 }
 
 // CLAUSES: v[i] = clamp(v[i] + dt * dvsum[i]) after the all-reduce (:96).
@@ -290,6 +303,19 @@ __global__ __launch_bounds__(256) void k_part_apply(float *__restrict__ v, const
     const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (st->frozen) return;
     if (i < n) v[i] = fminf(fmaxf(v[i] + dt * dvsum[i], -1.0f), 1.0f);
+}
+
+// CLAUSES_RS, after the reduce-scatter: rank r's voltages i in [r S, r S + cnt) (v[i + r] in the
+// gathered layout) take the summed dv of its block (:96) into the send block, whose flag slot carries
+// the summed unsat count on to the all-gather.
+__global__ __launch_bounds__(256) void k_part_reduce_apply(const float *__restrict__ v, const float *__restrict__ blk,
+                                                           float *__restrict__ send, int32_t S, int32_t rank,
+                                                           int32_t cnt, float dt, const PartStat *__restrict__ st) {
+    const int32_t k = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (k == 0) send[S] = blk[S];
+    if (k >= cnt) return;
+    const float vi = v[(int64_t)rank * S + k + rank];
+    send[k] = st->frozen ? vi : fminf(fmaxf(vi + dt * blk[k], -1.0f), 1.0f);
 }
 
 template <typename T> int upload(odesat_part *p, T **dst, const int64_t *src, int64_t count) {
@@ -319,8 +345,9 @@ extern "C" int odesat_part_create(int device, int world, int64_t n, int64_t m, i
                                   const int64_t *inc_slot, int64_t block, odesat_part **out) {
     if (!out) return fail(ODESAT_EINVAL, "null out");
     *out = nullptr;
+    // block > 0 with the full range [0, n): CLAUSES_RS (every variable folded, gathered layout)
     if (world < 1 || n <= 0 || m < 0 || mloc < 0 || mloc > m || !clause_ptr || v0 < 0 || v1 < v0 || v1 > n ||
-        block < 0 || (block > 0 && v1 - v0 > block))
+        block < 0 || (block > 0 && v1 - v0 > block && !(v0 == 0 && v1 == n)) || (block > 0 && world * block < n))
         return fail(ODESAT_EINVAL, "bad partition arguments");
     if (n >= (1ll << 29) || m >= INT32_MAX) return fail(ODESAT_EINVAL, "formula too large");
     const int64_t L = clause_ptr[mloc] - clause_ptr[0];
@@ -375,7 +402,7 @@ extern "C" int odesat_part_create(int device, int world, int64_t n, int64_t m, i
     std::vector<int64_t> ell((size_t)std::max<int64_t>(cstart[nchunk], 1), 0);
     for (int64_t k = 0; k < nv; ++k)
         for (int64_t j = 0; j < deg[k]; ++j) ell[cstart[k / 64] + 64 * j + (k % 64)] = inc_slot[var_ptr[k] + j];
-    p->voff = block > 0 ? v0 / block : 0;
+    p->voff = block > 0 && v1 - v0 <= block ? v0 / block : 0;
     // term layout: REGION (default), ELL or SLOT (ODESAT_PART_TERMS=region|ell|slot)
     p->terms = TERMS_REGION;
     if (const char *tl = std::getenv("ODESAT_PART_TERMS")) {
@@ -537,8 +564,9 @@ static void flag_src(const odesat_part *p, const float *v, const float *out, int
 extern "C" int odesat_part_rhs(odesat_part *p, const float *v, float *out, double dt, double zeta, int apply, int stop,
                                void *stream) {
     if (!p || !v || !out) return fail(ODESAT_EINVAL, "null argument");
-    if (apply != 0 && apply != 1) return fail(ODESAT_EINVAL, "apply must be 0 (CLAUSES) or 1 (VARIABLES)");
-    if (apply == 1 && p->S == 0) return fail(ODESAT_EINVAL, "VARIABLES needs a block size");
+    if (apply < 0 || apply > 2) return fail(ODESAT_EINVAL, "apply must be 0 (CLAUSES), 1 (VARIABLES) or 2 (CLAUSES_RS)");
+    if (apply != 0 && p->S == 0) return fail(ODESAT_EINVAL, "VARIABLES / CLAUSES_RS need a block size");
+    if (apply == 2 && (p->v0 != 0 || p->v1 != p->n)) return fail(ODESAT_EINVAL, "CLAUSES_RS folds every variable");
     PART_TRY(hipSetDevice(p->device));
     hipStream_t st = (hipStream_t)stream;
     const float *f;
@@ -583,15 +611,15 @@ extern "C" int odesat_part_rhs(odesat_part *p, const float *v, float *out, doubl
         if (p->terms == TERMS_ELL)
             hipLaunchKernelGGL((k_part_var<true, false>), dim3(blocks_for(nv)), dim3(256), 0, st, p->cstart, p->deg,
                                p->islot, p->w, v, (int32_t)p->voff, (int32_t)p->v0, (int32_t)p->v1, (float)dt, apply,
-                               out, p->stat, 0, 0);
+                               out, p->stat, 0, 0, (int32_t)p->S, p->world);
         else if (p->terms == TERMS_REGION)
             hipLaunchKernelGGL((k_part_var<false, true>), dim3((unsigned)(p->regions * bpr)), dim3(256), 0, st,
                                p->cstart, p->deg, p->islot, p->w, v, (int32_t)p->voff, (int32_t)p->v0, (int32_t)p->v1,
-                               (float)dt, apply, out, p->stat, (int32_t)p->regions, bpr);
+                               (float)dt, apply, out, p->stat, (int32_t)p->regions, bpr, (int32_t)p->S, p->world);
         else
             hipLaunchKernelGGL((k_part_var<false, false>), dim3(blocks_for(nv)), dim3(256), 0, st, p->cstart, p->deg,
                                p->islot, p->w, v, (int32_t)p->voff, (int32_t)p->v0, (int32_t)p->v1, (float)dt, apply,
-                               out, p->stat, 0, 0);
+                               out, p->stat, 0, 0, (int32_t)p->S, p->world);
     }
     PART_TRY(hipGetLastError());
     return ODESAT_OK;
@@ -602,6 +630,19 @@ extern "C" int odesat_part_apply(odesat_part *p, float *v, const float *dvsum, d
     PART_TRY(hipSetDevice(p->device));
     hipLaunchKernelGGL(k_part_apply, dim3(blocks_for(p->n)), dim3(256), 0, (hipStream_t)stream, v, dvsum,
                        (int32_t)p->n, (float)dt, p->stat);
+    PART_TRY(hipGetLastError());
+    return ODESAT_OK;
+}
+
+extern "C" int odesat_part_reduce_apply(odesat_part *p, const float *v, const float *block, float *send, int rank,
+                                        double dt, void *stream) {
+    if (!p || !v || !block || !send) return fail(ODESAT_EINVAL, "null argument");
+    if (p->S == 0 || p->v0 != 0 || p->v1 != p->n) return fail(ODESAT_EINVAL, "not a CLAUSES_RS slice");
+    if (rank < 0 || rank >= p->world) return fail(ODESAT_EINVAL, "rank out of range");
+    PART_TRY(hipSetDevice(p->device));
+    const int64_t cnt = std::max<int64_t>(0, std::min<int64_t>(p->S, p->n - (int64_t)rank * p->S));
+    hipLaunchKernelGGL(k_part_reduce_apply, dim3(blocks_for(std::max<int64_t>(cnt, 1))), dim3(256), 0,
+                       (hipStream_t)stream, v, block, send, (int32_t)p->S, rank, (int32_t)cnt, (float)dt, p->stat);
     PART_TRY(hipGetLastError());
     return ODESAT_OK;
 }

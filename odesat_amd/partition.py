@@ -18,6 +18,10 @@ Two partitions:
              dv of its own variables in the reference's order and updates them; one all-gather of
              S + 1 floats per rank (half an all-reduce's traffic) rebuilds v.  Bit-exact for any
              world size.
+  CLAUSES_RS the CLAUSES slice with the all-reduce split into its halves: the
+             partial dv is reduce-scattered (sum) onto the ranks' variable blocks of S, each rank
+             updates its own block, and an all-gather of the blocks rebuilds v (VARIABLES' layout).
+             Tolerance parity as CLAUSES (bit-exact at world = 1).
 The replica's bookkeeping (steps done, first sat step, frozen after it) lives on the device, so the
 host polls the stop condition at any interval without changing results.
 """
@@ -29,11 +33,14 @@ import numpy as np
 
 from . import _lib
 from ._lib import ODESAT_PART_CLAUSES as CLAUSES
+from ._lib import ODESAT_PART_CLAUSES_RS as CLAUSES_RS
 from ._lib import ODESAT_PART_VARIABLES as VARIABLES
 from ._lib import check, lib
 
-__all__ = ["CLAUSES", "VARIABLES", "block_size", "local_topology", "default_zeta", "PartitionedSolver",
-           "TorchComm", "LocalComm"]
+__all__ = ["CLAUSES", "CLAUSES_RS", "VARIABLES", "MODES", "block_size", "local_topology", "default_zeta",
+           "PartitionedSolver", "TorchComm", "LocalComm", "step_in_process"]
+
+MODES = {"clauses": CLAUSES, "variables": VARIABLES, "clauses_rs": CLAUSES_RS}
 
 
 def block_size(n: int, world: int) -> int:
@@ -64,10 +71,10 @@ def local_topology(cp, var, neg, n: int, mode: int, rank: int, world: int, order
     if not (0 <= rank < world):
         raise ValueError("bad rank / world")
     lens_all = np.diff(cp)
-    if mode == CLAUSES:
+    if mode in (CLAUSES, CLAUSES_RS):
         c0, c1 = rank * m // world, (rank + 1) * m // world
         local = np.arange(c0, c1, dtype=np.int64)
-        v0, v1, S = 0, n, 0
+        v0, v1, S = 0, n, (block_size(n, world) if mode == CLAUSES_RS else 0)
     elif mode == VARIABLES:
         S = block_size(n, world)
         v0, v1 = min(n, rank * S), min(n, (rank + 1) * S)
@@ -79,14 +86,14 @@ def local_topology(cp, var, neg, n: int, mode: int, rank: int, world: int, order
         touch[lens_all == 0] = rank == 0
         local = np.flatnonzero(touch).astype(np.int64)
     else:
-        raise ValueError("mode must be CLAUSES or VARIABLES")
+        raise ValueError("mode must be CLAUSES, VARIABLES or CLAUSES_RS")
     if order not in ("file", "minvar"):
         raise ValueError("order must be 'file' or 'minvar'")
     if order == "minvar" and len(local) and len(var):
         owner = np.repeat(np.arange(m, dtype=np.int64), lens_all)
         vmin = np.full(m, n, np.int64)
         np.minimum.at(vmin, owner, var)
-        local = local[np.argsort(vmin[local], kind="stable")]
+        local = local[np.argsort(vmin[local] * m + local)]  # unique keys: = a stable sort by vmin
     lens = lens_all[local]
     lcp = np.zeros(len(local) + 1, np.int64)
     np.cumsum(lens, out=lcp[1:])
@@ -94,7 +101,9 @@ def local_topology(cp, var, neg, n: int, mode: int, rank: int, world: int, order
     gslot = np.repeat(cp[local], lens) + (np.arange(L, dtype=np.int64) - np.repeat(lcp[:-1], lens))
     lvar, lneg = var[gslot], neg[gslot]
     sel = np.flatnonzero((lvar >= v0) & (lvar < v1))
-    inc = sel[np.lexsort((gslot[sel], lvar[sel]))]  # per variable: ascending global slot = clause, literal order
+    # per variable: ascending global slot = clause, literal order (one argsort of unique int64 keys;
+    # np.lexsort over the two columns is 3x slower at config 5's 12.6 M literals)
+    inc = sel[np.argsort(lvar[sel] * (int(cp[-1]) + 1) + gslot[sel])]
     counts = np.bincount(lvar[sel] - v0, minlength=v1 - v0)
     vptr = np.zeros(v1 - v0 + 1, np.int64)
     np.cumsum(counts, out=vptr[1:])
@@ -127,6 +136,16 @@ class TorchComm:
         else:
             self.dist.all_reduce(t)
 
+    def reduce_scatter_sum(self, block, full):
+        """block (this rank's len(full) / world floats) = the sum over ranks of full's block."""
+        if self.staged:  # gloo has no reduce-scatter: all-reduce on the host, keep this rank's block
+            h = full.cpu()
+            self.dist.all_reduce(h)
+            k = block.numel()
+            block.copy_(h[self.rank * k:(self.rank + 1) * k])
+        else:
+            self.dist.reduce_scatter_tensor(block, full)
+
 
 class LocalComm:
     """A single rank (world = 1, no collective), or rank `rank` of `world` when a test drives the
@@ -141,6 +160,10 @@ class LocalComm:
 
     def all_reduce_sum(self, t):
         assert self.world == 1, "LocalComm reduces only at world = 1"
+
+    def reduce_scatter_sum(self, block, full):
+        assert self.world == 1, "LocalComm reduces only at world = 1"
+        block.copy_(full)
 
 
 class PartitionedSolver:
@@ -165,6 +188,12 @@ class PartitionedSolver:
             S = t["block"]
             self.v = torch.ones(self.comm.world * (S + 1), dtype=f32, device=self.dev)  # gathered layout
             self.out = torch.ones(S + 1, dtype=f32, device=self.dev)                      # send block
+        elif self.mode == CLAUSES_RS:
+            S = t["block"]
+            self.v = torch.ones(self.comm.world * (S + 1), dtype=f32, device=self.dev)    # gathered layout
+            self.out = torch.ones(self.comm.world * (S + 1), dtype=f32, device=self.dev)  # partial dv, same layout
+            self.blk = torch.ones(S + 1, dtype=f32, device=self.dev)                      # reduce-scatter result
+            self.send = torch.ones(S + 1, dtype=f32, device=self.dev)                     # all-gather input
         else:
             self.v = torch.zeros(self.n, dtype=f32, device=self.dev)
             self.out = torch.ones(self.n + 1, dtype=f32, device=self.dev)                 # partial dv + unsat
@@ -185,9 +214,14 @@ class PartitionedSolver:
         return int(lib().odesat_part_device_bytes(self._h))
 
     # -- state --------------------------------------------------------------------------------
+    @property
+    def _apply(self) -> int:
+        """odesat_part_rhs's apply argument: 0 CLAUSES, 1 VARIABLES, 2 CLAUSES_RS."""
+        return {CLAUSES: 0, VARIABLES: 1, CLAUSES_RS: 2}[self.mode]
+
     def _v_index(self):
         i = np.arange(self.n)
-        return i + i // self.topo["block"] if self.mode == VARIABLES else i
+        return i + i // self.topo["block"] if self.mode != CLAUSES else i
 
     def _stream(self):
         import torch
@@ -205,6 +239,9 @@ class PartitionedSolver:
         host[self._v_index()] = np.asarray(v, np.float64).astype(np.float32)
         self.v.copy_(torch.from_numpy(host))
         self.out.fill_(1.0)
+        if self.mode == CLAUSES_RS:
+            self.blk.fill_(1.0)
+            self.send.fill_(1.0)
         check(lib().odesat_part_reset(self._h, self._stream()))
 
     def get_state(self):
@@ -220,33 +257,50 @@ class PartitionedSolver:
     # -- stepping -----------------------------------------------------------------------------
     def rhs(self, dt: float, zeta: float, stop: bool = True):
         """The rank's local part of a step: right-hand side + memory update into `out`."""
-        apply = 1 if self.mode == VARIABLES else 0
         check(lib().odesat_part_rhs(self._h, C.c_void_p(self.v.data_ptr()), C.c_void_p(self.out.data_ptr()),
-                                    float(dt), float(zeta), apply, int(stop), self._stream()))
+                                    float(dt), float(zeta), self._apply, int(stop), self._stream()))
 
     def post(self, dt: float):
-        """After the collective: CLAUSES applies the summed dv (VARIABLES' gather already is v)."""
+        """After the (first) collective: CLAUSES applies the summed dv; CLAUSES_RS updates this rank's
+        block of voltages from its reduce-scattered dv into the all-gather's send block (VARIABLES'
+        gather already is v)."""
         if self.mode == CLAUSES:
             check(lib().odesat_part_apply(self._h, C.c_void_p(self.v.data_ptr()), C.c_void_p(self.out.data_ptr()),
                                           float(dt), self._stream()))
+        elif self.mode == CLAUSES_RS:
+            check(lib().odesat_part_reduce_apply(self._h, C.c_void_p(self.v.data_ptr()),
+                                                 C.c_void_p(self.blk.data_ptr()), C.c_void_p(self.send.data_ptr()),
+                                                 self.comm.rank, float(dt), self._stream()))
+
+    def exchange_bytes(self) -> int:
+        """Bytes this rank contributes to the step's collective(s): the all-gather's block
+        (VARIABLES), the all-reduced vector (CLAUSES), or the reduce-scattered vector plus the
+        all-gather's block (CLAUSES_RS)."""
+        S = self.topo["block"]
+        return {VARIABLES: 4 * (S + 1), CLAUSES: 4 * (self.n + 1),
+                CLAUSES_RS: 4 * self.comm.world * (S + 1) + 4 * (S + 1)}[self.mode]
 
     def step(self, dt: float, zeta: float, stop: bool = True):
         """One fixed Euler step of the whole instance (system.rs:141-154), enqueued on torch's
-        current stream: local RHS + memory update, the collective, the voltage update.  With stop,
+        current stream: local RHS + memory update, the collective(s), the voltage update.  With stop,
         the first allsat step freezes the replica (later steps are no-ops), as simulate does."""
         self.rhs(dt, zeta, stop)
         if self.mode == VARIABLES:
             self.comm.all_gather(self.v, self.out)
+        elif self.mode == CLAUSES_RS:
+            self.comm.reduce_scatter_sum(self.blk, self.out)
         else:
             self.comm.all_reduce_sum(self.out)
         self.post(dt)
+        if self.mode == CLAUSES_RS:
+            self.comm.all_gather(self.v, self.send)
 
     def status(self, stop: bool = True) -> dict:
         """{steps_done, first_sat_step (-1 = none), frozen}; synchronises the stream."""
         sd, ss, fr = C.c_int64(0), C.c_int64(0), C.c_int32(0)
-        apply = 1 if self.mode == VARIABLES else 0
         check(lib().odesat_part_status(self._h, C.c_void_p(self.v.data_ptr()), C.c_void_p(self.out.data_ptr()),
-                                       apply, int(stop), self._stream(), C.byref(sd), C.byref(ss), C.byref(fr)))
+                                       self._apply, int(stop), self._stream(), C.byref(sd), C.byref(ss),
+                                       C.byref(fr)))
         return {"steps_done": sd.value, "first_sat_step": ss.value, "frozen": bool(fr.value)}
 
     def capturable(self) -> bool:
@@ -263,6 +317,9 @@ class PartitionedSolver:
         if not isinstance(self.comm, LocalComm):  # the communicator exists before the capture
             if self.mode == VARIABLES:
                 self.comm.all_gather(torch.empty_like(self.v), torch.empty_like(self.out))
+            elif self.mode == CLAUSES_RS:
+                self.comm.reduce_scatter_sum(torch.empty_like(self.blk), torch.zeros_like(self.out))
+                self.comm.all_gather(torch.empty_like(self.v), torch.empty_like(self.send))
             else:
                 self.comm.all_reduce_sum(torch.zeros_like(self.out))
         torch.cuda.synchronize(self.dev)
@@ -297,3 +354,33 @@ class PartitionedSolver:
             if stop and (k + 1) % poll == 0 and k + 1 < steps and self.status(stop)["frozen"]:
                 break
         return self.status(stop)
+
+
+def step_in_process(parts, dt: float, zeta: float, stop: bool = True):
+    """One step of `world` ranks held by ONE process (parts[r] = rank r, LocalComm(r, world), all on
+    the same device): every rank's local kernels, with the collectives done in process by torch ops
+    -- the same sums (CLAUSES: the ranks' partials added in rank order) and copies an RCCL call
+    would make.  Tests and single-GPU timing of a world's per-rank slices use it."""
+    import torch
+    mode = parts[0].mode
+    for p in parts:
+        p.rhs(dt, zeta, stop)
+    if mode == VARIABLES:
+        g = torch.cat([p.out for p in parts])
+        for p in parts:
+            p.v.copy_(g)
+    elif mode == CLAUSES:
+        tot = torch.stack([p.out for p in parts]).sum(0)
+        for p in parts:
+            p.out.copy_(tot)
+    else:
+        k = parts[0].blk.numel()
+        tot = torch.stack([p.out for p in parts]).sum(0)
+        for r, p in enumerate(parts):
+            p.blk.copy_(tot[r * k:(r + 1) * k])
+    for p in parts:
+        p.post(dt)
+    if mode == CLAUSES_RS:
+        g = torch.cat([p.send for p in parts])
+        for p in parts:
+            p.v.copy_(g)

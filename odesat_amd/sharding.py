@@ -98,7 +98,10 @@ def run_batch(dist, solver, replica0: int, **kw):
     return global_first_satisfied(dist, sat, replica0), r
 
 
-def run_inter(dist, solver, replica0: int, max_steps: int, chunk: int = 64, **kw):
+INTER_LOCKSTEP_CHUNK = 256  # steps between stop agreements; the CLI's value too (csrc/cli.cpp)
+
+
+def run_inter(dist, solver, replica0: int, max_steps: int, chunk: int = INTER_LOCKSTEP_CHUNK, **kw):
     """The inter command across ranks (system.rs:241-359) with the reference's exact stop: every
     replica on every rank takes the step T at which the first replica anywhere is allsat, and none
     goes further.  Ranks run chunks of `chunk` steps in lock step from a device checkpoint; after a

@@ -176,6 +176,10 @@ class Solver:
     def algorithm(self) -> int:
         return check(lib().odesat_get_algorithm(self._h))
 
+    def step_kernel(self, adaptive: bool = False) -> str:
+        """The kernel simulate launches for fixed or adaptive steps (odesat_step_kernel)."""
+        return lib().odesat_step_kernel(self._h, 1 if adaptive else 0).decode()
+
     @property
     def group_width(self) -> int:
         return check(lib().odesat_group_width(self._h))

@@ -23,7 +23,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--config", default="config5")
     p.add_argument("--fixture", default=None)
-    p.add_argument("--mode", default="variables", choices=["variables", "clauses"])
+    p.add_argument("--mode", default="variables", choices=["variables", "clauses", "clauses_rs"])
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--dt", type=float, default=0.01)
@@ -40,7 +40,7 @@ def main():
 
     from odesat_amd import cnf, device_count
     from odesat_amd import workloads as wl
-    from odesat_amd.partition import CLAUSES, VARIABLES, LocalComm, PartitionedSolver, TorchComm, default_zeta
+    from odesat_amd.partition import MODES, LocalComm, PartitionedSolver, TorchComm, default_zeta
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -66,7 +66,7 @@ def main():
         n = c["n"]
         workload = f"{args.config}: random 3-SAT n={n} m={c['m']} seed={c['seed']}"
     m = len(cp) - 1
-    mode = VARIABLES if args.mode == "variables" else CLAUSES
+    mode = MODES[args.mode]
     comm = TorchComm(dist) if dist is not None else LocalComm()
     t0 = time.perf_counter()
     s = PartitionedSolver(cp, var, neg, n, mode, comm=comm, device=device, order=args.order)
@@ -114,7 +114,7 @@ def main():
             json.dump({"v": v.tolist(), "steps_done": st["steps_done"]}, fh)
     if rank == 0:
         t = s.topo
-        exchange = (4 * world * (t["block"] + 1)) if mode == VARIABLES else 4 * (n + 1)
+        exchange = s.exchange_bytes()
         print(json.dumps({
             "metric": "ODE steps/s of one instance partitioned across GPUs (BASELINE configs[4])",
             "value": args.steps / wall, "unit": "steps/s", "n_gpus": world, "steps": args.steps,
@@ -123,7 +123,8 @@ def main():
             "config": {"workload": workload, "mode": args.mode, "order": args.order,
                        "terms": os.environ.get("ODESAT_PART_TERMS", "ell"),
                        "graph_steps": args.graph if graph is not None else 0,
-                       "collective": "all_gather" if mode == VARIABLES else "all_reduce",
+                       "collective": {"variables": "all_gather", "clauses": "all_reduce",
+                                      "clauses_rs": "reduce_scatter + all_gather"}[args.mode],
                        "exchange_bytes_per_step": exchange, "local_clauses_rank0": int(len(t["clauses"])),
                        "setup_s": setup_s, "backend": dist.get_backend() if dist is not None else None},
         }))

@@ -7,8 +7,9 @@ per-step traffic (P) is ~0 for k_onchip, the clause memories for k_resident.  Tw
 HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes; on gfx950 FETCH_SIZE tallies 128-B read requests
 at 64 B, MI355X_MICROARCH.md HBM section); each counter comes from its own --pmc pass, kernel trace only.
 
-usage: python scripts/make_profile_json.py <kernel substring> <batch> <dtype> <config> <out.json> k1:<dir> k2:<dir>
-       (each dir holds the p*/run_counter_collection.csv of scripts/pmc.sh)
+usage: python scripts/make_profile_json.py <kernel substring> <batch> <dtype> <config> <out.json> [mode=adaptive]
+           k1:<dir> k2:<dir>
+       (each dir holds the p*/run_counter_collection.csv of scripts/pmc.sh; mode defaults to fixed)
 """
 import collections
 import csv
@@ -28,8 +29,12 @@ def counters(root, kern):
 
 def main():
     kern, batch, dtype, config, out = sys.argv[1:6]
+    mode = "fixed"
     pts = []
     for a in sys.argv[6:]:
+        if a.startswith("mode="):
+            mode = a[5:]
+            continue
         k, d = a.split(":", 1)
         c = counters(d, kern)
         pt = {"steps": int(k), "fetch_size_kib": c["FETCH_SIZE"], "write_size_kib": c["WRITE_SIZE"]}
@@ -46,7 +51,7 @@ def main():
         per = (p2[key] - p1[key]) / dk
         return p1[key] - p1["steps"] * per, per
 
-    res = {"kernel": kern, "batch": int(batch), "dtype": dtype, "config": config, "points": pts}
+    res = {"kernel": kern, "batch": int(batch), "dtype": dtype, "config": config, "mode": mode, "points": pts}
     res["hbm_bytes_fixed"], res["hbm_bytes_per_step"] = fit("hbm_bytes")
     if all("SQ_INSTS_VALU" in p for p in (p1, p2)):
         res["valu_insts_fixed"], res["valu_insts_per_step"] = fit("SQ_INSTS_VALU")

@@ -1,4 +1,5 @@
-"""Fixed workload for rocprofv3 counter passes: config-2 instance, B replicas, K fixed steps."""
+"""Fixed workload for rocprofv3 counter passes: config-2 instance (CONFIG), B replicas, K fixed steps
+(ADAPTIVE=1: adaptive steps, tol 1e-3) in one launch, DTYPE f32 / f64, ALG forces an algorithm."""
 import os
 import sys
 
@@ -22,6 +23,7 @@ with Solver(f, B, os.environ.get("DTYPE", "f32")) as s:
     if "ALG" in os.environ:
         s.set_algorithm(int(os.environ["ALG"]))
     s.init_state(42)
-    s.simulate(dt=0.01, max_steps=K, stop=ODESAT_STOP_NONE, poll_interval=K)  # one launch of K steps
+    s.simulate(adaptive=os.environ.get("ADAPTIVE", "0") == "1", dt=0.01, tol=1e-3, max_steps=K, stop=ODESAT_STOP_NONE,
+               poll_interval=K)  # one launch of K steps
     s.synchronize()
 print("done", B, K, CHUNK, SCHED)

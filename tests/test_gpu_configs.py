@@ -204,11 +204,10 @@ CLAUSES_TOL = 1e-5  # CLAUSES at world > 1 sums per-rank partial dv (reordered f
 
 def test_config5_partitioned_full_size_vs_oracle():
     """One replica of n = 1M, m = 4.2M over 2 ranks on the box's GPU (the exchange done in-process):
-    VARIABLES bit-exact, CLAUSES bit-exact at world 1 and within CLAUSES_TOL at world 2, against
-    oc32's fixed steps (system.rs:141-154), 5 steps of dt 0.01."""
-    import torch
-
-    from odesat_amd.partition import CLAUSES, VARIABLES, LocalComm, PartitionedSolver, default_zeta
+    VARIABLES bit-exact, CLAUSES and CLAUSES_RS (reduce-scatter + all-gather) bit-exact at world 1 and
+    within CLAUSES_TOL at world 2, against oc32's fixed steps (system.rs:141-154), 5 steps of dt 0.01."""
+    from odesat_amd.partition import (CLAUSES, CLAUSES_RS, VARIABLES, LocalComm, PartitionedSolver, default_zeta,
+                                      step_in_process)
     c = wl.CONFIGS["config5"]
     n, m = c["n"], c["m"]
     var, neg = wl.random_ksat(n, m, 3, c["seed"])
@@ -222,23 +221,12 @@ def test_config5_partitioned_full_size_vs_oracle():
     v, xs, xl = v0.copy(), xs0.copy(), np.ones(m, np.float32)
     for _ in range(K):
         o.euler_step_fixed(v, xs, xl, np.float32(dt), np.float32(zeta))
-    for mode, world in ((VARIABLES, 2), (CLAUSES, 1), (CLAUSES, 2)):
+    for mode, world in ((VARIABLES, 2), (CLAUSES, 1), (CLAUSES, 2), (CLAUSES_RS, 1), (CLAUSES_RS, 2)):
         parts = [PartitionedSolver(cp, v_, n_, n, mode, comm=LocalComm(r, world)) for r in range(world)]
         for p in parts:
             p.set_state(v0, xs0, np.ones(m))
         for _ in range(K):
-            for p in parts:
-                p.rhs(dt, zeta, False)
-            if mode == VARIABLES:
-                g = torch.cat([p.out for p in parts])
-                for p in parts:
-                    p.v.copy_(g)
-            else:
-                tot = torch.stack([p.out for p in parts]).sum(0)
-                for p in parts:
-                    p.out.copy_(tot)
-            for p in parts:
-                p.post(dt)
+            step_in_process(parts, dt, zeta, False)
         for p in parts:
             st = p.status(False)
             assert st["steps_done"] == K

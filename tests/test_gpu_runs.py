@@ -162,6 +162,39 @@ def test_inter_multistep_launches_equal_lockstep(monkeypatch, alg, wave, narrow,
         assert same(s1[0], v) and same(s1[1], xs) and same(s1[2], xl)
 
 
+def test_set_state_ends_a_stopped_inter_run(monkeypatch):
+    """a STOP_ANY run that stopped, then odesat_set_state with states outside ONCHIP's
+    range.  set_state ends the run (and its stop word), so a continue runs its steps (it returned 0
+    before) and does not mark the state in range; a fresh simulate then takes its first step on the
+    clamping kernel.  Both equal the oracle's simulate_inter from the same states."""
+    f = product_formula("easy")
+    B = 40
+    o = orc.Oracle(*(lambda g: (g.clause_ptr, g.var, g.neg, g.varnum))(oracle_formula("easy")), "f32")
+    rng = np.random.default_rng(5)
+    v = rng.uniform(-1.5, 1.5, (B, o.n)).astype(np.float32)
+    xs = rng.uniform(-0.5, 1.5, (B, o.m)).astype(np.float32)
+    xl = rng.uniform(0.5, 3.0, (B, o.m)).astype(np.float32)
+    kw = dict(dt=0.1, max_steps=30, stop=ODESAT_STOP_ANY, poll_interval=30)
+    monkeypatch.setenv("ODESAT_WAVE", "0")  # one replica per group, as ONCHIP needs (REPLAY above)
+    monkeypatch.setenv("ODESAT_RES_NARROW", "0")
+    with Solver(f, B, "f32") as s:
+        s.set_algorithm(_lib.ODESAT_ALG_ONCHIP)
+        s.init_state(4)
+        r = s.simulate(dt=0.1, max_steps=6000, stop=ODESAT_STOP_ANY, poll_interval=500)
+        assert (r["first_sat_step"] >= 0).any()
+        s.set_state(v, xs, xl)
+        rc = s.simulate(resume=True, **kw)
+        sc = s.get_state()
+        s.set_state(v, xs, xl)
+        rf = s.simulate(**kw)
+        sf = s.get_state()
+    ov, oxs, oxl = v.copy(), xs.copy(), xl.copy()
+    t, _, _, _ = o.simulate_inter(ov, oxs, oxl, dt=np.float32(0.1), steps=30)
+    assert t > 0 and rc["steps_run"] == t and rf["steps_run"] == t
+    for got in (sc, sf):
+        assert same(got[0], ov) and same(got[1], oxs) and same(got[2], oxl)
+
+
 def test_onchip_inter_at_config2_size_stop_none_equivalent():
     """Config 2's instance, B = 64, STOP_ANY in one 40-step launch with no replica satisfied: the same
     states as STOP_NONE (the out-of-place launch and its parity flip change nothing)."""

@@ -4,7 +4,8 @@ SURVEY.md §8e).
 CPU: the local topologies (every rank's fold covers exactly the reference's accumulation of its
 variables), and the distributed step at world_size 2 over gloo with the numpy restatement
 (oracle/np_oracle.py) standing in for the per-rank kernels: the VARIABLES partition reproduces the
-single-process oracle bit for bit, the CLAUSES partition within a stated tolerance.
+single-process oracle bit for bit, the CLAUSES partition (all-reduce, or CLAUSES_RS: reduce-scatter +
+all-gather) within a stated tolerance.
 GPU: the HIP kernels, at world 1 and as 2-3 ranks on one device with the exchange done in-process,
 against the oracle's f32 restatement: bit-exact (VARIABLES, and CLAUSES at world 1), tolerance
 (CLAUSES at world 2); the stop bookkeeping against simulate (system.rs:190-203); and one real
@@ -18,7 +19,7 @@ import sys
 import numpy as np
 import pytest
 
-from odesat_amd.partition import CLAUSES, VARIABLES, block_size, default_zeta, local_topology
+from odesat_amd.partition import CLAUSES, CLAUSES_RS, VARIABLES, block_size, default_zeta, local_topology
 from tests.common import oracle_formula
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -77,14 +78,15 @@ def test_variables_topology_folds_exactly_the_reference_order(name, world, order
     assert seen == list(range(n))
 
 
+@pytest.mark.parametrize("mode", [CLAUSES, CLAUSES_RS])
 @pytest.mark.parametrize("world", [1, 2, 5])
-def test_clauses_topology_partitions_the_clauses(world):
+def test_clauses_topology_partitions_the_clauses(world, mode):
     cp, var, neg, n = _arrays("rand200")
     m = len(cp) - 1
     allc = []
     for r in range(world):
-        t = local_topology(cp, var, neg, n, CLAUSES, r, world)
-        assert (t["v0"], t["v1"], t["block"]) == (0, n, 0)
+        t = local_topology(cp, var, neg, n, mode, r, world)
+        assert (t["v0"], t["v1"], t["block"]) == (0, n, block_size(n, world) if mode == CLAUSES_RS else 0)
         assert t["var_ptr"][-1] == t["clause_ptr"][-1]  # every local literal is one incidence
         assert sorted(t["clauses"].tolist()) == list(range(r * m // world, (r + 1) * m // world))
         allc.extend(sorted(t["clauses"].tolist()))
@@ -143,6 +145,23 @@ def _gloo_worker(rank, world, port, out, mode, steps, dt):
             g = g.numpy().reshape(world, S + 1)
             v = g[:, :S].reshape(-1)[:n].copy()
             unsat_hist.append(float(g[:, S].sum()))
+        elif mode == CLAUSES_RS:  # reduce-scatter (gloo: all-reduce, keep own block), update, all-gather
+            full = np.zeros(world * (S + 1), T)
+            i = np.arange(n)
+            full[i + i // S] = dv
+            full[S::S + 1] = uns
+            buf = torch.from_numpy(full)
+            td.all_reduce(buf)
+            blk = buf.numpy()[rank * (S + 1):(rank + 1) * (S + 1)]
+            own = slice(rank * S, min(n, (rank + 1) * S))
+            send = np.zeros(S + 1, T)
+            send[:own.stop - own.start] = np.fmin(np.fmax(v[own] + T(dt) * blk[:own.stop - own.start], T(-1.0)), T(1.0))
+            send[S] = blk[S]
+            g = torch.zeros(world * (S + 1), dtype=torch.float32)
+            td.all_gather_into_tensor(g, torch.from_numpy(send))
+            g = g.numpy().reshape(world, S + 1)
+            v = g[:, :S].reshape(-1)[:n].copy()
+            unsat_hist.append(float(g[0, S]))
         else:
             buf = torch.from_numpy(np.concatenate([dv, [T(uns)]]).astype(T))
             td.all_reduce(buf)
@@ -156,7 +175,7 @@ def _gloo_worker(rank, world, port, out, mode, steps, dt):
     td.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", [VARIABLES, CLAUSES])
+@pytest.mark.parametrize("mode", [VARIABLES, CLAUSES, CLAUSES_RS])
 def test_two_rank_gloo_step_matches_single_process_oracle(tmp_path, mode):
     import torch.multiprocessing as mp
 
@@ -200,21 +219,8 @@ def _oracle_run(name, steps, dt, seed=7, stop=False):
     return init, (v, xs, xl), steps, sats
 
 
-def _exchange(parts, mode):
-    """The collective of `parts` (ranks of one process on one device), in place."""
-    import torch
-    if mode == VARIABLES:
-        g = torch.cat([p.out for p in parts])
-        for p in parts:
-            p.v.copy_(g)
-    else:
-        s = torch.stack([p.out for p in parts]).sum(0)
-        for p in parts:
-            p.out.copy_(s)
-
-
 def _run_parts(name, mode, world, steps, dt, stop=False, poll=7):
-    from odesat_amd.partition import LocalComm, PartitionedSolver
+    from odesat_amd.partition import LocalComm, PartitionedSolver, step_in_process
     cp, var, neg, n = _arrays(name)
     m = len(cp) - 1
     init, _, _, _ = _oracle_run(name, 0, dt)
@@ -223,11 +229,7 @@ def _run_parts(name, mode, world, steps, dt, stop=False, poll=7):
         p.set_state(*init)
     zeta = default_zeta(n, m)
     for k in range(steps):
-        for p in parts:
-            p.rhs(dt, zeta, stop)
-        _exchange(parts, mode)
-        for p in parts:
-            p.post(dt)
+        step_in_process(parts, dt, zeta, stop)
         if stop and (k + 1) % poll == 0 and parts[0].status(stop)["frozen"]:
             break
     sts = [p.status(stop) for p in parts]
@@ -239,7 +241,8 @@ def _run_parts(name, mode, world, steps, dt, stop=False, poll=7):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["rand200", "easy", "small"])
-@pytest.mark.parametrize("mode,world", [(VARIABLES, 1), (VARIABLES, 2), (VARIABLES, 3), (CLAUSES, 1), (CLAUSES, 2)])
+@pytest.mark.parametrize("mode,world", [(VARIABLES, 1), (VARIABLES, 2), (VARIABLES, 3), (CLAUSES, 1), (CLAUSES, 2),
+                                        (CLAUSES_RS, 1), (CLAUSES_RS, 2), (CLAUSES_RS, 3)])
 def test_partition_kernels_match_oracle(name, mode, world):
     steps, dt = 30, 0.05
     _, (v, xs, xl), _, sats = _oracle_run(name, steps, dt)
@@ -260,7 +263,7 @@ def test_partition_kernels_match_oracle(name, mode, world):
     {"ODESAT_PART_TERMS": "slot"}, {"ODESAT_PART_TERMS": "ell"}, {"ODESAT_PART_TERMS": "region"},
     {"ODESAT_PART_PACK": "0"}, {"ODESAT_PART_K3": "0"}, {"ODESAT_PART_XCD": "1"},
     {"ODESAT_PART_REGIONS": "24", "ODESAT_PART_PACK": "0"}])
-@pytest.mark.parametrize("mode,world", [(VARIABLES, 2), (CLAUSES, 1)])
+@pytest.mark.parametrize("mode,world", [(VARIABLES, 2), (CLAUSES, 1), (CLAUSES_RS, 1)])
 def test_partition_layouts_match_oracle(monkeypatch, env, mode, world):
     """Every term layout / clause record / clause kernel / placement choice (read when a slice is
     created) folds the same terms in the same order: the same bits as the oracle."""
@@ -276,7 +279,7 @@ def test_partition_layouts_match_oracle(monkeypatch, env, mode, world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,world", [(VARIABLES, 2), (CLAUSES, 1)])
+@pytest.mark.parametrize("mode,world", [(VARIABLES, 2), (CLAUSES, 1), (CLAUSES_RS, 1)])
 def test_partition_stop_matches_simulate(mode, world):
     """easy.cnf is SAT: the replica freezes at simulate's stop step, polled every 7 steps."""
     steps, dt = 4000, 0.1
