@@ -67,6 +67,8 @@ struct odesat_solver {
     int4 *wv_rec4 = nullptr;  // [m] k_wave: literal | variable-major term position << 16, per literal
     int32_t *wv_vst = nullptr;  // [n+1] k_wave: first term position of each variable
     int wv_wpw = 1;             // k_wave: replicas per workgroup sharing the LDS topology
+    bool solo = false;          // k_solo (wave.hpp) instead of k_wave: one replica per workgroup, lanes' slots in registers
+    int solo_nl = 64, solo_cpl = 1, solo_vpl = 1;  // k_solo: lanes per replica, clause / variable slots per lane
     int wv_tw = 1;              // k_wave: waves per replica, fixed steps
     int wv_tw_ada = 1;          // ... adaptive steps (four barriers per step instead of two: at most 4)
     bool res_ada = false; // adaptive steps fit in LDS too (else they run FUSED on the same layout)
@@ -750,6 +752,17 @@ template <typename T, bool ADA, int WPW, int TW> int launch_wave_k(odesat_solver
     return ODESAT_OK;
 }
 
+template <typename T, bool ADA, int CPL, int VPL> int launch_solo_k(odesat_solver *s, WArgs<T> a) {
+    const size_t lds = (size_t)(s->n + s->L) * sizeof(T);
+    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_solo<T, ADA, CPL, VPL>), (int)RES_LDS_MAX));
+    {
+        Timed tm(s, 0);
+        hipLaunchKernelGGL((k_solo<T, ADA, CPL, VPL>), dim3((unsigned)s->G), dim3((unsigned)s->solo_nl), lds, s->stream, a);
+    }
+    HIP_TRY(hipGetLastError());
+    return ODESAT_OK;
+}
+
 template <typename T>
 int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
                 int stop_mode, bool oop) {
@@ -778,6 +791,21 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     a.xl_max = (T)1e4 * (T)s->m;  // system.rs:95
     a.tol = tol;
     a.G = s->G;
+    if (s->solo) {
+        auto so = [&](auto cc, auto vv) -> int {
+            constexpr int CPL = decltype(cc)::value, VPL = decltype(vv)::value;
+            return adaptive ? launch_solo_k<T, true, CPL, VPL>(s, a) : launch_solo_k<T, false, CPL, VPL>(s, a);
+        };
+        switch (s->solo_cpl * 10 + s->solo_vpl) {
+            case 11: return so(IC<1>{}, IC<1>{});
+            case 12: return so(IC<1>{}, IC<2>{});
+            case 21: return so(IC<2>{}, IC<1>{});
+            case 22: return so(IC<2>{}, IC<2>{});
+            case 41: return so(IC<4>{}, IC<1>{});
+            case 42: return so(IC<4>{}, IC<2>{});
+            default: return fail(ODESAT_EINVAL, "k_solo shape not available");
+        }
+    }
     auto go = [&](auto ww, auto tw) -> int {
         constexpr int WPW = decltype(ww)::value, TW = decltype(tw)::value;
         return adaptive ? launch_wave_k<T, true, WPW, TW>(s, a) : launch_wave_k<T, false, WPW, TW>(s, a);
@@ -1343,6 +1371,23 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
                 hipMemcpy(s->wv_vst, vst.data(), (n + 1) * 4, hipMemcpyHostToDevice) != hipSuccess)
                 return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
             s->res_ada = true;  // wave_lds_bytes(adaptive) fits by selection
+            // k_solo (wave.hpp): the latency path when k_wave would run one replica per workgroup
+            // anyway (small batches, B = 1 for solve): every lane's clause and variable slots in
+            // registers.  Lanes: the fewest multiple of 64 (at most 1024) giving each lane at most two
+            // clauses and two variables.  ODESAT_SOLO=0/1 and ODESAT_SOLO_LANES override.
+            int64_t nl = 64;
+            while (nl < SOLO_MAX_NL && (m > 2 * nl || n > 2 * nl)) nl += 64;
+            if (const char *ev = std::getenv("ODESAT_SOLO_LANES")) {
+                const int64_t want = std::atoll(ev);
+                if (want >= 64 && want <= SOLO_MAX_NL && want % 64 == 0) nl = want;
+            }
+            const int64_t cpl = (m + nl - 1) / nl, vpl = (n + nl - 1) / nl;
+            const bool fits = cpl <= 4 && vpl <= 2 && (size_t)(n + L) * s->tsize <= RES_LDS_MAX;
+            s->solo = fits && s->wv_wpw == 1;
+            if (const char *ev = std::getenv("ODESAT_SOLO")) s->solo = fits && std::atoi(ev) != 0;
+            s->solo_nl = (int)nl;
+            s->solo_cpl = cpl <= 1 ? 1 : (cpl <= 2 ? 2 : 4);
+            s->solo_vpl = (int)vpl;
         }
         if ((rc = onchip_setup(s, tiles, wst, lits))) return bail(rc);
         if (s->oc_tr > 0) s->alg = ODESAT_ALG_ONCHIP;
@@ -1428,7 +1473,7 @@ extern "C" const char *odesat_step_kernel(const odesat_solver *s, int adaptive) 
     if (!s) return nullptr;
     if ((s->alg == ODESAT_ALG_RESIDENT || s->alg == ODESAT_ALG_ONCHIP) && (!adaptive || s->res_ada)) {
         if (s->alg == ODESAT_ALG_ONCHIP && !adaptive) return "k_onchip";
-        return s->res_wave ? "k_wave" : "k_resident";
+        return s->res_wave ? (s->solo ? "k_solo" : "k_wave") : "k_resident";
     }
     return s->alg == ODESAT_ALG_TWOPASS ? "k_clause_u" : "k_step";
 }

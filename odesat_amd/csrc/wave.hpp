@@ -22,6 +22,8 @@
 
 #include "kernels.hpp"
 
+#include <type_traits>
+
 namespace odk {
 
 constexpr int WAVE_NTH = 64;
@@ -62,6 +64,64 @@ template <typename T> struct WClause {
     T v[3], xs, xl, C1;
 };
 
+// One clause's arithmetic (system.rs:43-95) for a pass: the three dv terms into d[] (stored at the
+// clause's term positions by the caller), C, and by pass the memory update in place (W_FIXED), the
+// clause's C kept for the second pass (W_ADA1: the memories stay y) or -- from the first pass's C1 --
+// the full-step clone and the first half step of y's memories, then the second half step with its
+// max_error terms into e (W_ADA2).  Shared by k_wave and k_solo, so both are the same expressions.
+template <typename T, int PK>
+__device__ __forceinline__ bool clause_math(const int (&lit)[3], const T (&v)[3], T &xs, T &xl, T &C1, T h, T zeta,
+                                            T xl_max, T (&d)[3], T &e) {
+    const T one = (T)1.0, halfc = (T)0.5, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
+    T q[3], val[3];
+    T mn = inf_v<T>(), sec = inf_v<T>();
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {  // :43-57
+        q[j] = (lit[j] & 1) ? (T)-1.0 : (T)1.0;
+        val[j] = one - q[j] * v[j];
+        minsec(val[j], mn, sec);
+    }
+    const T C = halfc * mn;  // :60
+    T xs_m = xs, xl_m = xl;
+    T xs_f = xs_m, xl_f = xl_m;
+    if (PK == W_ADA2) {  // y's memories -> the full-step clone and the first half step (:124-128)
+        const T half = (T)0.5 * h;
+        const T dxs1 = (T)20.0 * (xs_m + eps) * (C1 - (T)0.25);  // :84
+        const T dxl1 = (T)5.0 * (C1 - (T)0.05);                  // :85
+        xs_f = dmin(dmax(xs_m + h * dxs1, eps), xs_hi);
+        xl_f = dmin(dmax(xl_m + h * dxl1, one), xl_max);
+        const T xs_h = dmin(dmax(xs_m + half * dxs1, eps), xs_hi);
+        const T xl_h = dmin(dmax(xl_m + half * dxl1, one), xl_max);
+        xs_m = xs_h;
+        xl_m = xl_h;
+    }
+    const T tt = xl_m * xs_m;
+    const T tr = (one + zeta * xl_m) * (one - xs_m);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) d[j] = tt * (halfc * q[j] * (val[j] != mn ? mn : sec));  // :64-70
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {  // :73-80 (zero unless C == val_j; adding it keeps the sum exact)
+        const T r_ = (C == one - q[j] * v[j]) ? halfc * (q[j] - v[j]) : (T)0.0;
+        d[j] = d[j] + tr * r_;
+    }
+    const T dxs = (T)20.0 * (xs_m + eps) * (C - (T)0.25);  // :84
+    const T dxl = (T)5.0 * (C - (T)0.05);                  // :85
+    if (PK == W_FIXED) {
+        xs = dmin(dmax(xs_m + h * dxs, eps), xs_hi);  // :94-95
+        xl = dmin(dmax(xl_m + h * dxl, one), xl_max);
+    } else if (PK == W_ADA1) {
+        C1 = C;  // the memories stay y until the second pass (an allsat replica takes no step)
+    } else {
+        const T half = (T)0.5 * h;  // second half step (:130), max_error terms (:132)
+        const T xs_n = dmin(dmax(xs_m + half * dxs, eps), xs_hi);
+        const T xl_n = dmin(dmax(xl_m + half * dxl, one), xl_max);
+        e = dmax(e, dmax(dabs(xs_f - xs_n), dabs(xl_f - xl_n)));
+        xs = xs_n;
+        xl = xl_n;
+    }
+    return PK != W_ADA2 && !(C < (T)0.25);  // :88 (unsat)
+}
+
 // Phase 1 over the replica's clauses, one lane's share.  Returns whether one of this lane's clauses
 // is unsat (:88, W_FIXED / W_ADA1) and raises e to the memories' max_error terms (W_ADA2).
 // Lane l of the replica's NL lanes takes clauses l, l + NL, ...  Software-pipelined: the records of
@@ -72,7 +132,6 @@ template <typename T> struct WClause {
 template <typename T, int PK, int NL>
 __device__ __forceinline__ bool lane_clauses(const WArgs<T> &a, const int4 *rec4, const T *vL, T *tL, T *cmL, T *cL,
                                              int l, T h, T &e) {
-    const T one = (T)1.0, halfc = (T)0.5, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
     bool uns = false;
     if (l >= a.m) return false;  // (NL > m: the lanes without a clause)
     const int last = a.m - 1;
@@ -91,60 +150,20 @@ __device__ __forceinline__ bool lane_clauses(const WArgs<T> &a, const int4 *rec4
     WClause<T> W;
     gather(l, rec4[l], W);
     for (int c = l; c < a.m; c += NL) {
-        const WClause<T> X = W;  // this clause
+        WClause<T> X = W;  // this clause
         const int cn = min(c + NL, last);
         gather(cn, rn, W);       // the next clause's voltages and memories
         rn = rec4[min(c + 2 * NL, last)];
-        T q[3], val[3], d[3];
-        T mn = inf_v<T>(), sec = inf_v<T>();
+        T d[3];
+        uns = clause_math<T, PK>(X.lit, X.v, X.xs, X.xl, X.C1, h, a.zeta, a.xl_max, d, e) || uns;
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {  // :43-57
-            q[j] = (X.lit[j] & 1) ? (T)-1.0 : (T)1.0;
-            val[j] = one - q[j] * X.v[j];
-            minsec(val[j], mn, sec);
-        }
-        const T C = halfc * mn;  // :60
-        T xs_m = X.xs, xl_m = X.xl;
-        T xs_f = xs_m, xl_f = xl_m;
-        if (PK == W_ADA2) {  // y's memories -> the full-step clone and the first half step (:124-128)
-            const T C1 = X.C1, half = (T)0.5 * h;
-            const T dxs1 = (T)20.0 * (xs_m + eps) * (C1 - (T)0.25);  // :84
-            const T dxl1 = (T)5.0 * (C1 - (T)0.05);                  // :85
-            xs_f = dmin(dmax(xs_m + h * dxs1, eps), xs_hi);
-            xl_f = dmin(dmax(xl_m + h * dxl1, one), a.xl_max);
-            const T xs_h = dmin(dmax(xs_m + half * dxs1, eps), xs_hi);
-            const T xl_h = dmin(dmax(xl_m + half * dxl1, one), a.xl_max);
-            xs_m = xs_h;
-            xl_m = xl_h;
-        }
-        const T tt = xl_m * xs_m;
-        const T tr = (one + a.zeta * xl_m) * (one - xs_m);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) d[j] = tt * (halfc * q[j] * (val[j] != mn ? mn : sec));  // :64-70
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {  // :73-80 (zero unless C == val_j; adding it keeps the sum exact)
-            const T r_ = (C == one - q[j] * X.v[j]) ? halfc * (q[j] - X.v[j]) : (T)0.0;
-            d[j] = d[j] + tr * r_;
-            tL[X.pos[j]] = d[j];
-        }
-        if (PK != W_ADA2) uns = uns || !(C < (T)0.25);  // :88
-        const T dxs = (T)20.0 * (xs_m + eps) * (C - (T)0.25);  // :84
-        const T dxl = (T)5.0 * (C - (T)0.05);                  // :85
-        if (PK == W_FIXED) {
-            T2 m2;
-            m2.x = dmin(dmax(xs_m + h * dxs, eps), xs_hi);  // :94-95
-            m2.y = dmin(dmax(xl_m + h * dxl, one), a.xl_max);
-            reinterpret_cast<T2 *>(cmL)[c] = m2;
-        } else if (PK == W_ADA1) {
-            cL[c] = C;  // the memories stay y until the second pass (an allsat replica takes no step)
+        for (int j = 0; j < 3; ++j) tL[X.pos[j]] = d[j];
+        if (PK == W_ADA1) {
+            cL[c] = X.C1;
         } else {
-            const T half = (T)0.5 * h;  // second half step (:130), max_error terms (:132)
-            const T xs_n = dmin(dmax(xs_m + half * dxs, eps), xs_hi);
-            const T xl_n = dmin(dmax(xl_m + half * dxl, one), a.xl_max);
-            e = dmax(e, dmax(dabs(xs_f - xs_n), dabs(xl_f - xl_n)));
             T2 m2;
-            m2.x = xs_n;
-            m2.y = xl_n;
+            m2.x = X.xs;
+            m2.y = X.xl;
             reinterpret_cast<T2 *>(cmL)[c] = m2;
         }
     }
@@ -306,6 +325,181 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
     T *CMo = (q ? a.c1 : a.c0) + (size_t)g * a.m * 2;
     for (int i = l; i < a.n; i += NL) Vo[i] = vL[i];
     for (int i = l; i < 2 * a.m; i += NL) CMo[i] = cmL[i];
+    if (l == 0) {
+        if (a.oop) a.par[g] = (uint8_t)q;
+        a.act[g] = (uint8_t)act;
+        a.sat_step[g] = sat;
+        a.steps_done[g] = done;
+        if (ADAPTIVE) a.dtr[g] = dtr;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_solo -- the latency path for one replica (solve, the criterion benches: B = 1) and small
+// batches of tiny formulas.  k_wave's two phases, with everything a lane owns kept in registers
+// for the launch: one replica per workgroup, a team of NL = blockDim lanes; lane l owns clauses l,
+// l + NL, ... (CPL slots: their literal and term-position records and their memories, plus the
+// adaptive pass's C) and variables l, l + NL, ... (VPL slots: the voltage, its term range and the
+// adaptive full-step clone).  Per step LDS carries only what crosses lanes -- v for the clause
+// gathers, the terms for the fold -- so a step is: the voltage gathers (one round trip), the clause
+// arithmetic (clause_math, k_wave's expressions), the term stores, one barrier, the term reads
+// (one round trip per 8 terms), the fold and the voltage stores, one barrier.  Bit-identical to
+// k_wave and the oracle.
+// ------------------------------------------------------------------------------------------------
+constexpr int SOLO_MAX_NL = 1024;
+
+template <typename T> __device__ __forceinline__ T solo_fold(const T *tL, int s, int d, int L) {
+    T dv = (T)0.0;  // :33, then the reference's left fold of the variable's terms (:80)
+    for (int k0 = 0; k0 < d; k0 += 8) {
+        T t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = tL[min(s + min(k0 + u, d - 1), L - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (k0 + u < d) dv += t[u];
+    }
+    return dv;
+}
+
+template <typename T, bool ADAPTIVE, int CPL, int VPL>
+__global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char wave_smem[];
+    using U = typename Bits<T>::U;
+    __shared__ U errW[SOLO_MAX_NL / 64];
+    const int NL = (int)blockDim.x, l = (int)threadIdx.x, TW = NL / 64;
+    const int g = blockIdx.x;  // this workgroup's replica (group width 1)
+    if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
+    if (g >= a.G || a.act[g] == 0) return;                              // uniform per workgroup
+    T *vL = reinterpret_cast<T *>(wave_smem);
+    T *tL = vL + a.n;
+    const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
+    const T *V = (p ? a.v1 : a.v0) + (size_t)g * a.n;
+    const T *CM = (p ? a.c1 : a.c0) + (size_t)g * a.m * 2;
+    const int mlast = a.m - 1, nlast = a.n - 1;
+    int lit[CPL][3], pos[CPL][3];
+    T xs[CPL], xl[CPL], C1[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {  // records and memories of this lane's clauses (clamped: loadable)
+        const int c = min(l + k * NL, mlast);
+        const int4 r4 = a.rec4[c];
+        lit[k][0] = r4.x & 0xffff, lit[k][1] = r4.y & 0xffff, lit[k][2] = r4.z & 0xffff;
+        pos[k][0] = (int)((uint32_t)r4.x >> 16), pos[k][1] = (int)((uint32_t)r4.y >> 16);
+        pos[k][2] = (int)((uint32_t)r4.z >> 16);
+        xs[k] = CM[2 * c];
+        xl[k] = CM[2 * c + 1];
+        C1[k] = (T)0.0;
+    }
+    int vs[VPL], vd[VPL];
+    T vr[VPL], vf[VPL];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {  // this lane's variables: voltage, term range
+        const int i = l + j * NL, ii = min(i, nlast);
+        vs[j] = a.vst[ii];
+        vd[j] = i < a.n ? a.vst[ii + 1] - vs[j] : 0;
+        vr[j] = V[ii];
+        vf[j] = vr[j];
+        if (i < a.n) vL[i] = vr[j];
+    }
+    __syncthreads();
+    int act = 1;
+    int64_t sat = a.sat_step[g], done = a.steps_done[g];
+    T dtr = ADAPTIVE ? a.dtr[g] : a.dt;
+    // phase 1 over this lane's clauses: the voltage gathers of every slot first, then the arithmetic
+    auto clauses = [&](auto pk, T h, T &e) -> bool {
+        constexpr int PK = decltype(pk)::value;
+        T vv[CPL][3];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) vv[k][j] = vL[lit[k][j] >> 1];
+        bool uns = false;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            if (l + k * NL < a.m) {
+                T d[3];
+                uns = clause_math<T, PK>(lit[k], vv[k], xs[k], xl[k], C1[k], h, a.zeta, a.xl_max, d, e) || uns;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) tL[pos[k][j]] = d[j];
+            }
+        }
+        return uns;
+    };
+    for (int k = 0; k < a.nsteps; ++k) {
+        const int step = a.step0 + k;
+        const T h = dtr;
+        T e = (T)0.0;
+        bool uns, go = false;
+        if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
+            uns = __syncthreads_or(clauses(std::integral_constant<int, W_FIXED>{}, h, e));  // also orders the terms before the fold
+#pragma unroll
+            for (int j = 0; j < VPL; ++j)
+                if (l + j * NL < a.n) {
+                    vr[j] = dmin(dmax(vr[j] + h * solo_fold(tL, vs[j], vd[j], a.L), (T)-1.0), (T)1.0);  // :96
+                    vL[l + j * NL] = vr[j];
+                }
+        } else {  // euler_step (:111-139)
+            uns = __syncthreads_or(clauses(std::integral_constant<int, W_ADA1>{}, h, e));
+            go = uns;  // an allsat replica takes no step (:122)
+            const T half = (T)0.5 * h;
+            if (go) {
+#pragma unroll
+                for (int j = 0; j < VPL; ++j)
+                    if (l + j * NL < a.n) {
+                        const T d = solo_fold(tL, vs[j], vd[j], a.L), v = vr[j];
+                        vf[j] = dmin(dmax(v + h * d, (T)-1.0), (T)1.0);     // full-step clone
+                        vr[j] = dmin(dmax(v + half * d, (T)-1.0), (T)1.0);  // first half step
+                        vL[l + j * NL] = vr[j];
+                    }
+            }
+            __syncthreads();  // the half step's voltages before the second pass; the terms read
+            if (go) clauses(std::integral_constant<int, W_ADA2>{}, h, e);
+            __syncthreads();  // the second pass's terms before its fold
+            if (go) {
+#pragma unroll
+                for (int j = 0; j < VPL; ++j)
+                    if (l + j * NL < a.n) {
+                        const T vn = dmin(dmax(vr[j] + half * solo_fold(tL, vs[j], vd[j], a.L), (T)-1.0), (T)1.0);
+                        e = dmax(e, dabs(vf[j] - vn));  // :101-108
+                        vr[j] = vn;
+                        vL[l + j * NL] = vn;
+                    }
+                U eb = tobits(e);  // non-negative floats order as their bits
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const U o = __shfl_xor(eb, off, 64);
+                    eb = o > eb ? o : eb;
+                }
+                if ((l & 63) == 0) errW[l >> 6] = eb;
+            }
+        }
+        done += 1;
+        if (!uns) {  // allsat: the fixed step was still taken (:148-152); adaptive took none
+            if (sat < 0) sat = step;
+            if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                            // simulate() breaks (:193)
+            if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
+        }
+        __syncthreads();  // the voltages before the next step's gathers (and the error words)
+        if (ADAPTIVE && go) {  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
+            U eb = errW[0];
+            for (int w = 1; w < TW; ++w) eb = errW[w] > eb ? errW[w] : eb;
+            dtr = dmax(dmin(dtr * dsqrt((T)a.tol / frombits(eb)), (T)1e3), (T)0.0078125);
+        }
+        if (!act) break;  // uniform
+    }
+    const bool q = a.oop ? !p : p;
+    T *Vo = (q ? a.v1 : a.v0) + (size_t)g * a.n;
+    T *CMo = (q ? a.c1 : a.c0) + (size_t)g * a.m * 2;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j)
+        if (l + j * NL < a.n) Vo[l + j * NL] = vr[j];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = l + k * NL;
+        if (c < a.m) {
+            CMo[2 * c] = xs[k];
+            CMo[2 * c + 1] = xl[k];
+        }
+    }
     if (l == 0) {
         if (a.oop) a.par[g] = (uint8_t)q;
         a.act[g] = (uint8_t)act;

@@ -77,7 +77,13 @@ def variants(prec, uniform3, distinct):
          ("resident-r4", {"ODESAT_GROUP_WIDTH": "4"}, _lib.ODESAT_ALG_RESIDENT)]
     if uniform3:
         for team in ("1", "2", "4"):
-            v.append((f"wave-t{team}", {"ODESAT_WAVE": "1", "ODESAT_WAVE_TEAM": team}, _lib.ODESAT_ALG_RESIDENT))
+            v.append((f"wave-t{team}", {"ODESAT_WAVE": "1", "ODESAT_SOLO": "0", "ODESAT_WAVE_TEAM": team},
+                      _lib.ODESAT_ALG_RESIDENT))
+        for lanes in ("64", "128", "0"):  # k_solo: one wave, two waves, the default team
+            env = {"ODESAT_WAVE": "1", "ODESAT_SOLO": "1"}
+            if lanes != "0":
+                env["ODESAT_SOLO_LANES"] = lanes
+            v.append((f"solo-l{lanes}", env, _lib.ODESAT_ALG_RESIDENT))
         if prec == "f32" and distinct:
             v.append(("onchip", {"ODESAT_WAVE": "0", "ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "0"},
                       _lib.ODESAT_ALG_ONCHIP))
@@ -97,6 +103,8 @@ def run_variant(f, B, prec, env, alg, adaptive, K, poll):
                     s.set_algorithm(alg)
                 except _lib.OdesatError:
                     return None  # not available for this formula / layout
+            if "ODESAT_SOLO" in env and (s.step_kernel(adaptive) == "k_solo") != (env["ODESAT_SOLO"] == "1"):
+                return None  # the forced path is not available for this formula (k_solo: slots per lane)
             s.init_state(9)
             # fixed: dt 0.05; adaptive: the reference's initial dt 0.01 (system.rs:182)
             r = s.simulate(adaptive=adaptive, dt=0.01 if adaptive else 0.05, tol=1e-3, zeta=0.01, max_steps=K,
@@ -152,15 +160,17 @@ def test_fuzz_every_path_matches_oracle(seed, prec):
 
 def test_fuzz_covered_every_path():
     """The cases above reached every kernel family: FUSED (W = 64 and 8), TWOPASS, the RESIDENT
-    tile kernels (512-lane, one-wave and R = 4 tiles), k_wave with teams of 1, 2 and 4 waves, and
-    ONCHIP."""
+    tile kernels (512-lane, one-wave and R = 4 tiles), k_wave with teams of 1, 2 and 4 waves, k_solo
+    with teams of 64, 128 and the default lanes, and ONCHIP."""
     if not COVERED:
         pytest.skip("run together with test_fuzz_every_path_matches_oracle")
     need = [("fused", _lib.ODESAT_ALG_FUSED), ("twopass", _lib.ODESAT_ALG_TWOPASS),
             ("fused-w8", _lib.ODESAT_ALG_FUSED), ("resident-r1", _lib.ODESAT_ALG_RESIDENT),
             ("resident-narrow", _lib.ODESAT_ALG_RESIDENT), ("resident-r4", _lib.ODESAT_ALG_RESIDENT),
             ("wave-t1", _lib.ODESAT_ALG_RESIDENT), ("wave-t2", _lib.ODESAT_ALG_RESIDENT),
-            ("wave-t4", _lib.ODESAT_ALG_RESIDENT), ("onchip", _lib.ODESAT_ALG_ONCHIP)]
+            ("wave-t4", _lib.ODESAT_ALG_RESIDENT), ("onchip", _lib.ODESAT_ALG_ONCHIP),
+            ("solo-l64", _lib.ODESAT_ALG_RESIDENT), ("solo-l128", _lib.ODESAT_ALG_RESIDENT),
+            ("solo-l0", _lib.ODESAT_ALG_RESIDENT)]
     print(sorted(COVERED.items()))
     missing = [k for k in need if COVERED.get(k, 0) < 4]
     assert not missing, (missing, COVERED)

@@ -557,13 +557,15 @@ def test_onchip_long_launches_sat_and_freeze(monkeypatch):
             assert same(x, y)
 
 
-@pytest.mark.parametrize("team", [None, "1", "2"])
+@pytest.mark.parametrize("team", [None, "1", "2", "solo"])
 @pytest.mark.parametrize("n,m,prec,wave_env,wpw", [(250, 1065, "f64", None, 2), (600, 2520, "f32", "1", 1)])
 def test_wave_workgroup_widths(monkeypatch, n, m, prec, wave_env, wpw, team):
     """k_wave with 2 (config 3 in f64) and 1 (a larger instance, forced) replicas per workgroup
     equals FUSED bit for bit, fixed and adaptive -- with the automatic team (8 and 16 waves per
-    replica) and with teams of 1 and 2 waves."""
-    if team is not None:
+    replica) and with teams of 1 and 2 waves; and k_solo (one replica per workgroup, 4 clause slots
+    per lane at m = 2520) on the same formulas."""
+    monkeypatch.setenv("ODESAT_SOLO", "1" if team == "solo" else "0")
+    if team not in (None, "solo"):
         monkeypatch.setenv("ODESAT_WAVE_TEAM", team)
     from odesat_amd import _lib
     var, neg = wl.random_ksat(n, m, 3, 7)
@@ -580,6 +582,8 @@ def test_wave_workgroup_widths(monkeypatch, n, m, prec, wave_env, wpw, team):
             with Solver(f, 9, prec) as s:
                 assert s.group_width == 1
                 s.set_algorithm(alg)
+                if alg == _lib.ODESAT_ALG_RESIDENT:
+                    assert s.step_kernel(adaptive) == ("k_solo" if team == "solo" else "k_wave")
                 s.init_state(11)
                 r = s.simulate(adaptive=adaptive, dt=0.05, max_steps=40, stop=ODESAT_STOP_EACH, poll_interval=7)
                 out.append((r, s.get_state()))
@@ -592,18 +596,27 @@ def test_wave_workgroup_widths(monkeypatch, n, m, prec, wave_env, wpw, team):
 @pytest.mark.parametrize("stop", [ODESAT_STOP_EACH, ODESAT_STOP_ANY, ODESAT_STOP_NONE])
 @pytest.mark.parametrize("adaptive", [False, True])
 def test_wave_teams_equal_fused(monkeypatch, stop, adaptive):
-    """k_wave with one and with two waves per replica (ODESAT_WAVE_TEAM) equals FUSED bit for bit on
-    easy.cnf, where replicas satisfy and freeze at their own steps inside long launches: a frozen
-    replica's team keeps reaching the workgroup barriers of the others."""
+    """k_wave with one, two and four waves per replica (ODESAT_WAVE_TEAM) and k_solo with one, two
+    and three waves (ODESAT_SOLO_LANES) equal FUSED bit for bit on easy.cnf, where replicas satisfy
+    and freeze at their own steps inside long launches: a frozen replica's team keeps reaching the
+    workgroup barriers of the others."""
     from odesat_amd import _lib
     f = product_formula("easy")
     out = []
     for alg, team in ((_lib.ODESAT_ALG_FUSED, "1"), (_lib.ODESAT_ALG_RESIDENT, "1"), (_lib.ODESAT_ALG_RESIDENT, "2"),
-                      (_lib.ODESAT_ALG_RESIDENT, "4")):
+                      (_lib.ODESAT_ALG_RESIDENT, "4"), (_lib.ODESAT_ALG_RESIDENT, "solo64"),
+                      (_lib.ODESAT_ALG_RESIDENT, "solo128"), (_lib.ODESAT_ALG_RESIDENT, "solo192")):
         monkeypatch.setenv("ODESAT_WAVE", "1")
-        monkeypatch.setenv("ODESAT_WAVE_TEAM", team)
+        solo = team.startswith("solo")
+        monkeypatch.setenv("ODESAT_SOLO", "1" if solo else "0")
+        if solo:
+            monkeypatch.setenv("ODESAT_SOLO_LANES", team[4:])
+        else:
+            monkeypatch.setenv("ODESAT_WAVE_TEAM", team)
         with Solver(f, 37, "f32") as s:
             s.set_algorithm(alg)
+            if alg == _lib.ODESAT_ALG_RESIDENT:
+                assert s.step_kernel(adaptive) == ("k_solo" if solo else "k_wave")
             s.init_state(6)
             r = s.simulate(adaptive=adaptive, dt=0.1, tol=1e-3, max_steps=1500, stop=stop, poll_interval=300)
             out.append((r, s.get_state()))
