@@ -81,6 +81,7 @@ struct odesat_solver {
     uint64_t *oc_rec = nullptr;  // [tiles][512] slot-major clause records (onchip::make_rec)
     int32_t *oc_tcp = nullptr;   // [ntp * 8 + 1] wave starts (t * 8 + w) padded with m (static-index loads in k_onchip)
     int64_t oc_rec_bytes = 0;
+    bool oc_ada = false;  // ONCHIP also takes adaptive steps (onchip.hpp ADA_*)
     int oc_off = 0;  // pair offset of the wave-paired tiles (pair_tiles): barrier after tile t iff t + off is odd
     bool in_range = true;        // every replica's state is in ONCHIP's range (onchip.hip header)
     int64_t bytes = 0;
@@ -710,7 +711,7 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
                                      q[0] & 1, q[1] & 1, q[2] & 1);
             } else {
                 const uint32_t sink = 4u * (uint32_t)(s->n + l % onchip::SINKS);
-                r = onchip::make_rec(sink, sink, sink, false, false, false);
+                r = onchip::make_rec(sink, sink, sink, false, false, false) | (uint64_t)onchip::REC_EMPTY << 32;
             }
             rec[(size_t)t * onchip::NTH + l] = r;
         }
@@ -722,6 +723,10 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
     HIP_TRY(hipMemcpy(s->oc_tcp, ws.data(), ws.size() * 4, hipMemcpyHostToDevice));
     s->oc_tr = tr;
     s->oc_tl = tr < live ? nt - tr : 0;
+    // adaptive steps on chip: four voltage arrays in LDS, every tile in VGPRs; the first step of a
+    // call on a caller-supplied state runs k_resident's adaptive step (res_ada)
+    s->oc_ada = s->oc_tl == 0 && s->n <= onchip::ADA_MAX_N && s->res_ada;
+    if (const char *ev = std::getenv("ODESAT_ONCHIP_ADAPTIVE")) s->oc_ada = s->oc_ada && std::atoi(ev) != 0;
     return ODESAT_OK;
 }
 
@@ -885,8 +890,11 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
     }
 }
 
-int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zeta, int stop_mode, bool oop) {
+int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zeta, int stop_mode, bool oop,
+                  bool adaptive, double tol) {
     onchip::Args a{};
+    a.dtr = (float *)s->dtr;
+    a.tol = (float)tol;
     a.oop = oop ? 1 : 0;
     a.rec = s->oc_rec;
     a.rec_bytes = (uint32_t)s->oc_rec_bytes;
@@ -912,7 +920,8 @@ int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zet
     a.xl_max = 1e4f * (float)s->m;  // system.rs:95, as (T)1e4 * (T)m
     {
         Timed tm(s, 0);
-        HIP_TRY(onchip::launch(s->oc_tr, s->oc_off, a, s->G, onchip::lds_bytes(s->n, s->oc_tl), s->stream));
+        const size_t lds = adaptive ? onchip::LDS_MAX : onchip::lds_bytes(s->n, s->oc_tl);
+        HIP_TRY(onchip::launch(s->oc_tr, s->oc_off, a, s->G, lds, s->stream, adaptive));
     }
     return ODESAT_OK;
 }
@@ -1373,10 +1382,12 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             s->res_ada = true;  // wave_lds_bytes(adaptive) fits by selection
             // k_solo (wave.hpp): the latency path when k_wave would run one replica per workgroup
             // anyway (small batches, B = 1 for solve): every lane's clause and variable slots in
-            // registers.  Lanes: the fewest multiple of 64 (at most 1024) giving each lane at most two
-            // clauses and two variables.  ODESAT_SOLO=0/1 and ODESAT_SOLO_LANES override.
-            int64_t nl = 64;
-            while (nl < SOLO_MAX_NL && (m > 2 * nl || n > 2 * nl)) nl += 64;
+            // registers.  Lanes: one per clause, at least 256 (a wave per SIMD) and at most 512
+            // (measured, profiles/r03_solo_sweep.jsonl: hard.cnf f64 fixed 1.01 / 0.81 / 0.79 us per
+            // step at 128 / 256 / 512 lanes; config 3 at 512 lanes 15-25 % under k_wave's best team,
+            // at 1024 no faster and slower in f64 adaptive steps).
+            // ODESAT_SOLO=0/1 and ODESAT_SOLO_LANES override.
+            int64_t nl = std::min<int64_t>(512, std::max<int64_t>(256, (m + 63) / 64 * 64));
             if (const char *ev = std::getenv("ODESAT_SOLO_LANES")) {
                 const int64_t want = std::atoll(ev);
                 if (want >= 64 && want <= SOLO_MAX_NL && want % 64 == 0) nl = want;
@@ -1472,7 +1483,7 @@ extern "C" int odesat_group_width(const odesat_solver *s) { return s ? s->W : fa
 extern "C" const char *odesat_step_kernel(const odesat_solver *s, int adaptive) {
     if (!s) return nullptr;
     if ((s->alg == ODESAT_ALG_RESIDENT || s->alg == ODESAT_ALG_ONCHIP) && (!adaptive || s->res_ada)) {
-        if (s->alg == ODESAT_ALG_ONCHIP && !adaptive) return "k_onchip";
+        if (s->alg == ODESAT_ALG_ONCHIP && (!adaptive || s->oc_ada)) return "k_onchip";
         return s->res_wave ? (s->solo ? "k_solo" : "k_wave") : "k_resident";
     }
     return s->alg == ODESAT_ALG_TWOPASS ? "k_clause_u" : "k_step";
@@ -1673,7 +1684,8 @@ static int simulate_resident(odesat_solver *s, const odesat_params *p, bool adap
     // runs RESIDENT, whose clamps bring every state into range.  (The kernel omits the rigidity term
     // and uses med3 clamps: both exact for finite zeta and a finite, normal dt -- onchip.hip.)
     const double adt = std::fabs(p->dt);
-    const bool oc = s->alg == ODESAT_ALG_ONCHIP && !adaptive && std::fabs(zeta) <= 1e6 && adt >= 1e-30 && adt <= 1e30;
+    const bool oc = s->alg == ODESAT_ALG_ONCHIP && (!adaptive || s->oc_ada) && std::fabs(zeta) <= 1e6 && adt >= 1e-30 &&
+                    adt <= 1e30;
     const bool any = p->stop == ODESAT_STOP_ANY;
     const bool replay = any && (oc || s->res_wave || !adaptive);
     const int per_launch = any && !replay ? 1 : poll;
@@ -1681,7 +1693,7 @@ static int simulate_resident(odesat_solver *s, const odesat_params *p, bool adap
     if (replay && (rc = ensure_snapshot(s))) return rc;
     auto launch = [&](int64_t t0, int k, bool oop) -> int {
         const bool use_oc = oc && (t0 > 0 || s->in_range);
-        return use_oc ? launch_onchip(s, (int)(base + t0), k, p->dt, zeta, p->stop, oop)
+        return use_oc ? launch_onchip(s, (int)(base + t0), k, p->dt, zeta, p->stop, oop, adaptive, tol)
                       : dispatch_resident(s, (int)(base + t0), k, adaptive, p->dt, zeta, tol, p->stop, oop);
     };
     int64_t t = 0, next_poll = poll;
@@ -1695,7 +1707,9 @@ static int simulate_resident(odesat_solver *s, const odesat_params *p, bool adap
         t += k;
         const bool at_poll = t >= next_poll;
         if (at_poll) next_poll += poll;
-        if (replay) {  // every launch is polled, the last one too: it may have run past the stop
+        if (replay && k > 1) {  // every multi-step launch is polled, the last one too: it may have run past the stop
+            // (a one-step launch cannot run past it: later launches see the stop word and do nothing,
+            // so those are polled only at the poll interval, below)
             int32_t h_stop = INT_MAX;
             if ((rc = read_stop(s, &h_stop))) return rc;
             if (h_stop == INT_MAX) continue;
@@ -1756,7 +1770,7 @@ static int simulate_impl(odesat_solver *s, const odesat_params *p, bool cont, in
         }
     }
     const int poll = p->poll_interval > 0 ? p->poll_interval : 32;
-    if (s->alg == ODESAT_ALG_ONCHIP && !adaptive)
+    if (s->alg == ODESAT_ALG_ONCHIP && (!adaptive || s->oc_ada))
         return simulate_resident(s, p, adaptive, zeta, tol, poll, first_sat_step, steps_done, dt_out, steps_run);
     if ((s->alg == ODESAT_ALG_RESIDENT || s->alg == ODESAT_ALG_ONCHIP) && (!adaptive || s->res_ada))
         return simulate_resident(s, p, adaptive, zeta, tol, poll, first_sat_step, steps_done, dt_out, steps_run);

@@ -277,6 +277,168 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
     if constexpr (OFF == 1) __syncthreads();  // the last tile (TR + tl - 1, odd) ends no pair
 }
 
+// ------------------------------------------------------------------------------------------------
+// Adaptive steps (system.rs:111-139, onchip.hpp's ADA_* map).  Pass 1 is the RHS at y (terms with
+// y's memories, which stay in the registers); pass 2 the RHS at the half step.  One code path
+// serves both passes (a uniform flag selects), so a step runs the same ~40 KB of unrolled tile code
+// twice instead of two such sequences that would not share the instruction cache: each clause
+// gathers its voltages from the pass's source (A in pass 1, H in pass 2) and from A (y: their min
+// is pass 1's C, recomputed instead of stored), rebuilds its memories' full-step clone and first
+// half step from y's memories and that C (:124-128), and in pass 2 takes the second half step
+// (:130) and its max_error terms (:101-108).  The arithmetic is k_resident's / k_wave's in the
+// exact rewritten forms of the header (h dxs = (h/2) (2 dxs), (h/2) dxs = (h/4) (2 dxs), ...).
+// Empty slots (REC_EMPTY, onchip.hpp) compute on stand-in memories: their error terms are masked.
+
+struct GathA {  // a clause's gathered inputs: addresses, sign word, voltages from S and from A (y)
+    uint32_t a0, a1, a2, hi;
+    float v0, v1, v2, y0, y1, y2;
+};
+
+struct FrontA {  // literal values at S and their min / second min; min of the values at y
+    uint32_t a0, a1, a2, hi;
+    float val0, val1, val2, mn, sec, mn1;
+};
+
+__device__ __forceinline__ void gatherA(const Slot &S, GathA &G, uint32_t sb) {
+    G.a0 = S.lo & 0xffffu;
+    G.a1 = S.lo >> 16;
+    G.a2 = S.hi & 0xffffu;
+    G.hi = S.hi;
+    G.v0 = lds_f(G.a0 + sb);
+    G.v1 = lds_f(G.a1 + sb);
+    G.v2 = lds_f(G.a2 + sb);
+    G.y0 = lds_f(G.a0);
+    G.y1 = lds_f(G.a1);
+    G.y2 = lds_f(G.a2);
+}
+
+__device__ __forceinline__ void frontA(const GathA &G, FrontA &F) {
+    F.a0 = G.a0;
+    F.a1 = G.a1;
+    F.a2 = G.a2;
+    F.hi = G.hi;
+    const uint32_t s0 = G.hi & 0x80000000u, s1 = (G.hi << 1) & 0x80000000u, s2 = (G.hi << 2) & 0x80000000u;
+    F.val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
+    F.val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
+    F.val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
+    F.mn = fminf(fminf(F.val0, F.val1), F.val2);
+    F.sec = __builtin_amdgcn_fmed3f(F.val0, F.val1, F.val2);
+    const float y0 = 1.0f - __uint_as_float(__float_as_uint(G.y0) ^ s0);
+    const float y1 = 1.0f - __uint_as_float(__float_as_uint(G.y1) ^ s1);
+    const float y2 = 1.0f - __uint_as_float(__float_as_uint(G.y2) ^ s2);
+    F.mn1 = fminf(fminf(y0, y1), y2);  // 2 C of pass 1 (:60)
+}
+
+__device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &mem, float h, float hh, float hq, bool p2,
+                                      Pend &Q, uint32_t &cmax, float &e) {
+    const uint32_t s0 = F.hi & 0x80000000u, s1 = (F.hi << 1) & 0x80000000u, s2 = (F.hi << 2) & 0x80000000u;
+    const float xs = mem.x, xl = mem.y;  // y's memories
+    // full-step clone and first half step of the memories (:124-128) from pass 1's C
+    const float dxs1 = (20.0f * (xs + 0.001f)) * (F.mn1 - 0.5f);  // 2 dxs (:84)
+    const float dxl1 = 2.5f * (F.mn1 - 0.1f);                      // :85
+    const float xs_f = __builtin_amdgcn_fmed3f(xs + hh * dxs1, 0.001f, 1.0f - 0.001f);
+    const float xl_f = __builtin_amdgcn_fmed3f(xl + h * dxl1, 1.0f, a.xl_max);
+    const float xs_h = __builtin_amdgcn_fmed3f(xs + hq * dxs1, 0.001f, 1.0f - 0.001f);
+    const float xl_h = __builtin_amdgcn_fmed3f(xl + hh * dxl1, 1.0f, a.xl_max);
+    // the pass's RHS: at y (pass 1) or at the half step (pass 2)
+    const float xs_t = p2 ? xs_h : xs, xl_t = p2 ? xl_h : xl;
+    const float mn = F.mn;
+    const float tt = xl_t * xs_t;
+    const float tm = tt * mn, ts = tt * F.sec;
+    Q.a0 = F.a0;
+    Q.a1 = F.a1;
+    Q.a2 = F.a2;
+    Q.d0 = __uint_as_float(__float_as_uint(F.val0 != mn ? tm : ts) ^ s0);  // 2 xl xs G (:64-70, :80)
+    Q.d1 = __uint_as_float(__float_as_uint(F.val1 != mn ? tm : ts) ^ s1);
+    Q.d2 = __uint_as_float(__float_as_uint(F.val2 != mn ? tm : ts) ^ s2);
+    cmax = max(cmax, __float_as_uint(mn));  // :88 (pass 1)
+    asm volatile("" : "+v"(cmax));
+    // second half step (:130) and its max_error terms (:132), pass 2
+    const float dxs2 = (20.0f * (xs_t + 0.001f)) * (mn - 0.5f);
+    const float dxl2 = 2.5f * (mn - 0.1f);
+    const float xs_n = __builtin_amdgcn_fmed3f(xs_t + hq * dxs2, 0.001f, 1.0f - 0.001f);
+    const float xl_n = __builtin_amdgcn_fmed3f(xl_t + hh * dxl2, 1.0f, a.xl_max);
+    const float ee = fmaxf(e, fmaxf(fabsf(xs_f - xs_n), fabsf(xl_f - xl_n)));
+    e = (p2 && !(F.hi & REC_EMPTY)) ? ee : e;
+    mem.x = p2 ? xs_n : xs;
+    mem.y = p2 ? xl_n : xl;
+    asm volatile("" : "+v"(mem.x), "+v"(mem.y), "+v"(e));
+}
+
+__device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &slot3, float2 &mem1, Pend &P,
+                                           FrontA &Fn, GathA &Gn, int t, float h, float hh, float hq, uint32_t sb,
+                                           bool p2, uint32_t &cmax, float &e, bool bar) {
+    const float o0 = lds_f(P.a0 + ADA_D), o1 = lds_f(P.a1 + ADA_D), o2 = lds_f(P.a2 + ADA_D);
+    lds_st(P.a0 + ADA_D, o0 + P.d0);
+    lds_st(P.a1 + ADA_D, o1 + P.d1);
+    lds_st(P.a2 + ADA_D, o2 + P.d2);
+    __builtin_amdgcn_sched_barrier(0);
+    GathA G3;
+    gatherA(slot3, G3, sb);
+    slot3 = load_rec(R, t + 7);
+    __builtin_amdgcn_sched_barrier(0);
+    backA(a, Fn, mem1, h, hh, hq, p2, P, cmax, e);
+    frontA(Gn, Fn);
+    __builtin_amdgcn_sched_barrier(0);
+    if (bar) __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    Gn = G3;
+}
+
+// Register tile T of an adaptive pass; the pass's last tile ends no pair (passA closes with a barrier).
+template <int TR, int OFF, int T>
+__device__ __forceinline__ void reg_tileA(const Args &a, const Recs &R, float2 (&mr)[TR], Slot (&ring)[4], Pend &P,
+                                          FrontA &Fn, GathA &Gn, float h, float hh, float hq, uint32_t sb, bool p2,
+                                          uint32_t &cmax, float &e) {
+    constexpr bool bar = ((T + OFF) & 1) != 0 && T + 1 < TR;
+    if constexpr (T + 1 < TR) {
+        tile_stepA(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, hq, sb, p2, cmax, e, bar);
+    } else {  // the (empty) tile after the last: stand-in memories, nothing stored
+        float2 m = make_float2(0.0f, 0.0f);
+        tile_stepA(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, hq, sb, p2, cmax, e, bar);
+    }
+}
+
+template <int TR, int OFF, int... Ts>
+__device__ __forceinline__ void reg_tilesA(std::integer_sequence<int, Ts...>, const Args &a, const Recs &R,
+                                           float2 (&mr)[TR], Slot (&ring)[4], Pend &P, FrontA &Fn, GathA &Gn, float h,
+                                           float hh, float hq, uint32_t sb, bool p2, uint32_t &cmax, float &e) {
+    (reg_tileA<TR, OFF, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, hq, sb, p2, cmax, e), ...);
+}
+
+// One adaptive pass over every tile (all in registers): the RHS at the source sb (0: A, ADA_H: H)
+// into D and, in pass 2, the memories' second half step; pass 1 raises the unsat flag at `flag`
+// (:88).  Ends with a barrier.
+template <int TR, int OFF>
+__device__ __forceinline__ void passA(const Args &a, float2 (&mr)[TR], float h, int lane, uint32_t sb, bool p2,
+                                      uint32_t flag, float &e) {
+    Recs R;
+    R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec, 0, (int)a.rec_bytes, 0x00020000);
+    R.voff = (uint32_t)lane * 8u;
+    R.soff = 0u;
+    asm volatile("" : "+s"(R.soff));
+    const float hh = 0.5f * h, hq = 0.25f * h;
+    uint32_t cmax = 0u;
+    Slot ring[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) ring[s] = load_rec(R, s);
+    Pend P;
+    GathA G0, G1, Gn;
+    gatherA(ring[0], G0, sb);
+    ring[0] = load_rec(R, 4);
+    gatherA(ring[1], G1, sb);
+    ring[1] = load_rec(R, 5);
+    gatherA(ring[2], Gn, sb);
+    ring[2] = load_rec(R, 6);
+    FrontA F0, Fn;
+    frontA(G0, F0);
+    frontA(G1, Fn);
+    backA(a, F0, mr[0], h, hh, hq, p2, P, cmax, e);
+    reg_tilesA<TR, OFF>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, hq, sb, p2, cmax, e);
+    if (!p2 && !(__uint_as_float(cmax) < 0.5f)) lds_st(flag, 1.0f);
+    __syncthreads();
+}
+
 typedef const __attribute__((address_space(4))) int32_t cint32;
 
 // The state moves through HBM once per launch, read once and written once: non-temporal (aux nt),
@@ -358,7 +520,7 @@ __device__ __forceinline__ void mem_store(std::integer_sequence<int, Gs...>, con
 }
 
 // The kernel declares no static LDS, so dynamic LDS -- and the records' byte addresses -- start at 0.
-template <int TR, int OFF>
+template <int TR, int OFF, bool ADA>
 __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     const int g = blockIdx.x, lane = threadIdx.x;
     const int wl = lane & 63;  // slot of this lane in its wave's share of a tile
@@ -372,7 +534,9 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     // buffer and par flips, so the launch's starting state survives for a replay
     const bool q = a.oop ? !p : p;
     const int n2 = a.n + SINKS;
-    const uint32_t UNS = DVC + 4u * (uint32_t)n2;  // two unsat flags
+    constexpr uint32_t DV = ADA ? ADA_D : DVC;
+    // two unsat flags (adaptive: after A's sinks, then the waves' error words)
+    const uint32_t UNS = ADA ? 4u * (uint32_t)n2 : DVC + 4u * (uint32_t)n2;
     int64_t sat = a.sat_step[g], done = a.steps_done[g];
     const cint32 *tcw = (const cint32 *)a.tc + __builtin_amdgcn_readfirstlane(lane >> 6);  // this wave's starts
 
@@ -387,7 +551,8 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                 const int i = i0 + u * NTH;
                 if (i < n2) {
                     lds_st(4u * i, i < a.n ? x[u] : 1.0f);
-                    lds_st(4u * i + DVC, 0.0f);
+                    lds_st(4u * i + DV, 0.0f);
+                    if (ADA && i >= a.n) lds_st(4u * i + ADA_H, 1.0f);  // H's sinks (pass 2 gathers them)
                 }
             }
         }
@@ -405,6 +570,65 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
 
     const float h = a.dt, hh = 0.5f * a.dt;
     Stamps S{};
+    float dtr = ADA ? a.dtr[g] : a.dt;
+    if constexpr (ADA) {
+        for (int k = 0; k < a.nsteps; ++k) {  // euler_step (system.rs:111-139)
+            const float hk = dtr, hhk = 0.5f * dtr, hqk = 0.25f * dtr;
+            const uint32_t flag = UNS + 4u * (k & 1);
+            float e = 0.0f;
+            bool uns = false;
+            // the two passes run ONE instance of the unrolled tile code (a loop the compiler keeps)
+#pragma clang loop unroll(disable)
+            for (int ps = 0; ps < 2; ++ps) {
+                const bool p2 = ps == 1;
+                passA<TR, OFF>(a, mr, hk, lane, p2 ? ADA_H : 0u, p2, flag, e);  // RHS at y, then at the half step
+                if (!p2) {
+                    uns = lds_f(flag) != 0.0f;  // uniform
+                    if (!uns) {  // an allsat replica takes no step (:122): drop pass 1's terms
+                        for (int i = lane; i < a.n; i += NTH) lds_st(4u * i + ADA_D, 0.0f);
+                        break;
+                    }
+                    for (int i = lane; i < a.n; i += NTH) {  // full-step clone and first half step (:124-128)
+                        const float d2 = lds_f(4u * i + ADA_D), y = lds_f(4u * i);
+                        lds_st(4u * i + ADA_D, 0.0f);
+                        lds_st(4u * i + ADA_F, __builtin_amdgcn_fmed3f(y + hhk * d2, -1.0f, 1.0f));
+                        lds_st(4u * i + ADA_H, __builtin_amdgcn_fmed3f(y + hqk * d2, -1.0f, 1.0f));
+                    }
+                    __syncthreads();
+                } else {
+                    for (int i = lane; i < a.n; i += NTH) {  // second half step (:130), max_error (:101-108)
+                        const float d2 = lds_f(4u * i + ADA_D);
+                        lds_st(4u * i + ADA_D, 0.0f);
+                        const float vn = __builtin_amdgcn_fmed3f(lds_f(4u * i + ADA_H) + hqk * d2, -1.0f, 1.0f);
+                        e = fmaxf(e, fabsf(lds_f(4u * i + ADA_F) - vn));
+                        lds_st(4u * i, vn);
+                    }
+                    uint32_t eb = __float_as_uint(e);  // non-negative: the bits order as the values
+#pragma unroll
+                    for (int off = 32; off >= 1; off >>= 1) eb = max(eb, (uint32_t)__shfl_xor((int)eb, off, 64));
+                    if ((lane & 63) == 0) lds_st(UNS + 8u + 4u * (uint32_t)(lane >> 6), __uint_as_float(eb));
+                }
+            }
+            if (lane == 0) lds_st(UNS + 4u * ((k + 1) & 1), 0.0f);  // read by everyone after this step's first pass
+            __syncthreads();
+            if (uns) {  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
+                uint32_t eb = 0u;
+#pragma unroll
+                for (int w = 0; w < WAVES; ++w) eb = max(eb, __float_as_uint(lds_f(UNS + 8u + 4u * w)));
+                dtr = fmaxf(fminf(dtr * sqrtf(a.tol / __uint_as_float(eb)), 1e3f), 0.0078125f);
+            }
+            done += 1;
+            if (!uns) {  // allsat: no step taken (:122)
+                const int step = a.step0 + k;
+                if (sat < 0) sat = step;
+                if (a.stop_mode == ODESAT_STOP_ANY && lane == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
+                if (a.stop_mode == ODESAT_STOP_EACH) {                                      // simulate (:193)
+                    act = 0;
+                    break;
+                }
+            }
+        }
+    } else
     for (int k = 0; k < a.nsteps; ++k) {  // euler_step_fixed (system.rs:141-154)
         uint32_t cmax = 0u;
 #ifdef ONCHIP_STAMPS
@@ -459,22 +683,34 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         a.act[g] = (uint8_t)act;
         a.sat_step[g] = sat;
         a.steps_done[g] = done;
+        if (ADA) a.dtr[g] = dtr;
     }
 }
 
-template <int TR, int OFF> hipError_t launch_t(const Args &a, int G, size_t lds, hipStream_t stream) {
-    hipError_t e = odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_onchip<TR, OFF>), (int)LDS_MAX);
+template <int TR, int OFF, bool ADA> hipError_t launch_t(const Args &a, int G, size_t lds, hipStream_t stream) {
+    hipError_t e = odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_onchip<TR, OFF, ADA>), (int)LDS_MAX);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_onchip<TR, OFF>), dim3((unsigned)G), dim3(NTH), lds, stream, a);
+    hipLaunchKernelGGL((k_onchip<TR, OFF, ADA>), dim3((unsigned)G), dim3(NTH), lds, stream, a);
     return hipGetLastError();
 }
 
 }  // namespace
 
-hipError_t launch(int tr, int off, const Args &a, int G, size_t lds, hipStream_t stream) {
+hipError_t launch(int tr, int off, const Args &a, int G, size_t lds, hipStream_t stream, bool adaptive) {
     switch (tr) {
-#define ONCHIP_CASE(N) \
-    case N: return off ? launch_t<N, 1>(a, G, lds, stream) : launch_t<N, 0>(a, G, lds, stream);
+#ifdef ONCHIP_ONLY_TR  // experiments: one shape (scripts/build_variant.sh style quick builds)
+#define ONCHIP_CASE(N)                                                                                  \
+    case N:                                                                                             \
+        if constexpr (N == ONCHIP_ONLY_TR) {                                                            \
+            if (adaptive) return off ? launch_t<N, 1, true>(a, G, lds, stream) : launch_t<N, 0, true>(a, G, lds, stream); \
+            return off ? launch_t<N, 1, false>(a, G, lds, stream) : launch_t<N, 0, false>(a, G, lds, stream); \
+        } else return hipErrorInvalidValue;
+#else
+#define ONCHIP_CASE(N)                                                                                  \
+    case N:                                                                                             \
+        if (adaptive) return off ? launch_t<N, 1, true>(a, G, lds, stream) : launch_t<N, 0, true>(a, G, lds, stream); \
+        return off ? launch_t<N, 1, false>(a, G, lds, stream) : launch_t<N, 0, false>(a, G, lds, stream);
+#endif
         ONCHIP_CASE(8) ONCHIP_CASE(16) ONCHIP_CASE(24) ONCHIP_CASE(32) ONCHIP_CASE(40) ONCHIP_CASE(48)
         ONCHIP_CASE(56) ONCHIP_CASE(64) ONCHIP_CASE(66) ONCHIP_CASE(68) ONCHIP_CASE(70) ONCHIP_CASE(72)
         ONCHIP_CASE(74) ONCHIP_CASE(76) ONCHIP_CASE(78) ONCHIP_CASE(80) ONCHIP_CASE(82) ONCHIP_CASE(84)

@@ -48,6 +48,14 @@ inline int tl_max(int64_t n) {
     return (int)(L.gap_tiles + L.after_tiles) / 4 * 4;
 }
 
+// Adaptive steps (system.rs:111-139) keep four voltage arrays in LDS and every tile's memories in
+// VGPRs (no LDS tiles): A = the step's starting voltages y (and then its result), D = 2 dv (within
+// the ds instructions' 16-bit immediate of A, as DVC), H = the half step, F = the full-step clone,
+// n + SINKS floats each; A's region also holds the unsat flags and the waves' error words.
+constexpr uint32_t ADA_D = 40960, ADA_H = 81920, ADA_F = 122880;
+constexpr int ADA_FLAGS = 2 + WAVES;
+constexpr int ADA_MAX_N = (int)(ADA_D / 4) - SINKS - ADA_FLAGS;
+
 struct Args {
     const uint64_t *rec; // [tiles][NTH] slot-major clause records (make_rec), padded with empty tiles
     uint32_t rec_bytes;
@@ -65,6 +73,8 @@ struct Args {
     int32_t oop;         // 1: write the final state to the other buffer and flip par (replayable launch)
     float dt, xl_max;
     Lds lds;
+    float *dtr;          // [B] per-replica adaptive dt (adaptive launches)
+    float tol;           // adaptive tolerance, as the solver's f32
 };
 
 // Register-tile counts compiled (template instantiations; VGPRs ~ 50 + 2 TR, ~245 at TR = 96).
@@ -78,7 +88,9 @@ constexpr int TR_CHOICES[] = {8, 16, 24, 32, 40, 48, 56, 64, 66, 68, 70, 72, 74,
 constexpr int TR_MAX = 96;
 
 // Record of one clause slot (8 bytes): lo = a0 | a1 << 16, hi = a2 | neg0 << 31 | neg1 << 30 |
-// neg2 << 29, with a_j = 4 * var_j the LDS byte address of the literal's voltage.
+// neg2 << 29, with a_j = 4 * var_j the LDS byte address of the literal's voltage; an empty slot
+// (all three literals at its lane's sink word) also has REC_EMPTY in hi.
+constexpr uint32_t REC_EMPTY = 1u << 28;
 inline uint64_t make_rec(uint32_t a0, uint32_t a1, uint32_t a2, bool n0, bool n1, bool n2) {
     const uint32_t lo = a0 | (a1 << 16);
     const uint32_t hi = a2 | (n0 ? 0x80000000u : 0u) | (n1 ? 0x40000000u : 0u) | (n2 ? 0x20000000u : 0u);
@@ -86,7 +98,8 @@ inline uint64_t make_rec(uint32_t a0, uint32_t a1, uint32_t a2, bool n0, bool n1
 }
 
 // Launch over replicas [0, G) on `stream`; tr must be one of TR_CHOICES, off (0 / 1) the pair offset
-// of the wave-paired tiles (a barrier after tile t iff t + off is odd).
-hipError_t launch(int tr, int off, const Args &a, int G, size_t lds, hipStream_t stream);
+// of the wave-paired tiles (a barrier after tile t iff t + off is odd).  adaptive: euler_step with
+// per-replica dt (a.dtr, a.tol); needs a.tl == 0 and n <= ADA_MAX_N, and LDS_MAX bytes of LDS.
+hipError_t launch(int tr, int off, const Args &a, int G, size_t lds, hipStream_t stream, bool adaptive = false);
 
 }  // namespace onchip

@@ -348,6 +348,9 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
 // ------------------------------------------------------------------------------------------------
 constexpr int SOLO_MAX_NL = 1024;
 
+// 8 term reads in flight per round (16 measured slower: profiles/r03_solo_sweep2.jsonl -- hard.cnf
+// f64 at 256 lanes 1.00 vs 0.81 us per fixed step -- the extra registers and reads cost more than
+// the second round trip of the few high-degree variables saves)
 template <typename T> __device__ __forceinline__ T solo_fold(const T *tL, int s, int d, int L) {
     T dv = (T)0.0;  // :33, then the reference's left fold of the variable's terms (:80)
     for (int k0 = 0; k0 < d; k0 += 8) {

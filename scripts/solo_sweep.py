@@ -32,7 +32,8 @@ def main():
     shapes = [("wave-t1", {"ODESAT_SOLO": "0", "ODESAT_WAVE_TEAM": "1"}),
               ("wave-t2", {"ODESAT_SOLO": "0", "ODESAT_WAVE_TEAM": "2"}),
               ("wave-t4", {"ODESAT_SOLO": "0", "ODESAT_WAVE_TEAM": "4"})]
-    shapes += [(f"solo-l{k}", {"ODESAT_SOLO": "1", "ODESAT_SOLO_LANES": str(k)}) for k in (64, 128, 192, 256, 512)]
+    shapes += [(f"solo-l{k}", {"ODESAT_SOLO": "1", "ODESAT_SOLO_LANES": str(k)}) for k in (128, 256, 512, 1024)]
+    shapes += [("solo-default", {"ODESAT_SOLO": "1"})]
     for fname, f, B, steps in (("hard", hard, 1, args.steps), ("config3", cfg3, 1, args.steps // 4),
                                ("config3", cfg3, 64, args.steps // 10)):
         for prec in ("f64", "f32"):

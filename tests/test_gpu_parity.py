@@ -536,9 +536,10 @@ def test_onchip_lds_tiles_match_resident_and_oracle(stop, monkeypatch, pair_off)
     assert same(v[0], ov) and same(xs[0], oxs) and same(xl[0], oxl)
 
 
-def test_onchip_long_launches_sat_and_freeze(monkeypatch):
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_onchip_long_launches_sat_and_freeze(monkeypatch, adaptive):
     """STOP_EACH over launches of many steps: replicas that satisfy easy.cnf freeze at their own
-    step inside a launch (ONCHIP == k_wave == FUSED, states and sat steps)."""
+    step inside a launch (ONCHIP == k_wave == FUSED, states, sat steps and adaptive dt)."""
     from odesat_amd import _lib
     f = product_formula("easy")
     out = []
@@ -547,14 +548,50 @@ def test_onchip_long_launches_sat_and_freeze(monkeypatch):
         monkeypatch.setenv("ODESAT_RES_NARROW", "0")
         with Solver(f, 40, "f32") as s:
             s.set_algorithm(alg)
+            if alg == _lib.ODESAT_ALG_ONCHIP:
+                assert s.step_kernel(adaptive) == "k_onchip"
             s.init_state(4)
-            r = s.simulate(dt=0.1, max_steps=3000, stop=ODESAT_STOP_EACH, poll_interval=500)
-            out.append((r["first_sat_step"], r["steps_done"], s.get_state()))
+            r = s.simulate(adaptive=adaptive, dt=0.1, tol=1e-3, max_steps=3000, stop=ODESAT_STOP_EACH,
+                           poll_interval=500)
+            out.append((r["first_sat_step"], r["steps_done"], r["dt"], s.get_state()))
     assert (out[0][0] >= 0).any()
     for o in out[1:]:
-        assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1])
-        for x, y in zip(out[0][2], o[2]):
+        assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1]) and same(out[0][2], o[2])
+        for x, y in zip(out[0][3], o[3]):
             assert same(x, y)
+
+
+@pytest.mark.parametrize("stop", ["each", "any", "none"])
+def test_onchip_adaptive_matches_resident_and_oracle(stop, monkeypatch):
+    """Adaptive steps on chip (k_onchip's adaptive variant: four voltage arrays in LDS, the clause
+    memories in VGPRs, one code instance for both passes) == k_resident's adaptive step
+    (ODESAT_ONCHIP_ADAPTIVE=0) bit for bit on every stop policy, per-replica dt included, and
+    replica 0 == the oracle's f32 simulate with tol 1e-3 (system.rs:111-139, :204-234)."""
+    from odesat_amd import _lib
+    f, (cp, v_, n_) = _instance(3000, 12600, 5)
+    pol = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[stop]
+    B, K = 6, 30
+    out = []
+    for ada in ("1", "0"):
+        monkeypatch.setenv("ODESAT_ONCHIP_ADAPTIVE", ada)
+        with Solver(f, B, "f32") as s:
+            assert s.algorithm == _lib.ODESAT_ALG_ONCHIP
+            assert s.step_kernel(True) == ("k_onchip" if ada == "1" else "k_resident")
+            s.init_state(9)
+            r = s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=K, stop=pol, poll_interval=10)
+            out.append((r, s.get_state()))
+    (r1, s1), (r2, s2) = out
+    assert np.array_equal(r1["first_sat_step"], r2["first_sat_step"]) and np.array_equal(r1["steps_done"], r2["steps_done"])
+    assert same(r1["dt"], r2["dt"])
+    for x, y in zip(s1, s2):
+        assert same(x, y)
+    o = Oracle(cp, v_, n_, 3000, "f32")
+    ov = init_voltages(9, 0, 1, 3000)[0].astype(np.float32)
+    oxs, oxl = o.init_short_term_memory(), np.ones(12600, np.float32)
+    t, _, _, h, _ = o.simulate(ov, oxs, oxl, tol=np.float32(1e-3), dt=None, steps=int(r1["steps_done"][0]),
+                               zeta=np.float32(0.001))
+    assert t == r1["steps_done"][0] and same(np.float32(h), np.float32(r1["dt"][0]))
+    assert same(s1[0][0], ov) and same(s1[1][0], oxs) and same(s1[2][0], oxl)
 
 
 @pytest.mark.parametrize("team", [None, "1", "2", "solo"])
