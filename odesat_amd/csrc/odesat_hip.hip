@@ -895,12 +895,6 @@ int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zet
     onchip::Args a{};
     a.dtr = (float *)s->dtr;
     a.tol = (float)tol;
-    if (const char *ev = std::getenv("ODESAT_ONCHIP_STAGGER_TICKS")) {  // experiment: staggered first round
-        a.stagger = std::atoi(ev);
-        int cus = 256;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, s->device) != hipSuccess || cus <= 0) cus = 256;
-        a.stagger_wgs = s->G > cus ? cus : 0;
-    }
     a.oop = oop ? 1 : 0;
     a.rec = s->oc_rec;
     a.rec_bytes = (uint32_t)s->oc_rec_bytes;

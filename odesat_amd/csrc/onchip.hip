@@ -524,13 +524,6 @@ template <int TR, int OFF, bool ADA>
 __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     const int g = blockIdx.x, lane = threadIdx.x;
     const int wl = lane & 63;  // slot of this lane in its wave's share of a tile
-    if (a.stagger > 0 && g < a.stagger_wgs) {
-        // the first round of workgroups (one per CU) starts in four phases, so the later rounds --
-        // each CU runs its workgroups back to back -- keep moving their state through HBM while
-        // other CUs compute, instead of all CUs loading and storing at once
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime(), wait = (uint64_t)((g / 8) % 4) * (uint64_t)a.stagger;
-        while (__builtin_amdgcn_s_memrealtime() - t0 < wait) __builtin_amdgcn_s_sleep(8);
-    }
     int act = a.act[g];
     if (!act) return;  // frozen replica (uniform)
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica

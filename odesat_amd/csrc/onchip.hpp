@@ -75,8 +75,6 @@ struct Args {
     Lds lds;
     float *dtr;          // [B] per-replica adaptive dt (adaptive launches)
     float tol;           // adaptive tolerance, as the solver's f32
-    int32_t stagger;     // first-round workgroups b < stagger_wgs wait (b / 8 % 4) * stagger ticks of the 100 MHz clock
-    int32_t stagger_wgs;
 };
 
 // Register-tile counts compiled (template instantiations; VGPRs ~ 50 + 2 TR, ~245 at TR = 96).
