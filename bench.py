@@ -142,7 +142,9 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     devices = 1
-    if world > 1:
+    # ODESAT_BENCH_DIST=1: a process group even at world 1 (rehearses the RCCL paths -- TorchComm,
+    # graph-captured collectives -- on a one-GPU box)
+    if world > 1 or os.environ.get("ODESAT_BENCH_DIST") == "1":
         import torch
         import torch.distributed as td
         ndev = torch.cuda.device_count()
@@ -375,34 +377,52 @@ def main():
                      "batch_per_gpu": B, "kernel": a_,
                      "roofline": roofline(args, a_, ms_, l_, b_, dtype=kw.get("dtype"), mode=mode, steps=ran)}
 
-    if "f64" in legs and args.config == "config2" and args.dtype == "f32":
-        simple_leg("f64", dtype="f64")
-    if "adaptive" in legs and args.config == "config2":
-        simple_leg("adaptive", adaptive=True)
+    def leg(name, fn):
+        """One extra leg: its object, or {"error": ...} -- a failing leg never costs the headline line.
+        (Every rank runs the same code on the same data, so a leg fails on all ranks alike.)"""
+        try:
+            fn()
+        except Exception as e:  # noqa: BLE001 -- reported in the line, traceback on stderr
+            import traceback
+            traceback.print_exc()
+            res[name] = {"error": f"{type(e).__name__}: {e}"}
 
-    if "inter" in legs:  # simulate_inter (STOP_ANY): multi-step launches with replay at the stop step
+    if "f64" in legs and args.config == "config2" and args.dtype == "f32":
+        leg("f64", lambda: simple_leg("f64", dtype="f64"))
+    if "adaptive" in legs and args.config == "config2":
+        leg("adaptive", lambda: simple_leg("adaptive", adaptive=True))
+
+    def inter_leg():  # simulate_inter (STOP_ANY): multi-step launches with replay at the stop step
         ri = run_batch(B, False, stop=ODESAT_STOP_ANY)
         wi, ran = max_over_ranks(dist, ri[0]), ri[5]  # a stop before `steps` ends the run early
         res["inter"] = {"value": B * world * ran / wi, "ms_per_step": wi * 1e3 / ran, "steps_run": ran,
                         "vs_stop_none": (B * world * ran / wi) / value}
 
+    if "inter" in legs:
+        leg("inter", inter_leg)
     if "config4" in legs:
-        res["inter_config4"] = config4_leg(args, world, rank, local, dist)
-
+        leg("inter_config4", lambda: res.__setitem__("inter_config4", config4_leg(args, world, rank, local, dist)))
     # ------------------------------------------ config 5: one instance partitioned over the ranks ---
     if "config5" in legs:
-        res["partition_config5"] = config5_leg(args, world, rank, local, dist)
+        leg("partition_config5",
+            lambda: res.__setitem__("partition_config5", config5_leg(args, world, rank, local, dist)))
 
-    if "extra" in legs and args.extra_batch != B:
+    def extra_leg():
         w2 = max_over_ranks(dist, run_batch(args.extra_batch, False)[0])
         res["extra_batch"] = {"batch_per_gpu": args.extra_batch, "value": args.extra_batch * world * args.steps / w2,
                               "ms_per_step": w2 * 1e3 / args.steps}
 
-    if "ab" in legs and kern == "k_onchip":
+    if "extra" in legs and args.extra_batch != B:
+        leg("extra_batch", extra_leg)
+
+    def ab_leg():
         w3, ms3, l3, b3, a3, _ = run_batch(B, True, "resident")
         w3 = max_over_ranks(dist, w3)
         res["ab_hbm_streaming"] = {"value": B * world * args.steps / w3, "ms_per_step": w3 * 1e3 / args.steps,
                                    "roofline": roofline(args, a3, ms3, l3, b3)}
+
+    if "ab" in legs and kern == "k_onchip":
+        leg("ab_hbm_streaming", ab_leg)
 
     cpu = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu:
