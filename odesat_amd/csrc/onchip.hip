@@ -294,9 +294,9 @@ struct GathA {  // a clause's gathered inputs: addresses, sign word, voltages fr
     float v0, v1, v2, y0, y1, y2;
 };
 
-struct FrontA {  // literal values at S and their min / second min; min of the values at y
+struct FrontA {  // literal values at S and their min / second min; the voltages at y (pass 2's use)
     uint32_t a0, a1, a2, hi;
-    float val0, val1, val2, mn, sec, mn1;
+    float val0, val1, val2, mn, sec, y0, y1, y2;
 };
 
 __device__ __forceinline__ void gatherA(const Slot &S, GathA &G, uint32_t sb) {
@@ -323,25 +323,31 @@ __device__ __forceinline__ void frontA(const GathA &G, FrontA &F) {
     F.val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
     F.mn = fminf(fminf(F.val0, F.val1), F.val2);
     F.sec = __builtin_amdgcn_fmed3f(F.val0, F.val1, F.val2);
-    const float y0 = 1.0f - __uint_as_float(__float_as_uint(G.y0) ^ s0);
-    const float y1 = 1.0f - __uint_as_float(__float_as_uint(G.y1) ^ s1);
-    const float y2 = 1.0f - __uint_as_float(__float_as_uint(G.y2) ^ s2);
-    F.mn1 = fminf(fminf(y0, y1), y2);  // 2 C of pass 1 (:60)
+    F.y0 = G.y0;
+    F.y1 = G.y1;
+    F.y2 = G.y2;
 }
 
 __device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &mem, float h, float hh, float hq, bool p2,
                                       Pend &Q, uint32_t &cmax, float &e) {
     const uint32_t s0 = F.hi & 0x80000000u, s1 = (F.hi << 1) & 0x80000000u, s2 = (F.hi << 2) & 0x80000000u;
     const float xs = mem.x, xl = mem.y;  // y's memories
-    // full-step clone and first half step of the memories (:124-128) from pass 1's C
-    const float dxs1 = (20.0f * (xs + 0.001f)) * (F.mn1 - 0.5f);  // 2 dxs (:84)
-    const float dxl1 = 2.5f * (F.mn1 - 0.1f);                      // :85
-    const float xs_f = __builtin_amdgcn_fmed3f(xs + hh * dxs1, 0.001f, 1.0f - 0.001f);
-    const float xl_f = __builtin_amdgcn_fmed3f(xl + h * dxl1, 1.0f, a.xl_max);
-    const float xs_h = __builtin_amdgcn_fmed3f(xs + hq * dxs1, 0.001f, 1.0f - 0.001f);
-    const float xl_h = __builtin_amdgcn_fmed3f(xl + hh * dxl1, 1.0f, a.xl_max);
+    float xs_t = xs, xl_t = xl, xs_f = 0.0f, xl_f = 0.0f;
+    if (p2) {  // uniform: pass 1 computes none of this
+        // pass 1's 2 C (:60) from the voltages at y, then the full-step clone and the first half
+        // step of the memories (:124-128)
+        const float y0 = 1.0f - __uint_as_float(__float_as_uint(F.y0) ^ s0);
+        const float y1 = 1.0f - __uint_as_float(__float_as_uint(F.y1) ^ s1);
+        const float y2 = 1.0f - __uint_as_float(__float_as_uint(F.y2) ^ s2);
+        const float mn1 = fminf(fminf(y0, y1), y2);
+        const float dxs1 = (20.0f * (xs + 0.001f)) * (mn1 - 0.5f);  // 2 dxs (:84)
+        const float dxl1 = 2.5f * (mn1 - 0.1f);                      // :85
+        xs_f = __builtin_amdgcn_fmed3f(xs + hh * dxs1, 0.001f, 1.0f - 0.001f);
+        xl_f = __builtin_amdgcn_fmed3f(xl + h * dxl1, 1.0f, a.xl_max);
+        xs_t = __builtin_amdgcn_fmed3f(xs + hq * dxs1, 0.001f, 1.0f - 0.001f);  // the half step's memories
+        xl_t = __builtin_amdgcn_fmed3f(xl + hh * dxl1, 1.0f, a.xl_max);
+    }
     // the pass's RHS: at y (pass 1) or at the half step (pass 2)
-    const float xs_t = p2 ? xs_h : xs, xl_t = p2 ? xl_h : xl;
     const float mn = F.mn;
     const float tt = xl_t * xs_t;
     const float tm = tt * mn, ts = tt * F.sec;
@@ -353,15 +359,16 @@ __device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &me
     Q.d2 = __uint_as_float(__float_as_uint(F.val2 != mn ? tm : ts) ^ s2);
     cmax = max(cmax, __float_as_uint(mn));  // :88 (pass 1)
     asm volatile("" : "+v"(cmax));
-    // second half step (:130) and its max_error terms (:132), pass 2
-    const float dxs2 = (20.0f * (xs_t + 0.001f)) * (mn - 0.5f);
-    const float dxl2 = 2.5f * (mn - 0.1f);
-    const float xs_n = __builtin_amdgcn_fmed3f(xs_t + hq * dxs2, 0.001f, 1.0f - 0.001f);
-    const float xl_n = __builtin_amdgcn_fmed3f(xl_t + hh * dxl2, 1.0f, a.xl_max);
-    const float ee = fmaxf(e, fmaxf(fabsf(xs_f - xs_n), fabsf(xl_f - xl_n)));
-    e = (p2 && !(F.hi & REC_EMPTY)) ? ee : e;
-    mem.x = p2 ? xs_n : xs;
-    mem.y = p2 ? xl_n : xl;
+    if (p2) {  // second half step (:130) and its max_error terms (:132)
+        const float dxs2 = (20.0f * (xs_t + 0.001f)) * (mn - 0.5f);
+        const float dxl2 = 2.5f * (mn - 0.1f);
+        const float xs_n = __builtin_amdgcn_fmed3f(xs_t + hq * dxs2, 0.001f, 1.0f - 0.001f);
+        const float xl_n = __builtin_amdgcn_fmed3f(xl_t + hh * dxl2, 1.0f, a.xl_max);
+        const float ee = fmaxf(e, fmaxf(fabsf(xs_f - xs_n), fabsf(xl_f - xl_n)));
+        e = (F.hi & REC_EMPTY) ? e : ee;
+        mem.x = xs_n;
+        mem.y = xl_n;
+    }
     asm volatile("" : "+v"(mem.x), "+v"(mem.y), "+v"(e));
 }
 
