@@ -94,11 +94,12 @@ def parse():
     return args
 
 
-def visible_gpus():
+def visible_gpus(topology="/sys/class/kfd/kfd/topology/nodes", dri="/dev/dri", env=None):
     """GPUs this process could use, counted WITHOUT a HIP call (the parent of the rank processes must
     not initialise the GPU): the KFD topology's GPU nodes whose render node is present and accessible,
     narrowed by ROCR/HIP/CUDA_VISIBLE_DEVICES.  None when the topology is unreadable."""
-    nodes = sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"))
+    env = os.environ if env is None else env
+    nodes = sorted(glob.glob(os.path.join(topology, "*", "properties")))
     if not nodes:
         return None
     count = 0
@@ -109,11 +110,11 @@ def visible_gpus():
             continue
         if int(props.get("simd_count", "0")) <= 0:
             continue  # a CPU node
-        dev = f"/dev/dri/renderD{props.get('drm_render_minor', '-1')}"
+        dev = os.path.join(dri, f"renderD{props.get('drm_render_minor', '-1')}")
         if os.path.exists(dev) and os.access(dev, os.R_OK | os.W_OK):
             count += 1
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
-        v = os.environ.get(var)
+        v = env.get(var)
         if v is not None and v.strip() != "":
             count = min(count, len([x for x in v.split(",") if x.strip() != ""]))
     return count

@@ -111,3 +111,24 @@ def test_bench_gpus_without_enough_devices_fails_loudly():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "GPU(s) are visible" in r.stderr
+
+
+def test_bench_counts_gpus_without_hip(tmp_path):
+    """bench.py's spawn_ranks counts GPUs from the KFD topology (no HIP call in the launcher's parent):
+    GPU nodes only (simd_count > 0), whose render node exists, narrowed by *_VISIBLE_DEVICES."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    topo, dri = tmp_path / "nodes", tmp_path / "dri"
+    dri.mkdir()
+    for node, simd, minor in ((0, 0, None), (1, 256, 128), (2, 256, 129), (3, 256, 130)):
+        d = topo / str(node)
+        d.mkdir(parents=True)
+        lines = [f"simd_count {simd}"] + ([f"drm_render_minor {minor}"] if minor is not None else [])
+        (d / "properties").write_text("\n".join(lines) + "\n")
+    for minor in (128, 129):  # node 3's render node is not in this container
+        (dri / f"renderD{minor}").write_text("")
+    assert bench.visible_gpus(str(topo), str(dri), env={}) == 2
+    assert bench.visible_gpus(str(topo), str(dri), env={"HIP_VISIBLE_DEVICES": "0"}) == 1
+    assert bench.visible_gpus(str(topo), str(dri), env={"ROCR_VISIBLE_DEVICES": ""}) == 2
+    assert bench.visible_gpus(str(tmp_path / "none"), str(dri), env={}) is None
