@@ -47,7 +47,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD (SIMD-32),
 # at the 2.4 GHz max clock (MI355X_MICROARCH.md, wave scheduling / chip-level parameters)
 VALU_PEAK_GINST = 1024 * 2.4e9 / 2 / 1e9
-LEGS = ("f64", "adaptive", "inter", "config4", "config5", "extra", "ab")
+LEGS = ("f64", "adaptive", "f64_adaptive", "inter", "config4", "config5", "extra", "ab")
 CLAUSES_TOL = 1e-5       # the CLAUSES partitions' stated tolerance against a world-1 run
 DIGEST_REPLICAS = 4      # inter_config4: replicas per rank re-integrated by rank 0
 
@@ -392,6 +392,9 @@ def main():
         leg("f64", lambda: simple_leg("f64", dtype="f64"))
     if "adaptive" in legs and args.config == "config2":
         leg("adaptive", lambda: simple_leg("adaptive", adaptive=True))
+    if "f64_adaptive" in legs and args.config == "config2" and args.dtype == "f32":
+        # the reference CLI's defaults together (f64, adaptive steps: system.rs:111-139)
+        leg("f64_adaptive", lambda: simple_leg("f64_adaptive", dtype="f64", adaptive=True))
 
     def inter_leg():  # simulate_inter (STOP_ANY): multi-step launches with replay at the stop step
         ri = run_batch(B, False, stop=ODESAT_STOP_ANY)

@@ -71,7 +71,8 @@ struct odesat_solver {
     int solo_nl = 64, solo_cpl = 1, solo_vpl = 1;  // k_solo: lanes per replica, clause / variable slots per lane
     int wv_tw = 1;              // k_wave: waves per replica, fixed steps
     int wv_tw_ada = 1;          // ... adaptive steps (four barriers per step instead of two: at most 4)
-    bool res_ada = false; // adaptive steps fit in LDS too (else they run FUSED on the same layout)
+    bool res_ada = false; // adaptive steps run k_resident (else FUSED on the same layout)
+    bool res_vfg = false; // ... with the full-step voltage clone in HBM (v and dv fill the LDS)
     int res_ntiles = 0;
     int32_t *res_tc = nullptr, *cmap = nullptr;
     int4 *res_cl4 = nullptr;  // [m] literals of internal clause k (3-SAT)
@@ -730,14 +731,14 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
     return ODESAT_OK;
 }
 
-template <typename T, int R, bool ADA, bool K3, int NTHR = ResShape<R>::NTH>
+template <typename T, int R, bool ADA, bool K3, int NTHR = ResShape<R>::NTH, bool VFG = false>
 int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
-    const size_t lds = res_lds_bytes(s->n, R, sizeof(T), ADA);
-    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR>),
+    const size_t lds = res_lds_bytes(s->n, R, sizeof(T), ADA && !VFG);
+    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR, VFG>),
                                    (int)RES_LDS_MAX));
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR>), dim3(s->G), dim3(NTHR), lds, s->stream, a);
+        hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR, VFG>), dim3(s->G), dim3(NTHR), lds, s->stream, a);
     }
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
@@ -851,6 +852,7 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
     a.par = s->par;
     a.cf = (T *)s->cf;
     a.ch = (T *)s->ch;
+    a.vf = (T *)s->vf;
     a.dtr = (T *)s->dtr;
     a.act = s->act;
     a.sat_step = s->sat_step;
@@ -867,6 +869,13 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
     a.xl_max = (T)1e4 * (T)s->m;  // system.rs:95
     a.tol = tol;
     const bool k3 = s->uniform_k == 3;
+    if (adaptive && s->res_vfg) {  // R = 1: the full-step clone in HBM
+        if (s->res_narrow)
+            return k3 ? launch_resident_k<T, 1, true, true, RES_NARROW, true>(s, a)
+                      : launch_resident_k<T, 1, true, false, RES_NARROW, true>(s, a);
+        return k3 ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true>(s, a)
+                  : launch_resident_k<T, 1, true, false, ResShape<1>::NTH, true>(s, a);
+    }
     if (s->res_narrow) {
         if (adaptive)
             return k3 ? launch_resident_k<T, 1, true, true, RES_NARROW>(s, a)
@@ -1359,6 +1368,14 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
         s->res_R = res_r;
         s->res_ada = res_fits(n, res_r, s->tsize, true);
+        // adaptive steps whose clone of v does not fit beside v and dv (f64 at n > 6.7 k, the CLI's
+        // default precision and mode on config 2): k_resident with the clone in HBM instead of FUSED
+        // on the one-replica layout.  ODESAT_RES_VFG=0 keeps FUSED.
+        if (!s->res_ada && res_r == 1 && !s->res_wave) {
+            s->res_vfg = true;
+            if (const char *ev = std::getenv("ODESAT_RES_VFG")) s->res_vfg = std::atoi(ev) != 0;
+            s->res_ada = s->res_vfg;
+        }
         s->res_ntiles = (int)tiles.size() - 1;
         s->alg = ODESAT_ALG_RESIDENT;
         if (s->res_wave) {  // k_wave: variable-major term positions, incidences sorted by (clause, literal)

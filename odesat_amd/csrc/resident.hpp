@@ -38,6 +38,7 @@ template <typename T> struct RArgs {
     T *v0, *v1, *c0, *c1;              // state buffers, group layout with W == R
     uint8_t *par;                      // flipped by an out-of-place launch
     T *cf, *ch;                        // adaptive scratch memories (full step, first half)
+    T *vf;                             // adaptive full-step voltages in HBM (VFG: LDS holds only v and dv)
     T *dtr;
     uint8_t *act;
     int64_t *sat_step, *steps_done;
@@ -331,8 +332,11 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
 
 // NTHR threads per workgroup: ResShape<R>::NTH, or one wave (RES_NARROW) for instances whose tile
 // chains are deep and narrow (a few dozen clauses per tile): one replica per wave, no idle waves.
+// VFG (adaptive steps whose full-step voltage clone does not fit next to v and dv: f64 at n > 6.7 k):
+// the clone lives in HBM (a.vf, the replica's own n words), written and read back by the same thread
+// in the two variable phases of a step -- 2 n words of traffic per replica-step on top of the memories.
 constexpr int RES_NARROW = 64;
-template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR>
+template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR, bool VFG = false>
 __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char res_smem[];
     using U = typename Bits<T>::U;
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     const size_t nR = (size_t)a.n * R;
     x.vL = reinterpret_cast<T *>(res_smem);
     x.dvL = x.vL + nR;
-    x.vfL = x.dvL + nR;
+    x.vfL = VFG ? a.vf + (size_t)blockIdx.x * nR : x.dvL + nR;
     const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;  // uniform: SGPR bases
     const bool oop = !ADAPTIVE && a.oop;
     T *V = (p ? a.v1 : a.v0) + (size_t)g * nR;

@@ -476,10 +476,11 @@ def test_default_layout_is_resident_for_config2():
     cp, v_, n_ = wl.formula_arrays(var, neg)
     f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
     # f32: the whole replica state fits on one CU (ONCHIP); f64: v and dv (160,000 B) fit in LDS
-    # (RESIDENT; adaptive steps then run FUSED)
+    # (RESIDENT; adaptive steps keep their full-step clone in HBM)
     for prec, alg in (("f32", _lib.ODESAT_ALG_ONCHIP), ("f64", _lib.ODESAT_ALG_RESIDENT)):
         with Solver(f, 1024, prec) as s:
             assert s.algorithm == alg and s.group_width == 1
+            assert s.step_kernel(True) == ("k_onchip" if prec == "f32" else "k_resident")
 
 
 def test_frozen_replicas_keep_state_across_buffer_flips():
@@ -591,6 +592,39 @@ def test_onchip_adaptive_matches_resident_and_oracle(stop, monkeypatch):
     t, _, _, h, _ = o.simulate(ov, oxs, oxl, tol=np.float32(1e-3), dt=None, steps=int(r1["steps_done"][0]),
                                zeta=np.float32(0.001))
     assert t == r1["steps_done"][0] and same(np.float32(h), np.float32(r1["dt"][0]))
+    assert same(s1[0][0], ov) and same(s1[1][0], oxs) and same(s1[2][0], oxl)
+
+
+@pytest.mark.parametrize("narrow", ["0", "1"])
+@pytest.mark.parametrize("stop", ["each", "any", "none"])
+def test_resident_adaptive_clone_in_hbm_matches_fused_and_oracle(stop, narrow, monkeypatch):
+    """f64 at n = 7000: v and dv fill 112 KB of LDS and the full-step clone (56 KB more) does not
+    fit, so adaptive steps run k_resident with the clone in HBM (VFG) instead of FUSED on the same
+    one-replica layout.  VFG == FUSED (ODESAT_RES_VFG=0) bit for bit on every stop policy, with
+    full-width and one-wave tiles, per-replica dt included; replica 0 == the oracle's f64 simulate
+    (system.rs:111-139)."""
+    monkeypatch.setenv("ODESAT_RES_NARROW", narrow)
+    f, (cp, v_, n_) = _instance(7000, 29400, 11)
+    pol = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[stop]
+    B, K = 5, 30
+    out = []
+    for vfg in ("1", "0"):
+        monkeypatch.setenv("ODESAT_RES_VFG", vfg)
+        with Solver(f, B, "f64") as s:
+            assert s.step_kernel(True) == ("k_resident" if vfg == "1" else "k_step")
+            s.init_state(3)
+            r = s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=K, stop=pol, poll_interval=10)
+            out.append((r, s.get_state()))
+    (r1, s1), (r2, s2) = out
+    assert np.array_equal(r1["first_sat_step"], r2["first_sat_step"]) and np.array_equal(r1["steps_done"], r2["steps_done"])
+    assert same(r1["dt"], r2["dt"])
+    for x, y in zip(s1, s2):
+        assert same(x, y)
+    o = Oracle(cp, v_, n_, 7000, "f64")
+    ov = init_voltages(3, 0, 1, 7000)[0]
+    oxs, oxl = o.init_short_term_memory(), np.ones(29400)
+    t, _, _, h, _ = o.simulate(ov, oxs, oxl, tol=1e-3, dt=None, steps=int(r1["steps_done"][0]), zeta=0.001)
+    assert t == r1["steps_done"][0] and same(h, r1["dt"][0])
     assert same(s1[0][0], ov) and same(s1[1][0], oxs) and same(s1[2][0], oxl)
 
 
