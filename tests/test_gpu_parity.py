@@ -634,8 +634,10 @@ def test_wave_workgroup_widths(monkeypatch, n, m, prec, wave_env, wpw, team):
     """k_wave with 2 (config 3 in f64) and 1 (a larger instance, forced) replicas per workgroup
     equals FUSED bit for bit, fixed and adaptive -- with the automatic team (8 and 16 waves per
     replica) and with teams of 1 and 2 waves; and k_solo (one replica per workgroup, 4 clause slots
-    per lane at m = 2520) on the same formulas."""
+    per lane at m = 2520 with 640 lanes: the default 512 would need 5) on the same formulas."""
     monkeypatch.setenv("ODESAT_SOLO", "1" if team == "solo" else "0")
+    if team == "solo":
+        monkeypatch.setenv("ODESAT_SOLO_LANES", "640")
     if team not in (None, "solo"):
         monkeypatch.setenv("ODESAT_WAVE_TEAM", team)
     from odesat_amd import _lib
