@@ -17,8 +17,9 @@
 // Exactness of the short arithmetic (the host launches this kernel only on "in-range" states:
 // v in [-1, 1], xs in [-1, 1], xl in [1, 1e30], |zeta| <= 1e6 -- every state after one step is, by
 // the clamps of system.rs:94-96; otherwise the first step of the call runs RESIDENT):
-//   * vals are finite and non-NaN, so the strict-< min / second-min scan of :43-57 is exactly
-//     min3 / med3 (ties give second = min, as the scan does);
+//   * vals are finite and non-NaN, so the strict-< min / second-min scan of :43-57 gives the
+//     smallest and the second smallest value (ties give second = min), and the value literal j's
+//     term selects is the min of the other two literals' values (see Front);
 //   * q * v with q = +-1 is a sign flip (v ^ signmask), and tt * (0.5 q sel) = +-((0.5 tt) sel)
 //     (a product by 0.5 or by +-1 is exact; |tt| >= 1e-3 and sel >= 2^-24 or 0, so nothing is
 //     subnormal);
@@ -118,9 +119,13 @@ __device__ __forceinline__ void gather(const Slot &S, Gath &G) {
 //   the clamps are med3 (finite arguments: the host requires a finite dt).
 // Scalings by 0.5 / 2 / 2.5 / +-1 are exact here (no subnormals: |A| >= 0.02, |mn - c| >= 2^-26 or 0,
 // |xl xs sel| >= 6e-11 or 0).
-struct Front {  // first half: literal values and their min / second min
+//   the term of literal j selects (val_j != mn ? mn : sec) (:64-70), which for finite values is
+//   exactly the min of the OTHER two literal values: the min when some other literal attains it,
+//   the second smallest (the scan's `sec`, ties included) when j does -- so sel_j = min(val_k, val_l)
+//   needs no compare and no select.
+struct Front {  // first half: the min (:49-55) and each literal's selected value
     uint32_t a0, a1, a2, hi;
-    float val0, val1, val2, mn, sec;
+    float sel0, sel1, sel2, mn;
 };
 
 __device__ __forceinline__ void front(const Gath &G, Front &F) {
@@ -129,11 +134,13 @@ __device__ __forceinline__ void front(const Gath &G, Front &F) {
     F.a2 = G.a2;
     F.hi = G.hi;
     const uint32_t s0 = G.hi & 0x80000000u, s1 = (G.hi << 1) & 0x80000000u, s2 = (G.hi << 2) & 0x80000000u;
-    F.val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
-    F.val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
-    F.val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
-    F.mn = fminf(fminf(F.val0, F.val1), F.val2);                  // min (:49-55)
-    F.sec = __builtin_amdgcn_fmed3f(F.val0, F.val1, F.val2);       // second min, ties -> min
+    const float val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
+    const float val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
+    const float val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
+    F.sel0 = fminf(val1, val2);
+    F.sel1 = fminf(val0, val2);
+    F.sel2 = fminf(val0, val1);
+    F.mn = fminf(F.sel2, val2);  // min (:49-55)
 }
 
 // Second half: the three dv terms into Q, the sat fold and the memory update in place
@@ -144,13 +151,12 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
     const float mn = F.mn;
     const float xs = mem.x, xl = mem.y;
     const float tt = xl * xs;
-    const float tm = tt * mn, ts = tt * F.sec;
     Q.a0 = F.a0;
     Q.a1 = F.a1;
     Q.a2 = F.a2;
-    Q.d0 = __uint_as_float(__float_as_uint(F.val0 != mn ? tm : ts) ^ s0);  // 2 xl xs G (:64-70, :80)
-    Q.d1 = __uint_as_float(__float_as_uint(F.val1 != mn ? tm : ts) ^ s1);
-    Q.d2 = __uint_as_float(__float_as_uint(F.val2 != mn ? tm : ts) ^ s2);
+    Q.d0 = __uint_as_float(__float_as_uint(tt * F.sel0) ^ s0);  // 2 xl xs G (:64-70, :80)
+    Q.d1 = __uint_as_float(__float_as_uint(tt * F.sel1) ^ s1);
+    Q.d2 = __uint_as_float(__float_as_uint(tt * F.sel2) ^ s2);
     cmax = max(cmax, __float_as_uint(mn));  // :88 -- unsat iff max mn >= 0.5
     asm volatile("" : "+v"(cmax));          // fold now: deferred, it would keep every tile's mn live
     const float dxs2 = (20.0f * (xs + 0.001f)) * (mn - 0.5f);  // 2 dxs (:84)
@@ -294,9 +300,9 @@ struct GathA {  // a clause's gathered inputs: addresses, sign word, voltages fr
     float v0, v1, v2, y0, y1, y2;
 };
 
-struct FrontA {  // literal values at S and their min / second min; the voltages at y (pass 2's use)
+struct FrontA {  // the min at S and each literal's selected value (see Front); the voltages at y (pass 2's use)
     uint32_t a0, a1, a2, hi;
-    float val0, val1, val2, mn, sec, y0, y1, y2;
+    float sel0, sel1, sel2, mn, y0, y1, y2;
 };
 
 __device__ __forceinline__ void gatherA(const Slot &S, GathA &G, uint32_t sb) {
@@ -318,11 +324,13 @@ __device__ __forceinline__ void frontA(const GathA &G, FrontA &F) {
     F.a2 = G.a2;
     F.hi = G.hi;
     const uint32_t s0 = G.hi & 0x80000000u, s1 = (G.hi << 1) & 0x80000000u, s2 = (G.hi << 2) & 0x80000000u;
-    F.val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
-    F.val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
-    F.val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
-    F.mn = fminf(fminf(F.val0, F.val1), F.val2);
-    F.sec = __builtin_amdgcn_fmed3f(F.val0, F.val1, F.val2);
+    const float val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
+    const float val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
+    const float val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
+    F.sel0 = fminf(val1, val2);
+    F.sel1 = fminf(val0, val2);
+    F.sel2 = fminf(val0, val1);
+    F.mn = fminf(F.sel2, val2);
     F.y0 = G.y0;
     F.y1 = G.y1;
     F.y2 = G.y2;
@@ -350,13 +358,12 @@ __device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &me
     // the pass's RHS: at y (pass 1) or at the half step (pass 2)
     const float mn = F.mn;
     const float tt = xl_t * xs_t;
-    const float tm = tt * mn, ts = tt * F.sec;
     Q.a0 = F.a0;
     Q.a1 = F.a1;
     Q.a2 = F.a2;
-    Q.d0 = __uint_as_float(__float_as_uint(F.val0 != mn ? tm : ts) ^ s0);  // 2 xl xs G (:64-70, :80)
-    Q.d1 = __uint_as_float(__float_as_uint(F.val1 != mn ? tm : ts) ^ s1);
-    Q.d2 = __uint_as_float(__float_as_uint(F.val2 != mn ? tm : ts) ^ s2);
+    Q.d0 = __uint_as_float(__float_as_uint(tt * F.sel0) ^ s0);  // 2 xl xs G (:64-70, :80)
+    Q.d1 = __uint_as_float(__float_as_uint(tt * F.sel1) ^ s1);
+    Q.d2 = __uint_as_float(__float_as_uint(tt * F.sel2) ^ s2);
     cmax = max(cmax, __float_as_uint(mn));  // :88 (pass 1)
     asm volatile("" : "+v"(cmax));
     if (p2) {  // second half step (:130) and its max_error terms (:132)
