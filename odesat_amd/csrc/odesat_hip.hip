@@ -69,6 +69,7 @@ struct odesat_solver {
     int wv_wpw = 1;             // k_wave: replicas per workgroup sharing the LDS topology
     bool solo = false;          // k_solo (wave.hpp) instead of k_wave: one replica per workgroup, lanes' slots in registers
     int solo_nl = 64, solo_cpl = 1, solo_vpl = 1;  // k_solo: lanes per replica, clause / variable slots per lane
+    bool solo_fast = true;      // k_solo's short arithmetic on in-range states (ODESAT_SOLO_FAST=0: the general form)
     int wv_tw = 1;              // k_wave: waves per replica, fixed steps
     int wv_tw_ada = 1;          // ... adaptive steps (four barriers per step instead of two: at most 4)
     bool res_ada = false; // adaptive steps run k_resident (else FUSED on the same layout)
@@ -758,12 +759,13 @@ template <typename T, bool ADA, int WPW, int TW> int launch_wave_k(odesat_solver
     return ODESAT_OK;
 }
 
-template <typename T, bool ADA, int CPL, int VPL> int launch_solo_k(odesat_solver *s, WArgs<T> a) {
+template <typename T, bool ADA, int CPL, int VPL, bool FAST> int launch_solo_k(odesat_solver *s, WArgs<T> a) {
     const size_t lds = (size_t)(s->n + s->L) * sizeof(T);
-    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_solo<T, ADA, CPL, VPL>), (int)RES_LDS_MAX));
+    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_solo<T, ADA, CPL, VPL, FAST>), (int)RES_LDS_MAX));
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_solo<T, ADA, CPL, VPL>), dim3((unsigned)s->G), dim3((unsigned)s->solo_nl), lds, s->stream, a);
+        hipLaunchKernelGGL((k_solo<T, ADA, CPL, VPL, FAST>), dim3((unsigned)s->G), dim3((unsigned)s->solo_nl), lds,
+                           s->stream, a);
     }
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
@@ -771,7 +773,7 @@ template <typename T, bool ADA, int CPL, int VPL> int launch_solo_k(odesat_solve
 
 template <typename T>
 int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
-                int stop_mode, bool oop) {
+                int stop_mode, bool oop, bool fast) {
     WArgs<T> a{};
     a.oop = oop ? 1 : 0;
     a.rec4 = s->wv_rec4;
@@ -800,7 +802,9 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     if (s->solo) {
         auto so = [&](auto cc, auto vv) -> int {
             constexpr int CPL = decltype(cc)::value, VPL = decltype(vv)::value;
-            return adaptive ? launch_solo_k<T, true, CPL, VPL>(s, a) : launch_solo_k<T, false, CPL, VPL>(s, a);
+            if (fast && s->solo_fast)
+                return adaptive ? launch_solo_k<T, true, CPL, VPL, true>(s, a) : launch_solo_k<T, false, CPL, VPL, true>(s, a);
+            return adaptive ? launch_solo_k<T, true, CPL, VPL, false>(s, a) : launch_solo_k<T, false, CPL, VPL, false>(s, a);
         };
         switch (s->solo_cpl * 10 + s->solo_vpl) {
             case 11: return so(IC<1>{}, IC<1>{});
@@ -836,8 +840,8 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
 
 template <typename T>
 int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
-                    int stop_mode, bool oop) {
-    if (s->res_wave) return launch_wave<T>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode, oop);
+                    int stop_mode, bool oop, bool fast) {
+    if (s->res_wave) return launch_wave<T>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode, oop, fast);
     if (oop && adaptive) return fail(ODESAT_EINVAL, "out-of-place RESIDENT launches are fixed-step only");
     RArgs<T> a{};
     a.oop = oop ? 1 : 0;
@@ -935,10 +939,13 @@ int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zet
     return ODESAT_OK;
 }
 
+// fast: every replica's state is in range (onchip.hip's header) and zeta and dt are finite (k_solo's
+// short arithmetic, wave.hpp)
 int dispatch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
-                      int stop_mode, bool oop) {
-    return s->dtype == ODESAT_F64 ? launch_resident<double>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode, oop)
-                                  : launch_resident<float>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode, oop);
+                      int stop_mode, bool oop, bool fast) {
+    return s->dtype == ODESAT_F64
+               ? launch_resident<double>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode, oop, fast)
+               : launch_resident<float>(s, step0, nsteps, adaptive, dt, zeta, tol, stop_mode, oop, fast);
 }
 
 template <typename T> int deriv_t(odesat_solver *s, double zeta) {
@@ -1416,6 +1423,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             s->solo_nl = (int)nl;
             s->solo_cpl = cpl <= 1 ? 1 : (cpl <= 2 ? 2 : 4);
             s->solo_vpl = (int)vpl;
+            if (const char *ev = std::getenv("ODESAT_SOLO_FAST")) s->solo_fast = std::atoi(ev) != 0;
         }
         if ((rc = onchip_setup(s, tiles, wst, lits))) return bail(rc);
         if (s->oc_tr > 0) s->alg = ODESAT_ALG_ONCHIP;
@@ -1708,10 +1716,12 @@ static int simulate_resident(odesat_solver *s, const odesat_params *p, bool adap
     const int per_launch = any && !replay ? 1 : poll;
     const int64_t base = s->t_base;
     if (replay && (rc = ensure_snapshot(s))) return rc;
+    const bool finite = std::fabs(zeta) <= 1e6 && adt >= 1e-30 && adt <= 1e30;  // (k_solo's short arithmetic)
     auto launch = [&](int64_t t0, int k, bool oop) -> int {
         const bool use_oc = oc && (t0 > 0 || s->in_range);
         return use_oc ? launch_onchip(s, (int)(base + t0), k, p->dt, zeta, p->stop, oop, adaptive, tol)
-                      : dispatch_resident(s, (int)(base + t0), k, adaptive, p->dt, zeta, tol, p->stop, oop);
+                      : dispatch_resident(s, (int)(base + t0), k, adaptive, p->dt, zeta, tol, p->stop, oop,
+                                          finite && (t0 > 0 || s->in_range));
     };
     int64_t t = 0, next_poll = poll;
     while (t < p->max_steps) {
