@@ -760,11 +760,17 @@ template <typename T, bool ADA, int WPW, int TW> int launch_wave_k(odesat_solver
 }
 
 template <typename T, bool ADA, int CPL, int VPL, bool FAST> int launch_solo_k(odesat_solver *s, WArgs<T> a) {
-    const size_t lds = (size_t)(s->n + s->L) * sizeof(T);
-    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_solo<T, ADA, CPL, VPL, FAST>), (int)RES_LDS_MAX));
-    {
+    if constexpr (FAST) {  // k_solo_fast: in-range states
+        const size_t lds = solo_fast_elems(s->n, s->L, sizeof(T)) * sizeof(T);
+        HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_solo_fast<T, ADA, CPL, VPL>), (int)RES_LDS_MAX));
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_solo<T, ADA, CPL, VPL, FAST>), dim3((unsigned)s->G), dim3((unsigned)s->solo_nl), lds,
+        hipLaunchKernelGGL((k_solo_fast<T, ADA, CPL, VPL>), dim3((unsigned)s->G), dim3((unsigned)s->solo_nl), lds,
+                           s->stream, a);
+    } else {
+        const size_t lds = (size_t)(s->n + s->L) * sizeof(T);
+        HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_solo<T, ADA, CPL, VPL, false>), (int)RES_LDS_MAX));
+        Timed tm(s, 0);
+        hipLaunchKernelGGL((k_solo<T, ADA, CPL, VPL, false>), dim3((unsigned)s->G), dim3((unsigned)s->solo_nl), lds,
                            s->stream, a);
     }
     HIP_TRY(hipGetLastError());
@@ -1423,7 +1429,9 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             s->solo_nl = (int)nl;
             s->solo_cpl = cpl <= 1 ? 1 : (cpl <= 2 ? 2 : 4);
             s->solo_vpl = (int)vpl;
-            if (const char *ev = std::getenv("ODESAT_SOLO_FAST")) s->solo_fast = std::atoi(ev) != 0;
+            // k_solo_fast's padded term blocks must fit as well
+            s->solo_fast = solo_fast_elems(n, L, s->tsize) * s->tsize <= RES_LDS_MAX;
+            if (const char *ev = std::getenv("ODESAT_SOLO_FAST")) s->solo_fast = s->solo_fast && std::atoi(ev) != 0;
         }
         if ((rc = onchip_setup(s, tiles, wst, lits))) return bail(rc);
         if (s->oc_tr > 0) s->alg = ODESAT_ALG_ONCHIP;

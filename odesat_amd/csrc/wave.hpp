@@ -423,6 +423,31 @@ __device__ __forceinline__ bool solo_fast(const T (&v)[3], const uint32_t (&sg)[
     return PK != W_ADA2 && !(mn < (T)0.5);  // :88 (unsat)
 }
 
+// Diagnostic build only (-DSOLO_STAMPS, scripts/build_variant.sh ... odesat_hip): per wave, s_memtime
+// stamps split each fixed step into the clause pass, the first barrier, the fold and the closing
+// barrier; sums in g_solo_stamps (read by odesat_solo_stamps).  Each stamp drains the wave's LDS
+// operations: read the SHARES.
+#ifdef SOLO_STAMPS
+__device__ unsigned long long g_solo_stamps[16 * 8];
+__device__ __forceinline__ uint64_t solo_memtime() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define SOLO_STAMP(i)                          \
+    do {                                       \
+        const uint64_t t_ = solo_memtime();    \
+        st_[i] += t_ - st_last;                \
+        st_last = t_;                          \
+    } while (0)
+#else
+#define SOLO_STAMP(i) \
+    do {              \
+    } while (0)
+#endif
+
 template <typename T, bool ADAPTIVE, int CPL, int VPL, bool FAST>
 __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char wave_smem[];
@@ -516,6 +541,10 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
     };
     // FAST: the terms are twice the reference's, so each h below is halved (exact)
     constexpr T SC = FAST ? (T)0.5 : (T)1.0;
+#ifdef SOLO_STAMPS
+    uint64_t st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_last = solo_memtime();
+#endif
     for (int k = 0; k < a.nsteps; ++k) {
         const int step = a.step0 + k;
         const T h = dtr;
@@ -523,7 +552,9 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
         bool uns, go = false;
         if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
             vote(clauses(std::integral_constant<int, W_FIXED>{}, h, e), k);
+            SOLO_STAMP(0);
             __syncthreads();  // the terms (and the votes) before the fold
+            SOLO_STAMP(1);
             uns = votes(k);
             const T hv = SC * h;
 #pragma unroll
@@ -532,6 +563,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
                     vr[j] = dmin(dmax(vr[j] + hv * solo_fold(tL, vs[j], vd[j], a.L), (T)-1.0), (T)1.0);  // :96
                     vL[l + j * NL] = vr[j];
                 }
+            SOLO_STAMP(2);
         } else {  // euler_step (:111-139)
             vote(clauses(std::integral_constant<int, W_ADA1>{}, h, e), k);
             __syncthreads();
@@ -575,7 +607,9 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
             if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                            // simulate() breaks (:193)
             if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
         }
+        SOLO_STAMP(3);
         __syncthreads();  // the voltages before the next step's gathers (and the error words)
+        SOLO_STAMP(4);
         if (ADAPTIVE && go) {  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
             U eb = errW[0];
             for (int w2 = 1; w2 < TW; ++w2) eb = errW[w2] > eb ? errW[w2] : eb;
@@ -583,6 +617,10 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
         }
         if (!act) break;  // uniform
     }
+#ifdef SOLO_STAMPS
+    if ((l & 63) == 0 && g == 0)
+        for (int i = 0; i < 8; ++i) g_solo_stamps[(l >> 6) * 8 + i] = st_[i];
+#endif
     const bool q = a.oop ? !p : p;
     T *Vo = (q ? a.v1 : a.v0) + (size_t)g * a.n;
     T *CMo = (q ? a.c1 : a.c0) + (size_t)g * a.m * 2;
@@ -606,4 +644,293 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_solo_fast -- k_solo on in-range states (the host's `fast` launches: onchip.hip's range, finite
+// zeta and dt): solo_fast's exact short arithmetic, and a step laid out for latency --
+//   * the terms of variable i sit in a padded block of SOLO_DPAD slots (16-byte aligned, the slots
+//     past its degree stay +0), so its fold is SOLO_DPAD / (16 / sizeof(T)) vector reads from one
+//     address and a chain of adds whose length is the wave's largest degree (a uniform bound; the
+//     added +0 terms change nothing, since dv starts at +0 and is never -0); terms of rank >= SOLO_DPAD
+//     go to an overflow area at n SOLO_DPAD + their variable-major position and are folded after;
+//   * the memory updates, which nothing in the step waits for, run after the barrier that follows
+//     the term stores, under the fold's LDS reads (adaptive: the first pass's clones and half step
+//     right after pass 1, the second half step after pass 2).
+// Bit-identical to k_solo, k_wave and the oracle (tests/test_gpu_parity.py, tests/test_gpu_fuzz.py).
+// ------------------------------------------------------------------------------------------------
+constexpr int SOLO_DPAD = 8;
+
+// LDS elements of k_solo_fast: v (rounded up to 16 bytes), the padded term blocks, the overflow area
+inline size_t solo_fast_elems(int64_t n, int64_t L, size_t tsize) {
+    const int64_t per16 = 16 / (int64_t)tsize;
+    return (size_t)((n + per16 - 1) / per16 * per16 + n * SOLO_DPAD + L);
+}
+
+// the terms (2 x the reference's) of one clause at voltages v, memories product tt; returns mn
+template <typename T>
+__device__ __forceinline__ T solo_terms(const T (&v)[3], const uint32_t (&sg)[3], T tt, T (&d)[3]) {
+    const T one = (T)1.0;
+    const T val0 = one - sflip(v[0], sg[0]), val1 = one - sflip(v[1], sg[1]), val2 = one - sflip(v[2], sg[2]);  // :47
+    const T sel0 = dmin(val1, val2), sel1 = dmin(val0, val2), sel2 = dmin(val0, val1);
+    d[0] = sflip(tt * sel0, sg[0]);  // 2 xl xs G (:64-70, :80)
+    d[1] = sflip(tt * sel1, sg[1]);
+    d[2] = sflip(tt * sel2, sg[2]);
+    return dmin(sel2, val2);  // :49-57
+}
+
+// one memory step of length hx from (xs, xl) with the clause's mn: xs + hx/2 * (2 dxs), xl + hx * dxl
+// (:84-85, :94-95; hx2 = hx / 2)
+template <typename T>
+__device__ __forceinline__ void solo_mem(T xs, T xl, T mn, T hx2, T hx, T xl_max, T &xs_o, T &xl_o) {
+    const T eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
+    const T dxs = ((T)20.0 * (xs + eps)) * (mn - (T)0.5);  // 2 dxs
+    const T dxl = (T)2.5 * (mn - (T)0.1);
+    xs_o = dmin(dmax(xs + hx2 * dxs, eps), xs_hi);
+    xl_o = dmin(dmax(xl + hx * dxl, (T)1.0), xl_max);
+}
+
+template <typename T, bool ADAPTIVE, int CPL, int VPL>
+__global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char wave_smem[];
+    using U = typename Bits<T>::U;
+    constexpr int PER16 = 16 / (int)sizeof(T);
+    typedef T TV __attribute__((ext_vector_type(PER16)));  // 16 bytes of terms
+    struct Terms {
+        TV t[VPL][SOLO_DPAD / PER16];
+    };
+    __shared__ U errW[SOLO_MAX_NL / 64];
+    __shared__ __attribute__((aligned(16))) int voteW[2][SOLO_MAX_NL / 64];
+    const int NL = (int)blockDim.x, l = (int)threadIdx.x, TW = NL / 64;
+    const int g = blockIdx.x;
+    if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
+    if (g >= a.G || a.act[g] == 0) return;                              // uniform per workgroup
+    const int n = a.n;
+    T *vL = reinterpret_cast<T *>(wave_smem);
+    T *pL = vL + (n + PER16 - 1) / PER16 * PER16;  // padded blocks, then the overflow area
+    for (int i = l; i < n * SOLO_DPAD; i += NL) pL[i] = (T)0.0;
+    const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
+    const T *V = (p ? a.v1 : a.v0) + (size_t)g * n;
+    const T *CM = (p ? a.c1 : a.c0) + (size_t)g * a.m * 2;
+    const int mlast = a.m - 1, nlast = n - 1;
+    int va[CPL][3], tp[CPL][3];  // voltage index and term slot of each literal
+    uint32_t sg[CPL][3];
+    T xs[CPL], xl[CPL], mk[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = min(l + k * NL, mlast);
+        const int4 r4 = a.rec4[c];
+        const int lit[3] = {r4.x & 0xffff, r4.y & 0xffff, r4.z & 0xffff};
+        const int pos[3] = {(int)((uint32_t)r4.x >> 16), (int)((uint32_t)r4.y >> 16), (int)((uint32_t)r4.z >> 16)};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int v = lit[j] >> 1, rank = pos[j] - a.vst[v];
+            va[k][j] = v;
+            tp[k][j] = rank < SOLO_DPAD ? v * SOLO_DPAD + rank : n * SOLO_DPAD + pos[j];
+            sg[k][j] = (lit[j] & 1) ? 0x80000000u : 0u;
+        }
+        xs[k] = CM[2 * c];
+        xl[k] = CM[2 * c + 1];
+        mk[k] = (T)0.0;
+    }
+    int vs[VPL], vd[VPL], dw[VPL];  // term range start, degree, the wave's largest degree (uniform)
+    T vr[VPL], vf[VPL];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int i = l + j * NL, ii = min(i, nlast);
+        vs[j] = a.vst[ii];
+        vd[j] = i < n ? a.vst[ii + 1] - vs[j] : 0;
+        int mx = vd[j];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) mx = max(mx, __shfl_xor(mx, off, 64));
+        dw[j] = __builtin_amdgcn_readfirstlane(mx);
+        vr[j] = V[ii];
+        vf[j] = vr[j];
+        if (i < n) vL[i] = vr[j];
+    }
+    if (l < 2 * (SOLO_MAX_NL / 64)) voteW[l >> 4][l & 15] = 0;
+    __syncthreads();
+    int act = 1;
+    int64_t sat = a.sat_step[g], done = a.steps_done[g];
+    T dtr = ADAPTIVE ? a.dtr[g] : a.dt;
+    const int w = l >> 6;
+    auto vote = [&](bool u, int k) {
+        const bool wu = __any(u);
+        if ((l & 63) == 0) voteW[k & 1][w] = wu ? 1 : 0;
+    };
+    auto votes = [&](int k) {
+        const int4 *vw = reinterpret_cast<const int4 *>(voteW[k & 1]);
+        int4 r4[SOLO_MAX_NL / 256];
+#pragma unroll
+        for (int j = 0; j < SOLO_MAX_NL / 256; ++j) r4[j] = vw[j];
+        int r = 0;
+#pragma unroll
+        for (int j = 0; j < SOLO_MAX_NL / 256; ++j) r |= r4[j].x | r4[j].y | r4[j].z | r4[j].w;
+        return r != 0;
+    };
+    // the clause pass: gathers of every slot first, then each slot's terms; mn into mn_o; unsat
+    auto clauses = [&](const T (&txs)[CPL], const T (&txl)[CPL], T (&mn_o)[CPL]) -> bool {
+        T vv[CPL][3];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) vv[k][j] = vL[va[k][j]];
+        bool uns = false;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            if (l + k * NL < a.m) {
+                T d[3];
+                mn_o[k] = solo_terms<T>(vv[k], sg[k], txl[k] * txs[k], d);
+#pragma unroll
+                for (int j = 0; j < 3; ++j) pL[tp[k][j]] = d[j];
+                uns = uns || !(mn_o[k] < (T)0.5);  // :88
+            }
+        return uns;
+    };
+    // the fold of every variable slot (2 dv: the reference's left fold of the 2x terms)
+    auto fold = [&]() {  // the reads of every variable slot's padded block
+        Terms r;
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+            const TV *b = reinterpret_cast<const TV *>(pL + (size_t)min(l + j * NL, nlast) * SOLO_DPAD);
+#pragma unroll
+            for (int q = 0; q < SOLO_DPAD / PER16; ++q) r.t[j][q] = b[q];
+        }
+        return r;
+    };
+    auto fold_sum = [&](const Terms &r, T (&dv)[VPL]) {
+        const auto &t = r.t;
+#pragma unroll
+        for (int j = 0; j < VPL; ++j) {
+            T x = (T)0.0 + t[j][0][0];  // :33, the first term
+#pragma unroll
+            for (int u = 1; u < SOLO_DPAD; ++u)
+                if (u < dw[j]) x = x + t[j][u / PER16][u % PER16];  // uniform bound: slots past a degree are +0
+            if (dw[j] > SOLO_DPAD)                                  // (uniform) terms of rank >= SOLO_DPAD
+                for (int u = SOLO_DPAD; u < vd[j]; ++u) x = x + pL[n * SOLO_DPAD + vs[j] + u];
+            dv[j] = x;
+        }
+    };
+    T mn2[CPL], xsf[CPL], xlf[CPL], xsh[CPL], xlh[CPL];
+    for (int k = 0; k < a.nsteps; ++k) {
+        const int step = a.step0 + k;
+        const T h = dtr, hh = (T)0.5 * h, hq = (T)0.25 * h;
+        T e = (T)0.0;
+        bool uns, go = false;
+        if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
+            vote(clauses(xs, xl, mk), k);
+            __syncthreads();  // the terms (and the votes) before the fold
+            const Terms t = fold();
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+                if (l + c * NL < a.m) solo_mem<T>(xs[c], xl[c], mk[c], hh, h, a.xl_max, xs[c], xl[c]);
+            uns = votes(k);
+            T dv[VPL];
+            fold_sum(t, dv);
+#pragma unroll
+            for (int j = 0; j < VPL; ++j)
+                if (l + j * NL < n) {
+                    vr[j] = dmin(dmax(vr[j] + hh * dv[j], (T)-1.0), (T)1.0);  // :96 (h dv = (h/2) (2 dv))
+                    vL[l + j * NL] = vr[j];
+                }
+        } else {  // euler_step (:111-139)
+            vote(clauses(xs, xl, mk), k);  // the RHS at y, y's memories
+            __syncthreads();
+            uns = votes(k);
+            go = uns;  // an allsat replica takes no step (:122)
+            if (go) {
+                const Terms t = fold();
+#pragma unroll
+                for (int c = 0; c < CPL; ++c)
+                    if (l + c * NL < a.m) {  // the memories' full-step clone and first half step (:124-128)
+                        solo_mem<T>(xs[c], xl[c], mk[c], hh, h, a.xl_max, xsf[c], xlf[c]);
+                        solo_mem<T>(xs[c], xl[c], mk[c], hq, hh, a.xl_max, xsh[c], xlh[c]);
+                    }
+                T dv[VPL];
+                fold_sum(t, dv);
+#pragma unroll
+                for (int j = 0; j < VPL; ++j)
+                    if (l + j * NL < n) {
+                        const T v = vr[j];
+                        vf[j] = dmin(dmax(v + hh * dv[j], (T)-1.0), (T)1.0);  // full-step clone
+                        vr[j] = dmin(dmax(v + hq * dv[j], (T)-1.0), (T)1.0);  // first half step
+                        vL[l + j * NL] = vr[j];
+                    }
+            }
+            __syncthreads();  // the half step's voltages before the second pass; the terms read
+            if (go) clauses(xsh, xlh, mn2);
+            __syncthreads();  // the second pass's terms before its fold
+            if (go) {
+                const Terms t = fold();
+#pragma unroll
+                for (int c = 0; c < CPL; ++c)
+                    if (l + c * NL < a.m) {  // second half step of the memories (:130), max_error (:132)
+                        T xsn, xln;
+                        solo_mem<T>(xsh[c], xlh[c], mn2[c], hq, hh, a.xl_max, xsn, xln);
+                        e = dmax(e, dmax(dabs(xsf[c] - xsn), dabs(xlf[c] - xln)));
+                        xs[c] = xsn;
+                        xl[c] = xln;
+                    }
+                T dv[VPL];
+                fold_sum(t, dv);
+#pragma unroll
+                for (int j = 0; j < VPL; ++j)
+                    if (l + j * NL < n) {
+                        const T vn = dmin(dmax(vr[j] + hq * dv[j], (T)-1.0), (T)1.0);  // second half step
+                        e = dmax(e, dabs(vf[j] - vn));  // :101-108
+                        vr[j] = vn;
+                        vL[l + j * NL] = vn;
+                    }
+                U eb = tobits(e);  // non-negative floats order as their bits
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const U o = __shfl_xor(eb, off, 64);
+                    eb = o > eb ? o : eb;
+                }
+                if ((l & 63) == 0) errW[l >> 6] = eb;
+            }
+        }
+        done += 1;
+        if (!uns) {  // allsat: the fixed step was still taken (:148-152); adaptive took none
+            if (sat < 0) sat = step;
+            if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                            // simulate() breaks (:193)
+            if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
+        }
+        __syncthreads();  // the voltages before the next step's gathers (and the error words)
+        if (ADAPTIVE && go) {  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
+            U eb = errW[0];
+            for (int w2 = 1; w2 < TW; ++w2) eb = errW[w2] > eb ? errW[w2] : eb;
+            dtr = dmax(dmin(dtr * dsqrt((T)a.tol / frombits(eb)), (T)1e3), (T)0.0078125);
+        }
+        if (!act) break;  // uniform
+    }
+    const bool q = a.oop ? !p : p;
+    T *Vo = (q ? a.v1 : a.v0) + (size_t)g * n;
+    T *CMo = (q ? a.c1 : a.c0) + (size_t)g * a.m * 2;
+#pragma unroll
+    for (int j = 0; j < VPL; ++j)
+        if (l + j * NL < n) Vo[l + j * NL] = vr[j];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = l + k * NL;
+        if (c < a.m) {
+            CMo[2 * c] = xs[k];
+            CMo[2 * c + 1] = xl[k];
+        }
+    }
+    if (l == 0) {
+        if (a.oop) a.par[g] = (uint8_t)q;
+        a.act[g] = (uint8_t)act;
+        a.sat_step[g] = sat;
+        a.steps_done[g] = done;
+        if (ADAPTIVE) a.dtr[g] = dtr;
+    }
+}
+
 }  // namespace odk
+
+#ifdef SOLO_STAMPS
+// Diagnostic build only: the per-wave stamp sums of replica 0's last k_solo launch, 16 waves x 8.
+extern "C" int odesat_solo_stamps(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(odk::g_solo_stamps), sizeof(unsigned long long) * 128, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -1,0 +1,35 @@
+"""Diagnostic: stamp breakdown of a k_solo fixed step (needs a -DSOLO_STAMPS build, ODESAT_LIB=...).
+hard.cnf, B = 1, f64, 2000 fixed steps; prints cycles per step per segment for each wave."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    from odesat_amd import _lib, cnf
+    from odesat_amd.system import ODESAT_STOP_NONE, Solver
+    with open(os.path.join(ROOT, "tests", "golden", "hard.cnf")) as fh:
+        _, f = cnf.normalize_cnf_variables(cnf.parse_dimacs_format(fh.read()))
+    steps = 2000
+    for prec in ("f64", "f32"):
+        with Solver(f, 1, prec) as s:
+            s.init_state(42)
+            s.simulate(max_steps=steps, stop=ODESAT_STOP_NONE, poll_interval=steps, adaptive=False, dt=0.01)
+            s.synchronize()
+            buf = (ctypes.c_ulonglong * 128)()
+            assert _lib.lib().odesat_solo_stamps(buf) == 0
+            names = ["clauses", "barrier1", "fold", "book", "barrier2"]
+            for w in range(16):
+                row = [buf[w * 8 + i] / steps for i in range(5)]
+                if sum(row) == 0:
+                    continue
+                print(json.dumps({"prec": prec, "wave": w, "lanes": os.environ.get("ODESAT_SOLO_LANES"),
+                                  **{n: round(x, 1) for n, x in zip(names, row)}, "total": round(sum(row), 1)}))
+
+
+if __name__ == "__main__":
+    main()

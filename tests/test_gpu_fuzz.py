@@ -84,6 +84,9 @@ def variants(prec, uniform3, distinct):
             if lanes != "0":
                 env["ODESAT_SOLO_LANES"] = lanes
             v.append((f"solo-l{lanes}", env, _lib.ODESAT_ALG_RESIDENT))
+        # k_solo's general arithmetic (the fast kernel, k_solo_fast, is the default on in-range states)
+        v.append(("solo-general", {"ODESAT_WAVE": "1", "ODESAT_SOLO": "1", "ODESAT_SOLO_FAST": "0"},
+                  _lib.ODESAT_ALG_RESIDENT))
         if prec == "f32" and distinct:
             v.append(("onchip", {"ODESAT_WAVE": "0", "ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "0"},
                       _lib.ODESAT_ALG_ONCHIP))
@@ -161,7 +164,7 @@ def test_fuzz_every_path_matches_oracle(seed, prec):
 def test_fuzz_covered_every_path():
     """The cases above reached every kernel family: FUSED (W = 64 and 8), TWOPASS, the RESIDENT
     tile kernels (512-lane, one-wave and R = 4 tiles), k_wave with teams of 1, 2 and 4 waves, k_solo
-    with teams of 64, 128 and the default lanes, and ONCHIP."""
+    with teams of 64, 128 and the default lanes (k_solo_fast) and in its general form, and ONCHIP."""
     if not COVERED:
         pytest.skip("run together with test_fuzz_every_path_matches_oracle")
     need = [("fused", _lib.ODESAT_ALG_FUSED), ("twopass", _lib.ODESAT_ALG_TWOPASS),
@@ -170,7 +173,7 @@ def test_fuzz_covered_every_path():
             ("wave-t1", _lib.ODESAT_ALG_RESIDENT), ("wave-t2", _lib.ODESAT_ALG_RESIDENT),
             ("wave-t4", _lib.ODESAT_ALG_RESIDENT), ("onchip", _lib.ODESAT_ALG_ONCHIP),
             ("solo-l64", _lib.ODESAT_ALG_RESIDENT), ("solo-l128", _lib.ODESAT_ALG_RESIDENT),
-            ("solo-l0", _lib.ODESAT_ALG_RESIDENT)]
+            ("solo-l0", _lib.ODESAT_ALG_RESIDENT), ("solo-general", _lib.ODESAT_ALG_RESIDENT)]
     print(sorted(COVERED.items()))
     missing = [k for k in need if COVERED.get(k, 0) < 4]
     assert not missing, (missing, COVERED)
