@@ -688,6 +688,27 @@ __device__ __forceinline__ void solo_mem(T xs, T xl, T mn, T hx2, T hx, T xl_max
     xl_o = dmin(dmax(xl + hx * dxl, (T)1.0), xl_max);
 }
 
+// The max of x over the wave (all 64 lanes active), uniform: a DPP butterfly within each quad, row
+// rotations within each row of 16, then the four rows' maxima by readlane.
+template <int CTRL> __device__ __forceinline__ uint32_t max_dpp(uint32_t x) {
+    return max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+    x = max_dpp<0xB1>(x);   // quad_perm [1, 0, 3, 2]
+    x = max_dpp<0x4E>(x);   // quad_perm [2, 3, 0, 1]
+    x = max_dpp<0x124>(x);  // row_ror:4
+    x = max_dpp<0x128>(x);  // row_ror:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+    return max(max(r0, r1), max(r2, r3));
+}
+__device__ __forceinline__ uint32_t wave_max_bits(uint32_t x) { return wave_max_u32(x); }
+__device__ __forceinline__ unsigned long long wave_max_bits(unsigned long long x) {  // (high word, then low word)
+    const uint32_t hi = wave_max_u32((uint32_t)(x >> 32));
+    const uint32_t lo = wave_max_u32((uint32_t)(x >> 32) == hi ? (uint32_t)x : 0u);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 template <typename T, bool ADAPTIVE, int CPL, int VPL>
 __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char wave_smem[];
@@ -697,7 +718,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
     struct Terms {
         TV t[VPL][SOLO_DPAD / PER16];
     };
-    __shared__ U errW[SOLO_MAX_NL / 64];
+    __shared__ U errM[2];  // per step parity: the max_error bits of the step (the waves' LDS atomic max)
     __shared__ __attribute__((aligned(16))) int voteW[2][SOLO_MAX_NL / 64];
     const int NL = (int)blockDim.x, l = (int)threadIdx.x, TW = NL / 64;
     const int g = blockIdx.x;
@@ -747,6 +768,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
         if (i < n) vL[i] = vr[j];
     }
     if (l < 2 * (SOLO_MAX_NL / 64)) voteW[l >> 4][l & 15] = 0;
+    if (l < 2) errM[l] = 0;
     __syncthreads();
     int act = 1;
     int64_t sat = a.sat_step[g], done = a.steps_done[g];
@@ -879,14 +901,10 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
                         vr[j] = vn;
                         vL[l + j * NL] = vn;
                     }
-                U eb = tobits(e);  // non-negative floats order as their bits
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) {
-                    const U o = __shfl_xor(eb, off, 64);
-                    eb = o > eb ? o : eb;
-                }
-                if ((l & 63) == 0) errW[l >> 6] = eb;
+                const U eb = wave_max_bits(tobits(e));  // non-negative floats order as their bits
+                if ((l & 63) == 0) atomicMax(&errM[k & 1], eb);
             }
+            if (l == 0) errM[(k + 1) & 1] = 0;  // read at the start of step k, before this step's first barrier
         }
         done += 1;
         if (!uns) {  // allsat: the fixed step was still taken (:148-152); adaptive took none
@@ -896,9 +914,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
         }
         __syncthreads();  // the voltages before the next step's gathers (and the error words)
         if (ADAPTIVE && go) {  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
-            U eb = errW[0];
-            for (int w2 = 1; w2 < TW; ++w2) eb = errW[w2] > eb ? errW[w2] : eb;
-            dtr = dmax(dmin(dtr * dsqrt((T)a.tol / frombits(eb)), (T)1e3), (T)0.0078125);
+            dtr = dmax(dmin(dtr * dsqrt((T)a.tol / frombits(errM[k & 1])), (T)1e3), (T)0.0078125);
         }
         if (!act) break;  // uniform
     }
