@@ -832,6 +832,10 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
         }
     };
     T mn2[CPL], xsf[CPL], xlf[CPL], xsh[CPL], xlh[CPL];
+#ifdef SOLO_STAMPS
+    uint64_t st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_last = solo_memtime();
+#endif
     for (int k = 0; k < a.nsteps; ++k) {
         const int step = a.step0 + k;
         const T h = dtr, hh = (T)0.5 * h, hq = (T)0.25 * h;
@@ -855,7 +859,9 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
                 }
         } else {  // euler_step (:111-139)
             vote(clauses(xs, xl, mk), k);  // the RHS at y, y's memories
+            SOLO_STAMP(0);
             __syncthreads();
+            SOLO_STAMP(1);
             uns = votes(k);
             go = uns;  // an allsat replica takes no step (:122)
             if (go) {
@@ -877,9 +883,13 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
                         vL[l + j * NL] = vr[j];
                     }
             }
+            SOLO_STAMP(2);
             __syncthreads();  // the half step's voltages before the second pass; the terms read
+            SOLO_STAMP(3);
             if (go) clauses(xsh, xlh, mn2);
+            SOLO_STAMP(4);
             __syncthreads();  // the second pass's terms before its fold
+            SOLO_STAMP(5);
             if (go) {
                 const Terms t = fold();
 #pragma unroll
@@ -901,6 +911,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
                         vr[j] = vn;
                         vL[l + j * NL] = vn;
                     }
+                // (an LDS atomic max from every lane instead: 38 ms per criterion call against 12.6)
                 const U eb = wave_max_bits(tobits(e));  // non-negative floats order as their bits
                 if ((l & 63) == 0) atomicMax(&errM[k & 1], eb);
             }
@@ -912,12 +923,18 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
             if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                            // simulate() breaks (:193)
             if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
         }
+        if (ADAPTIVE) SOLO_STAMP(6);
         __syncthreads();  // the voltages before the next step's gathers (and the error words)
         if (ADAPTIVE && go) {  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
             dtr = dmax(dmin(dtr * dsqrt((T)a.tol / frombits(errM[k & 1])), (T)1e3), (T)0.0078125);
         }
+        if (ADAPTIVE) SOLO_STAMP(7);
         if (!act) break;  // uniform
     }
+#ifdef SOLO_STAMPS
+    if ((l & 63) == 0 && g == 0)
+        for (int i = 0; i < 8; ++i) g_solo_stamps[(l >> 6) * 8 + i] = st_[i];
+#endif
     const bool q = a.oop ? !p : p;
     T *Vo = (q ? a.v1 : a.v0) + (size_t)g * n;
     T *CMo = (q ? a.c1 : a.c0) + (size_t)g * a.m * 2;

@@ -1,12 +1,10 @@
-# A/B of k_solo builds on the criterion benches (same box, alternated): expt/libsoloold.so vs the tree.
+#!/bin/bash
+# criterion benches, the product build against expt/lib$VAR.so, alternated
 set -u
-mkdir -p gpurun_out
-: > gpurun_out/solo_ab.txt
-for rep in 1 2; do
-  for v in old new; do
-    if [ $v = old ]; then export ODESAT_LIB=$PWD/expt/libsoloold.so; else unset ODESAT_LIB; fi
-    echo "== $v" >> gpurun_out/solo_ab.txt
-    timeout -k 10 120 python -u scripts/bench_criterion.py --no-cpu --calls 10 2>/dev/null >> gpurun_out/solo_ab.txt || { echo "crit $v failed"; exit 1; }
+cd "$(dirname "$0")/.."
+for r in 1 2; do
+  for lib in prod ${VARS:-}; do
+    if [ $lib = prod ]; then L=""; else L="ODESAT_LIB=$PWD/expt/lib$lib.so"; fi
+    echo "== $lib"; env $L timeout -k 10 300 python -u scripts/bench_criterion.py --no-cpu --calls 3 2>/dev/null || exit 1
   done
 done
-cat gpurun_out/solo_ab.txt

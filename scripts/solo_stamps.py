@@ -1,4 +1,4 @@
-"""Diagnostic: stamp breakdown of a k_solo fixed step (needs a -DSOLO_STAMPS build, ODESAT_LIB=...).
+"""Diagnostic: stamp breakdown of a k_solo_fast fixed / adaptive step (needs a -DSOLO_STAMPS build, ODESAT_LIB=...).
 hard.cnf, B = 1, f64, 2000 fixed steps; prints cycles per step per segment for each wave."""
 import ctypes
 import json
@@ -15,19 +15,20 @@ def main():
     with open(os.path.join(ROOT, "tests", "golden", "hard.cnf")) as fh:
         _, f = cnf.normalize_cnf_variables(cnf.parse_dimacs_format(fh.read()))
     steps = 2000
-    for prec in ("f64", "f32"):
+    for prec, adaptive in (("f64", False), ("f64", True)):
         with Solver(f, 1, prec) as s:
             s.init_state(42)
-            s.simulate(max_steps=steps, stop=ODESAT_STOP_NONE, poll_interval=steps, adaptive=False, dt=0.01)
+            s.simulate(max_steps=steps, stop=ODESAT_STOP_NONE, poll_interval=steps, adaptive=adaptive, dt=0.01, tol=0.01)
             s.synchronize()
             buf = (ctypes.c_ulonglong * 128)()
             assert _lib.lib().odesat_solo_stamps(buf) == 0
-            names = ["clauses", "barrier1", "fold", "book", "barrier2"]
+            names = (["clauses1", "barrier1", "fold1", "barrier2", "clauses2", "barrier3", "fold2", "barrier4_dt"]
+                     if adaptive else ["clauses", "barrier1", "fold", "book", "barrier2"])
             for w in range(16):
-                row = [buf[w * 8 + i] / steps for i in range(5)]
+                row = [buf[w * 8 + i] / steps for i in range(len(names))]
                 if sum(row) == 0:
                     continue
-                print(json.dumps({"prec": prec, "wave": w, "lanes": os.environ.get("ODESAT_SOLO_LANES"),
+                print(json.dumps({"prec": prec, "adaptive": adaptive, "wave": w, "lanes": os.environ.get("ODESAT_SOLO_LANES"),
                                   **{n: round(x, 1) for n, x in zip(names, row)}, "total": round(sum(row), 1)}))
 
 
