@@ -77,6 +77,9 @@ def parse():
     p.add_argument("--no-inter", action="store_true", help="skip the inter-mode (STOP_ANY) line")
     p.add_argument("--config5-graph", type=int, default=0,
                    help="steps per captured HIP graph in partition_config5 (0 = all timed steps in one graph)")
+    p.add_argument("--leg-deadline", type=float, default=900.0,
+                   help="seconds after the headline by which every extra leg must be done; past it each rank's "
+                        "watchdog ends the job (rank 0 first prints the line with the legs finished so far)")
     args = p.parse_args()
     skip = {x for x in args.skip.split(",") if x}
     if args.only:
@@ -320,6 +323,47 @@ def roofline(args, short, ms, launches, clause_bytes_step, batch=None, dtype=Non
     return r
 
 
+class Watchdog:
+    """A stuck extra leg (a collective that never completes on some node) must not cost the headline
+    line: past the deadline, rank 0 prints the line built so far (the unfinished legs marked) and every
+    rank ends its process.  `emit` prints at most once, from whichever thread gets there first."""
+
+    def __init__(self, deadline_s, rank, build_line):
+        import threading
+        self.rank, self.build_line = rank, build_line
+        self.lock = threading.Lock()
+        self.done = False
+        self.timer = threading.Timer(deadline_s, self._fire)
+        self.timer.daemon = True
+        self.timer.start()
+
+    def emit(self, extra=None):
+        with self.lock:
+            if self.done:
+                return False
+            self.done = True
+            if self.rank == 0:
+                print(json.dumps(self.build_line(extra)), flush=True)
+            return True
+
+    def _fire(self):
+        for _ in range(3):  # (the main thread may be adding a leg to the line while it is built)
+            try:
+                ok = self.emit({"watchdog": "leg deadline passed; unfinished legs are missing from this line"})
+                break
+            except RuntimeError:
+                with self.lock:
+                    self.done = False
+                ok = False
+        if ok:
+            sys.stderr.write("bench.py: leg deadline passed, ending the job\n")
+            sys.stderr.flush()
+            os._exit(0)
+
+    def cancel(self):
+        self.timer.cancel()
+
+
 def formula_of(config):
     from odesat_amd import cnf
     from odesat_amd import workloads as wl
@@ -367,6 +411,39 @@ def main():
     tsize = 4 if args.dtype == "f32" else 8
     step_bytes = B * (2 * n + 4 * m) * tsize  # algorithmic per GPU-step: v, xs, xl read + written once
     res = {}
+    cpu = cpu_all = None
+
+    def line(extra=None):
+        out = {
+            "metric": "ODE steps/s x batch on random 3-SAT n=10k m=42k (replica-steps/s)",
+            "value": value,
+            "unit": "replica-steps/s",
+            "n_gpus": devices,
+            "ranks": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32" if args.dtype == "f32" else "fp64",
+            "data": "synthetic: seeded random 3-SAT instance + counter-RNG initial voltages (no dataset)",
+            "config": {"workload": f"{args.config}: random 3-SAT n={n} m={m} seed={c['seed']}, fixed-step "
+                                   f"Euler dt=0.01, all replicas stepped (no early exit)",
+                       "global_batch": B * world, "batch_per_gpu": B, "n": n, "m": m,
+                       "parallelism": f"replica-sharded x{world} (no collectives)"},
+            "roofline": roof,
+            "step_kernels_ms": {"clause": ms[0], "variable": ms[1], "status": ms[2]},
+            "step_algorithmic_GBps": step_bytes * args.steps / wall / 1e9,
+            "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
+            **dict(res),
+        }
+        if extra:
+            out.update(extra)
+        return out
+
+    dog = Watchdog(args.leg_deadline, rank, line)
 
     def simple_leg(name, **kw):
         w, ms_, l_, b_, a_, ran = run_batch(B, True, **kw)
@@ -428,40 +505,14 @@ def main():
     if "ab" in legs and kern == "k_onchip":
         leg("ab_hbm_streaming", ab_leg)
 
-    cpu = cpu_all = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(cp, v_, n_, n, m, args.cpu_replicas, args.cpu_steps)
         t = cpu_threads()
         if t > 1:  # the same oracle on every host core this job has, beside the 1-core line
             cpu_all = cpu_baseline(cp, v_, n_, n, m, args.cpu_replicas * t, args.cpu_steps, threads=t)
 
-    if rank == 0:
-        out = {
-            "metric": "ODE steps/s x batch on random 3-SAT n=10k m=42k (replica-steps/s)",
-            "value": value,
-            "unit": "replica-steps/s",
-            "n_gpus": devices,
-            "ranks": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp32" if args.dtype == "f32" else "fp64",
-            "data": "synthetic: seeded random 3-SAT instance + counter-RNG initial voltages (no dataset)",
-            "config": {"workload": f"{args.config}: random 3-SAT n={n} m={m} seed={c['seed']}, fixed-step "
-                                   f"Euler dt=0.01, all replicas stepped (no early exit)",
-                       "global_batch": B * world, "batch_per_gpu": B, "n": n, "m": m,
-                       "parallelism": f"replica-sharded x{world} (no collectives)"},
-            "roofline": roof,
-            "step_kernels_ms": {"clause": ms[0], "variable": ms[1], "status": ms[2]},
-            "step_algorithmic_GBps": step_bytes * args.steps / wall / 1e9,
-            "cpu_baseline": cpu,
-            "cpu_baseline_all_cores": cpu_all,
-            **res,
-        }
-        print(json.dumps(out))
+    dog.cancel()
+    dog.emit()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -29,6 +29,12 @@ template <int R> struct ResShape {
     static constexpr int NL = NTH / R;  // clause lanes = tile capacity in clauses
 };
 constexpr int RES_DEPTH = 4;  // tiles in flight per lane (3-SAT register prefetch ring)
+// f64 rings (RES_DEPTH_F64; the host pads 3-SAT tilings to a multiple of 4 tiles, so a ring of 8
+// ends with a static half block): twice the memory bytes in flight per lane
+#ifndef RES_DEPTH_F64
+#define RES_DEPTH_F64 8
+#endif
+template <typename T> constexpr int res_depth() { return sizeof(T) == 8 ? RES_DEPTH_F64 : RES_DEPTH; }
 
 template <typename T> struct RArgs {
     const int4 *__restrict__ cl4;      // [m] 3-SAT: the clause's literals (var << 1 | neg), internal order
@@ -285,7 +291,7 @@ __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> 
     Pend<T> Q;
     res_clause3<T, R, PK>(a, x, CM, t + 1, S, Q, on, h, uns, e, CMr != CM);  // Q.ok = false past the last tile
     res_apply3<T, R>(x, P);
-    res_load3<T, R, PK>(a, x, CMr, t + 1 + RES_DEPTH, S);
+    res_load3<T, R, PK>(a, x, CMr, t + 1 + res_depth<T>(), S);
 #ifdef RES_TIMING_PAIRS  // timing-only diagnostic build (results race): a barrier after odd tiles only
     if (t & 1)
 #endif
@@ -300,26 +306,30 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
                                          bool &uns, T &e) {
     const int NT_ = a.ntiles;
     if constexpr (K3) {
-        static_assert(RES_DEPTH == 4, "the pipeline below is unrolled for 4 slots");
+        constexpr int D = res_depth<T>();
+        static_assert(D == 4 || D == 8, "the pipeline below is unrolled for 4 or 8 slots");
         // the host pads 3-SAT tilings to a multiple of 4 tiles (empty tiles), so the unrolled loop
-        // below runs whole
+        // below runs whole (D = 8: blocks of 8, then at most one static block of 4)
         if (NT_ == 0) {
             __syncthreads();
             return;
         }
-        TileLoad<T> b0, b1, b2, b3;
+        TileLoad<T> b[D];
         Pend<T> P;
-        res_load3<T, R, PK>(a, x, CMr, 0, b0);
-        res_load3<T, R, PK>(a, x, CMr, 1, b1);
-        res_load3<T, R, PK>(a, x, CMr, 2, b2);
-        res_load3<T, R, PK>(a, x, CMr, 3, b3);
-        res_clause3<T, R, PK>(a, x, CM, 0, b0, P, on, h, uns, e, CMr != CM);
-        res_load3<T, R, PK>(a, x, CMr, RES_DEPTH, b0);
-        for (int t0 = 0; t0 < NT_; t0 += 4) {  // iteration t computes tile t+1 from slot (t+1) % 4
-            res_iter3<T, R, PK>(a, x, CMr, CM, t0, b1, P, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CMr, CM, t0 + 1, b2, P, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CMr, CM, t0 + 2, b3, P, on, h, uns, e);
-            res_iter3<T, R, PK>(a, x, CMr, CM, t0 + 3, b0, P, on, h, uns, e);
+#pragma unroll
+        for (int i = 0; i < D; ++i) res_load3<T, R, PK>(a, x, CMr, i, b[i]);
+        res_clause3<T, R, PK>(a, x, CM, 0, b[0], P, on, h, uns, e, CMr != CM);
+        res_load3<T, R, PK>(a, x, CMr, D, b[0]);
+        int t0 = 0;
+        for (; t0 + D <= NT_; t0 += D) {  // iteration t computes tile t+1 from slot (t+1) % D
+#pragma unroll
+            for (int i = 0; i < D; ++i) res_iter3<T, R, PK>(a, x, CMr, CM, t0 + i, b[(i + 1) % D], P, on, h, uns, e);
+        }
+        if constexpr (D == 8) {
+            if (t0 < NT_) {  // four tiles left: slots 1 .. 4
+#pragma unroll
+                for (int i = 0; i < 4; ++i) res_iter3<T, R, PK>(a, x, CMr, CM, t0 + i, b[i + 1], P, on, h, uns, e);
+            }
         }
     } else {
         for (int t = 0; t < NT_; ++t) {

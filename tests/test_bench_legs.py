@@ -75,3 +75,41 @@ def test_bench_multi_gpu_legs_two_rank_gloo(tmp_path):
     for name in ("clauses", "clauses_rs", "variables"):
         assert c5[name]["value"] > 0 and c5[name]["exchange_bytes_per_rank"] > 0
     assert c5["variables"]["local_clauses_rank0"] < TINY5["m"]  # a share of the clauses
+
+
+def test_watchdog_prints_the_line_and_ends_the_job_past_the_deadline():
+    """A leg that never returns (a collective stuck on one node) costs only that leg: past
+    --leg-deadline rank 0 prints the line built so far, marked, and the process exits 0."""
+    import subprocess
+    import sys
+    import time
+    code = ("import sys, time; sys.path.insert(0, %r); import bench\n"
+            "res = {}\n"
+            "w = bench.Watchdog(0.5, 0, lambda e: {'value': 7.0, **res, **(e or {})})\n"
+            "res['f64'] = {'value': 1.0}\n"
+            "time.sleep(30)\n" % ROOT)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and time.time() - t0 < 25
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["value"] == 7.0 and d["f64"] == {"value": 1.0} and "watchdog" in d
+
+
+def test_watchdog_emits_once_when_the_legs_finish():
+    import contextlib
+    import io
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        w = bench.Watchdog(60.0, 0, lambda e: {"value": 3.0, **(e or {})})
+        w.cancel()
+        assert w.emit() and not w.emit()
+        w1 = bench.Watchdog(60.0, 1, lambda e: {"value": 3.0})  # other ranks print nothing
+        w1.cancel()
+        assert w1.emit()
+    lines = buf.getvalue().splitlines()
+    assert lines == [json.dumps({"value": 3.0})]
