@@ -70,6 +70,7 @@ struct odesat_solver {
     bool solo = false;          // k_solo (wave.hpp) instead of k_wave: one replica per workgroup, lanes' slots in registers
     int solo_nl = 64, solo_cpl = 1, solo_vpl = 1;  // k_solo: lanes per replica, clause / variable slots per lane
     bool solo_fast = true;      // k_solo's short arithmetic on in-range states (ODESAT_SOLO_FAST=0: the general form)
+    bool wave_fast = true;      // k_wave's likewise (ODESAT_WAVE_FAST=0)
     int wv_tw = 1;              // k_wave: waves per replica, fixed steps
     int wv_tw_ada = 1;          // ... adaptive steps (four barriers per step instead of two: at most 4)
     bool res_ada = false; // adaptive steps run k_resident (else FUSED on the same layout)
@@ -745,14 +746,14 @@ int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     return ODESAT_OK;
 }
 
-template <typename T, bool ADA, int WPW, int TW> int launch_wave_k(odesat_solver *s, WArgs<T> a) {
+template <typename T, bool ADA, int WPW, int TW, bool FAST> int launch_wave_k(odesat_solver *s, WArgs<T> a) {
     a.topo_bytes = (uint32_t)wave_topo_bytes(s->n, s->m);
     a.rep_bytes = (uint32_t)wave_lds_bytes(s->n, s->m, s->L, sizeof(T), ADA);
     const size_t lds = a.topo_bytes + (size_t)WPW * a.rep_bytes;
-    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_wave<T, ADA, WPW, TW>), (int)RES_LDS_MAX));
+    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_wave<T, ADA, WPW, TW, FAST>), (int)RES_LDS_MAX));
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_wave<T, ADA, WPW, TW>), dim3((unsigned)((s->G + WPW - 1) / WPW)),
+        hipLaunchKernelGGL((k_wave<T, ADA, WPW, TW, FAST>), dim3((unsigned)((s->G + WPW - 1) / WPW)),
                            dim3(WAVE_NTH * WPW * TW), lds, s->stream, a);
     }
     HIP_TRY(hipGetLastError());
@@ -824,7 +825,9 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     }
     auto go = [&](auto ww, auto tw) -> int {
         constexpr int WPW = decltype(ww)::value, TW = decltype(tw)::value;
-        return adaptive ? launch_wave_k<T, true, WPW, TW>(s, a) : launch_wave_k<T, false, WPW, TW>(s, a);
+        if (fast && s->wave_fast)  // in-range states: the short arithmetic (wave.hpp lane_clauses)
+            return adaptive ? launch_wave_k<T, true, WPW, TW, true>(s, a) : launch_wave_k<T, false, WPW, TW, true>(s, a);
+        return adaptive ? launch_wave_k<T, true, WPW, TW, false>(s, a) : launch_wave_k<T, false, WPW, TW, false>(s, a);
     };
     // (replicas per workgroup, waves per replica): at most 16 waves per workgroup
     switch (s->wv_wpw * 100 + (adaptive ? s->wv_tw_ada : s->wv_tw)) {
@@ -1141,12 +1144,12 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     for (auto e : s->pool) (void)hipEventDestroy(e);
     void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->pc, s->ps, s->empty, s->inc, s->v[0], s->v[1], s->c[0],
                     s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
-                    s->sat_step, s->steps_done, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec, s->oc_tcp, s->wv_rec4, s->wv_vst};
+                    s->sat_step, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec, s->oc_tcp, s->wv_rec4, s->wv_vst};
     for (void *p : ptrs) dfree(p);
     void *snaps[] = {s->snap_par, s->snap_sat, s->snap_done, s->snap_dt, s->ck_v, s->ck_c, s->ck_dt, s->ck_par,
                      s->ck_act, s->ck_sat, s->ck_done, s->ck_stop};
     for (void *p : snaps) dfree(p);
-    void *pinned[] = {s->h_sat, s->h_done, s->h_dt, s->h_stop, s->h_act};
+    void *pinned[] = {s->h_sat, s->h_dt, s->h_stop, s->h_act};  // (h_done lies inside h_sat's block)
     for (void *p : pinned)
         if (p) (void)hipHostFree(p);
     if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -1432,6 +1435,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             // k_solo_fast's padded term blocks must fit as well
             s->solo_fast = solo_fast_elems(n, L, s->tsize) * s->tsize <= RES_LDS_MAX;
             if (const char *ev = std::getenv("ODESAT_SOLO_FAST")) s->solo_fast = s->solo_fast && std::atoi(ev) != 0;
+            if (const char *ev = std::getenv("ODESAT_WAVE_FAST")) s->wave_fast = std::atoi(ev) != 0;
         }
         if ((rc = onchip_setup(s, tiles, wst, lits))) return bail(rc);
         if (s->oc_tr > 0) s->alg = ODESAT_ALG_ONCHIP;
@@ -1446,14 +1450,15 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     if ((rc = dmalloc(s, &s->err, s->Bp * 8))) return bail(rc);
     if ((rc = dmalloc(s, (void **)&s->unsat, s->Bp * 4))) return bail(rc);
     if ((rc = dmalloc(s, (void **)&s->act, s->Bp))) return bail(rc);
-    if ((rc = dmalloc(s, (void **)&s->sat_step, s->Bp * 8))) return bail(rc);
-    if ((rc = dmalloc(s, (void **)&s->steps_done, s->Bp * 8))) return bail(rc);
+    // sat steps and steps done side by side (one device-to-host copy returns both, finish_simulate)
+    if ((rc = dmalloc(s, (void **)&s->sat_step, 2 * s->Bp * 8))) return bail(rc);
+    s->steps_done = s->sat_step + s->Bp;
     if ((rc = dmalloc(s, (void **)&s->stop, 16))) return bail(rc);
-    if (hipHostMalloc((void **)&s->h_sat, s->Bp * 8) != hipSuccess ||
-        hipHostMalloc((void **)&s->h_done, s->Bp * 8) != hipSuccess ||
+    if (hipHostMalloc((void **)&s->h_sat, 2 * s->Bp * 8) != hipSuccess ||
         hipHostMalloc((void **)&s->h_dt, s->Bp * 8) != hipSuccess ||
         hipHostMalloc((void **)&s->h_stop, 16) != hipSuccess || hipHostMalloc((void **)&s->h_act, s->Bp) != hipSuccess)
         return bail(fail(ODESAT_ENOMEM, "hipHostMalloc failed"));
+    s->h_done = s->h_sat + s->Bp;
     if (hipMemsetAsync(s->err, 0, s->Bp * 8, s->stream) != hipSuccess)
         return bail(fail(ODESAT_EDEVICE, "memset failed"));
     // default state: v = 0, xs = init_short_term_memory, xl = 1
@@ -1647,8 +1652,12 @@ extern "C" int odesat_euler_step(odesat_solver *s, double tol, double *dt, doubl
 // Results of a simulate call: per-replica bookkeeping through the pinned staging buffers, one sync.
 static int finish_simulate(odesat_solver *s, const odesat_params *p, bool adaptive, int64_t t_run,
                            int64_t *first_sat_step, int64_t *steps_done, double *dt_out, int64_t *steps_run) {
-    if (first_sat_step) HIP_TRY(hipMemcpyAsync(s->h_sat, s->sat_step, s->B * 8, hipMemcpyDeviceToHost, s->stream));
-    if (steps_done) HIP_TRY(hipMemcpyAsync(s->h_done, s->steps_done, s->B * 8, hipMemcpyDeviceToHost, s->stream));
+    if (first_sat_step && steps_done)  // one copy: the two arrays are adjacent (Bp apart)
+        HIP_TRY(hipMemcpyAsync(s->h_sat, s->sat_step, (s->Bp + s->B) * 8, hipMemcpyDeviceToHost, s->stream));
+    else if (first_sat_step)
+        HIP_TRY(hipMemcpyAsync(s->h_sat, s->sat_step, s->B * 8, hipMemcpyDeviceToHost, s->stream));
+    else if (steps_done)
+        HIP_TRY(hipMemcpyAsync(s->h_done, s->steps_done, s->B * 8, hipMemcpyDeviceToHost, s->stream));
     if (dt_out && adaptive)
         HIP_TRY(hipMemcpyAsync(s->h_dt, s->dtr, s->B * s->tsize, hipMemcpyDeviceToHost, s->stream));
     if (p->stop == ODESAT_STOP_ANY) HIP_TRY(hipMemcpyAsync(s->h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream));

@@ -122,6 +122,60 @@ __device__ __forceinline__ bool clause_math(const int (&lit)[3], const T (&v)[3]
     return PK != W_ADA2 && !(C < (T)0.25);  // :88 (unsat)
 }
 
+// q v for q = -1 / +1: the sign bit of v flipped by the literal's sign word (0x80000000 or 0), on the
+// high dword in f64
+template <typename T> __device__ __forceinline__ T sflip(T x, uint32_t sg) {
+    if constexpr (sizeof(T) == 8) {
+        return __longlong_as_double((long long)((unsigned long long)__double_as_longlong(x) ^ ((unsigned long long)sg << 32)));
+    } else {
+        return __uint_as_float(__float_as_uint(x) ^ sg);
+    }
+}
+
+// the terms (2 x the reference's) of one clause at voltages v, memories product tt; returns mn
+template <typename T>
+__device__ __forceinline__ T solo_terms(const T (&v)[3], const uint32_t (&sg)[3], T tt, T (&d)[3]) {
+    const T one = (T)1.0;
+    const T val0 = one - sflip(v[0], sg[0]), val1 = one - sflip(v[1], sg[1]), val2 = one - sflip(v[2], sg[2]);  // :47
+    const T sel0 = dmin(val1, val2), sel1 = dmin(val0, val2), sel2 = dmin(val0, val1);
+    d[0] = sflip(tt * sel0, sg[0]);  // 2 xl xs G (:64-70, :80)
+    d[1] = sflip(tt * sel1, sg[1]);
+    d[2] = sflip(tt * sel2, sg[2]);
+    return dmin(sel2, val2);  // :49-57
+}
+
+// one memory step of length hx from (xs, xl) with the clause's mn: xs + hx/2 * (2 dxs), xl + hx * dxl
+// (:84-85, :94-95; hx2 = hx / 2)
+template <typename T>
+__device__ __forceinline__ void solo_mem(T xs, T xl, T mn, T hx2, T hx, T xl_max, T &xs_o, T &xl_o) {
+    const T eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
+    const T dxs = ((T)20.0 * (xs + eps)) * (mn - (T)0.5);  // 2 dxs
+    const T dxl = (T)2.5 * (mn - (T)0.1);
+    xs_o = dmin(dmax(xs + hx2 * dxs, eps), xs_hi);
+    xl_o = dmin(dmax(xl + hx * dxl, (T)1.0), xl_max);
+}
+
+// The max of x over the wave (all 64 lanes active), uniform: a DPP butterfly within each quad, row
+// rotations within each row of 16, then the four rows' maxima by readlane.
+template <int CTRL> __device__ __forceinline__ uint32_t max_dpp(uint32_t x) {
+    return max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+    x = max_dpp<0xB1>(x);   // quad_perm [1, 0, 3, 2]
+    x = max_dpp<0x4E>(x);   // quad_perm [2, 3, 0, 1]
+    x = max_dpp<0x124>(x);  // row_ror:4
+    x = max_dpp<0x128>(x);  // row_ror:8
+    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
+    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+    return max(max(r0, r1), max(r2, r3));
+}
+__device__ __forceinline__ uint32_t wave_max_bits(uint32_t x) { return wave_max_u32(x); }
+__device__ __forceinline__ unsigned long long wave_max_bits(unsigned long long x) {  // (high word, then low word)
+    const uint32_t hi = wave_max_u32((uint32_t)(x >> 32));
+    const uint32_t lo = wave_max_u32((uint32_t)(x >> 32) == hi ? (uint32_t)x : 0u);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 // Phase 1 over the replica's clauses, one lane's share.  Returns whether one of this lane's clauses
 // is unsat (:88, W_FIXED / W_ADA1) and raises e to the memories' max_error terms (W_ADA2).
 // Lane l of the replica's NL lanes takes clauses l, l + NL, ...  Software-pipelined: the records of
@@ -129,7 +183,9 @@ __device__ __forceinline__ bool clause_math(const int (&lit)[3], const T (&v)[3]
 // arithmetic and stores (nothing phase 1 stores is read by another
 // clause: terms, memories and C are per clause and v is constant), so one wave per SIMD keeps
 // three clauses' LDS reads in flight instead of waiting on each clause's dependent load chain.
-template <typename T, int PK, int NL>
+// FAST (in-range states): solo_terms / solo_mem's exact short forms -- 2 x terms (the fold's caller
+// halves h), the first pass keeps mn (= 2 C) for the second.
+template <typename T, int PK, int NL, bool FAST>
 __device__ __forceinline__ bool lane_clauses(const WArgs<T> &a, const int4 *rec4, const T *vL, T *tL, T *cmL, T *cL,
                                              int l, T h, T &e) {
     bool uns = false;
@@ -155,7 +211,29 @@ __device__ __forceinline__ bool lane_clauses(const WArgs<T> &a, const int4 *rec4
         gather(cn, rn, W);       // the next clause's voltages and memories
         rn = rec4[min(c + 2 * NL, last)];
         T d[3];
-        uns = clause_math<T, PK>(X.lit, X.v, X.xs, X.xl, X.C1, h, a.zeta, a.xl_max, d, e) || uns;
+        if constexpr (FAST) {
+            const uint32_t sg[3] = {(uint32_t)X.lit[0] << 31, (uint32_t)X.lit[1] << 31, (uint32_t)X.lit[2] << 31};
+            const T hh = (T)0.5 * h, hq = (T)0.25 * h;
+            if (PK == W_FIXED) {
+                const T mn = solo_terms<T>(X.v, sg, X.xl * X.xs, d);
+                solo_mem<T>(X.xs, X.xl, mn, hh, h, a.xl_max, X.xs, X.xl);
+                uns = uns || !(mn < (T)0.5);  // :88
+            } else if (PK == W_ADA1) {
+                X.C1 = solo_terms<T>(X.v, sg, X.xl * X.xs, d);  // mn1 = 2 C1
+                uns = uns || !(X.C1 < (T)0.5);
+            } else {
+                T xsf, xlf, xsh, xlh, xsn, xln;
+                solo_mem<T>(X.xs, X.xl, X.C1, hh, h, a.xl_max, xsf, xlf);  // full-step clone (:124-125)
+                solo_mem<T>(X.xs, X.xl, X.C1, hq, hh, a.xl_max, xsh, xlh);  // first half step (:128)
+                const T mn = solo_terms<T>(X.v, sg, xlh * xsh, d);
+                solo_mem<T>(xsh, xlh, mn, hq, hh, a.xl_max, xsn, xln);      // second half step (:130)
+                e = dmax(e, dmax(dabs(xsf - xsn), dabs(xlf - xln)));       // :132
+                X.xs = xsn;
+                X.xl = xln;
+            }
+        } else {
+            uns = clause_math<T, PK>(X.lit, X.v, X.xs, X.xl, X.C1, h, a.zeta, a.xl_max, d, e) || uns;
+        }
 #pragma unroll
         for (int j = 0; j < 3; ++j) tL[X.pos[j]] = d[j];
         if (PK == W_ADA1) {
@@ -174,10 +252,10 @@ __device__ __forceinline__ bool lane_clauses(const WArgs<T> &a, const int4 *rec4
 // waves).  The ballot runs after every lane's share has returned: taken inside lane_clauses, the
 // lanes without a clause (m < NL) would vote among themselves on a divergent path and leave the
 // result -- and the step loop's exit -- different across the wave's lanes.
-template <typename T, int PK, int NL>
+template <typename T, int PK, int NL, bool FAST>
 __device__ __forceinline__ bool wave_clauses(const WArgs<T> &a, const int4 *rec4, const T *vL, T *tL, T *cmL, T *cL,
                                              int l, T h, T &e) {
-    const bool u = lane_clauses<T, PK, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
+    const bool u = lane_clauses<T, PK, NL, FAST>(a, rec4, vL, tL, cmL, cL, l, h, e);
     return __any(u);
 }
 
@@ -216,7 +294,7 @@ template <int TW> __device__ __forceinline__ void team_sync() {
     else __syncthreads();
 }
 
-template <typename T, bool ADAPTIVE, int WPW, int TW>
+template <typename T, bool ADAPTIVE, int WPW, int TW, bool FAST = false>
 __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
     constexpr int NL = WAVE_NTH * TW;
     extern __shared__ __attribute__((aligned(16))) unsigned char wave_smem[];
@@ -274,26 +352,27 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
         const int act0 = act;  // this step's participation; the bookkeeping below may clear act
         bool go = false;
         if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
-            if (act0) uns = wave_clauses<T, W_FIXED, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
+            if (act0) uns = wave_clauses<T, W_FIXED, NL, FAST>(a, rec4, vL, tL, cmL, cL, l, h, e);
             uns = team_any(uns);
             if (TW == 1) team_sync<TW>();  // (TW > 1: team_any's barrier ordered phase 1's stores)
+            const T hv = FAST ? (T)0.5 * h : h;  // FAST: 2 x terms
             if (act0)
-                for (int i = l; i < a.n; i += NL) vL[i] = dmin(dmax(vL[i] + h * wave_fold(vst, tL, i), (T)-1.0), (T)1.0);
+                for (int i = l; i < a.n; i += NL) vL[i] = dmin(dmax(vL[i] + hv * wave_fold(vst, tL, i), (T)-1.0), (T)1.0);
         } else {  // euler_step (:111-139)
-            if (act0) uns = wave_clauses<T, W_ADA1, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
+            if (act0) uns = wave_clauses<T, W_ADA1, NL, FAST>(a, rec4, vL, tL, cmL, cL, l, h, e);
             uns = team_any(uns);
             if (TW == 1) team_sync<TW>();
             if (l == 0) errL[w] = 0;  // last read before the previous step's closing barrier
             go = act0 && uns;  // an allsat replica takes no step (:122)
-            const T half = (T)0.5 * h;
+            const T hf = FAST ? (T)0.5 * h : h, half = FAST ? (T)0.25 * h : (T)0.5 * h;  // FAST: 2 x terms
             if (go)
                 for (int i = l; i < a.n; i += NL) {
                     const T d = wave_fold(vst, tL, i), v = vL[i];
-                    vfL[i] = dmin(dmax(v + h * d, (T)-1.0), (T)1.0);    // full-step clone
+                    vfL[i] = dmin(dmax(v + hf * d, (T)-1.0), (T)1.0);   // full-step clone
                     vL[i] = dmin(dmax(v + half * d, (T)-1.0), (T)1.0);  // first half step
                 }
             team_sync<TW>();
-            if (go) wave_clauses<T, W_ADA2, NL>(a, rec4, vL, tL, cmL, cL, l, h, e);
+            if (go) wave_clauses<T, W_ADA2, NL, FAST>(a, rec4, vL, tL, cmL, cL, l, h, e);
             team_sync<TW>();
             if (go)
                 for (int i = l; i < a.n; i += NL) {
@@ -362,16 +441,6 @@ template <typename T> __device__ __forceinline__ T solo_fold(const T *tL, int s,
             if (k0 + u < d) dv += t[u];
     }
     return dv;
-}
-
-// q v for q = -1 / +1: the sign bit of v flipped by the literal's sign word (0x80000000 or 0), on the
-// high dword in f64
-template <typename T> __device__ __forceinline__ T sflip(T x, uint32_t sg) {
-    if constexpr (sizeof(T) == 8) {
-        return __longlong_as_double((long long)((unsigned long long)__double_as_longlong(x) ^ ((unsigned long long)sg << 32)));
-    } else {
-        return __uint_as_float(__float_as_uint(x) ^ sg);
-    }
 }
 
 // One clause on an in-range state (FAST): the exact short forms of onchip.hip's header, in T.
@@ -663,50 +732,6 @@ constexpr int SOLO_DPAD = 8;
 inline size_t solo_fast_elems(int64_t n, int64_t L, size_t tsize) {
     const int64_t per16 = 16 / (int64_t)tsize;
     return (size_t)((n + per16 - 1) / per16 * per16 + n * SOLO_DPAD + L);
-}
-
-// the terms (2 x the reference's) of one clause at voltages v, memories product tt; returns mn
-template <typename T>
-__device__ __forceinline__ T solo_terms(const T (&v)[3], const uint32_t (&sg)[3], T tt, T (&d)[3]) {
-    const T one = (T)1.0;
-    const T val0 = one - sflip(v[0], sg[0]), val1 = one - sflip(v[1], sg[1]), val2 = one - sflip(v[2], sg[2]);  // :47
-    const T sel0 = dmin(val1, val2), sel1 = dmin(val0, val2), sel2 = dmin(val0, val1);
-    d[0] = sflip(tt * sel0, sg[0]);  // 2 xl xs G (:64-70, :80)
-    d[1] = sflip(tt * sel1, sg[1]);
-    d[2] = sflip(tt * sel2, sg[2]);
-    return dmin(sel2, val2);  // :49-57
-}
-
-// one memory step of length hx from (xs, xl) with the clause's mn: xs + hx/2 * (2 dxs), xl + hx * dxl
-// (:84-85, :94-95; hx2 = hx / 2)
-template <typename T>
-__device__ __forceinline__ void solo_mem(T xs, T xl, T mn, T hx2, T hx, T xl_max, T &xs_o, T &xl_o) {
-    const T eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
-    const T dxs = ((T)20.0 * (xs + eps)) * (mn - (T)0.5);  // 2 dxs
-    const T dxl = (T)2.5 * (mn - (T)0.1);
-    xs_o = dmin(dmax(xs + hx2 * dxs, eps), xs_hi);
-    xl_o = dmin(dmax(xl + hx * dxl, (T)1.0), xl_max);
-}
-
-// The max of x over the wave (all 64 lanes active), uniform: a DPP butterfly within each quad, row
-// rotations within each row of 16, then the four rows' maxima by readlane.
-template <int CTRL> __device__ __forceinline__ uint32_t max_dpp(uint32_t x) {
-    return max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, 0xf, 0xf, false));
-}
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
-    x = max_dpp<0xB1>(x);   // quad_perm [1, 0, 3, 2]
-    x = max_dpp<0x4E>(x);   // quad_perm [2, 3, 0, 1]
-    x = max_dpp<0x124>(x);  // row_ror:4
-    x = max_dpp<0x128>(x);  // row_ror:8
-    const uint32_t r0 = (uint32_t)__builtin_amdgcn_readlane((int)x, 0), r1 = (uint32_t)__builtin_amdgcn_readlane((int)x, 16);
-    const uint32_t r2 = (uint32_t)__builtin_amdgcn_readlane((int)x, 32), r3 = (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
-    return max(max(r0, r1), max(r2, r3));
-}
-__device__ __forceinline__ uint32_t wave_max_bits(uint32_t x) { return wave_max_u32(x); }
-__device__ __forceinline__ unsigned long long wave_max_bits(unsigned long long x) {  // (high word, then low word)
-    const uint32_t hi = wave_max_u32((uint32_t)(x >> 32));
-    const uint32_t lo = wave_max_u32((uint32_t)(x >> 32) == hi ? (uint32_t)x : 0u);
-    return ((unsigned long long)hi << 32) | lo;
 }
 
 template <typename T, bool ADAPTIVE, int CPL, int VPL>

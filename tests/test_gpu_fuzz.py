@@ -84,6 +84,9 @@ def variants(prec, uniform3, distinct):
             if lanes != "0":
                 env["ODESAT_SOLO_LANES"] = lanes
             v.append((f"solo-l{lanes}", env, _lib.ODESAT_ALG_RESIDENT))
+        # k_wave's general arithmetic (its short forms are the default on in-range states)
+        v.append(("wave-general", {"ODESAT_WAVE": "1", "ODESAT_SOLO": "0", "ODESAT_WAVE_TEAM": "2",
+                                   "ODESAT_WAVE_FAST": "0"}, _lib.ODESAT_ALG_RESIDENT))
         # k_solo's general arithmetic (the fast kernel, k_solo_fast, is the default on in-range states)
         v.append(("solo-general", {"ODESAT_WAVE": "1", "ODESAT_SOLO": "1", "ODESAT_SOLO_FAST": "0"},
                   _lib.ODESAT_ALG_RESIDENT))
@@ -173,7 +176,8 @@ def test_fuzz_covered_every_path():
             ("wave-t1", _lib.ODESAT_ALG_RESIDENT), ("wave-t2", _lib.ODESAT_ALG_RESIDENT),
             ("wave-t4", _lib.ODESAT_ALG_RESIDENT), ("onchip", _lib.ODESAT_ALG_ONCHIP),
             ("solo-l64", _lib.ODESAT_ALG_RESIDENT), ("solo-l128", _lib.ODESAT_ALG_RESIDENT),
-            ("solo-l0", _lib.ODESAT_ALG_RESIDENT), ("solo-general", _lib.ODESAT_ALG_RESIDENT)]
+            ("solo-l0", _lib.ODESAT_ALG_RESIDENT), ("solo-general", _lib.ODESAT_ALG_RESIDENT),
+            ("wave-general", _lib.ODESAT_ALG_RESIDENT)]
     print(sorted(COVERED.items()))
     missing = [k for k in need if COVERED.get(k, 0) < 4]
     assert not missing, (missing, COVERED)
