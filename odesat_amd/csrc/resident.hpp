@@ -28,7 +28,10 @@ template <int R> struct ResShape {
     static constexpr int NTH = R == 1 ? 512 : 1024;
     static constexpr int NL = NTH / R;  // clause lanes = tile capacity in clauses
 };
-constexpr int RES_DEPTH = 4;  // tiles in flight per lane (3-SAT register prefetch ring)
+#ifndef RES_DEPTH_F32
+#define RES_DEPTH_F32 4
+#endif
+constexpr int RES_DEPTH = RES_DEPTH_F32;  // tiles in flight per lane (3-SAT register prefetch ring)
 // f64 rings (RES_DEPTH_F64; the host pads 3-SAT tilings to a multiple of 4 tiles, so a ring of 8
 // ends with a static half block): twice the memory bytes in flight per lane
 #ifndef RES_DEPTH_F64

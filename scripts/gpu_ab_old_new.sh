@@ -8,7 +8,7 @@ OLD=${OLD:-old}
 B="timeout -k 10 150 python bench.py --no-cpu --only ${LEGS_ONLY:-adaptive} --extra-batch 0"
 val() { python -c 'import json,sys
 d=json.loads(sys.stdin.read().strip().splitlines()[-1]); a=d.get("adaptive",{})
-f=d.get("f64",{}); print("%.4g" % d["value"], "%.1f" % d["roofline"]["mean_launch_us"], "ada %.4g" % a.get("value",0), "f64 %.4g" % f.get("value",0))'; }
+f=d.get("f64",{}); ab=d.get("ab_hbm_streaming",{}); print("ab %.4g" % ab.get("value",0), "%.4g" % d["value"], "%.1f" % d["roofline"]["mean_launch_us"], "ada %.4g" % a.get("value",0), "f64 %.4g" % f.get("value",0))'; }
 for r in 1 2 3; do
   for st in "20 5" "200 50"; do
     set -- $st
