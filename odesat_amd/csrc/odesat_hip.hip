@@ -82,6 +82,7 @@ struct odesat_solver {
     // memories in VGPRs, [oc_tr, oc_tr + oc_tl) in LDS.  oc_tr == 0: not available
     int oc_tr = 0, oc_tl = 0;
     uint64_t *oc_rec = nullptr;  // [tiles][512] slot-major clause records (onchip::make_rec)
+    uint32_t *oc_rec12 = nullptr;  // ONCHIP_REC12: the same in 12 bytes (onchip::make_rec12)
     int32_t *oc_tcp = nullptr;   // [ntp * 8 + 1] wave starts (t * 8 + w) padded with m (static-index loads in k_onchip)
     int64_t oc_rec_bytes = 0;
     bool oc_ada = false;  // ONCHIP also takes adaptive steps (onchip.hpp ADA_*)
@@ -703,22 +704,30 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
     // slot-major records, padded with empty tiles so every tile a pass touches exists; an empty
     // slot of lane l points all three literals at sink word n + l % 32 (v = 1.0 there)
     std::vector<uint64_t> rec((size_t)ntp * onchip::NTH);
+    std::vector<uint32_t> rec12(ONCHIP_REC12 ? rec.size() * 3 : 0);
     for (int t = 0; t < ntp; ++t)
         for (int l = 0; l < onchip::NTH; ++l) {
             const size_t g = (size_t)t * W8 + l / 64;
             const int32_t k = ws[g] + l % 64;
+            const size_t i = (size_t)t * onchip::NTH + l;
             uint64_t r;
             if (k < ws[g + 1]) {
                 const int32_t *q = &lits[3 * (size_t)k];
-                r = onchip::make_rec(4u * (uint32_t)(q[0] >> 1), 4u * (uint32_t)(q[1] >> 1), 4u * (uint32_t)(q[2] >> 1),
-                                     q[0] & 1, q[1] & 1, q[2] & 1);
+                const uint32_t a0 = 4u * (uint32_t)(q[0] >> 1), a1 = 4u * (uint32_t)(q[1] >> 1), a2 = 4u * (uint32_t)(q[2] >> 1);
+                r = onchip::make_rec(a0, a1, a2, q[0] & 1, q[1] & 1, q[2] & 1);
+                if (ONCHIP_REC12) onchip::make_rec12(a0, a1, a2, q[0] & 1, q[1] & 1, q[2] & 1, &rec12[3 * i]);
             } else {
                 const uint32_t sink = 4u * (uint32_t)(s->n + l % onchip::SINKS);
                 r = onchip::make_rec(sink, sink, sink, false, false, false) | (uint64_t)onchip::REC_EMPTY << 32;
+                if (ONCHIP_REC12) onchip::make_rec12(sink, sink, sink, false, false, false, &rec12[3 * i]);
             }
-            rec[(size_t)t * onchip::NTH + l] = r;
+            rec[i] = r;
         }
     int rc;
+    if (ONCHIP_REC12) {
+        if ((rc = dmalloc(s, (void **)&s->oc_rec12, rec12.size() * 4))) return rc;
+        HIP_TRY(hipMemcpy(s->oc_rec12, rec12.data(), rec12.size() * 4, hipMemcpyHostToDevice));
+    }
     s->oc_rec_bytes = (int64_t)(rec.size() * sizeof(uint64_t));
     if ((rc = dmalloc(s, (void **)&s->oc_rec, rec.size() * sizeof(uint64_t)))) return rc;
     HIP_TRY(hipMemcpy(s->oc_rec, rec.data(), rec.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
@@ -920,6 +929,8 @@ int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zet
     a.oop = oop ? 1 : 0;
     a.rec = s->oc_rec;
     a.rec_bytes = (uint32_t)s->oc_rec_bytes;
+    a.rec12 = s->oc_rec12;
+    a.rec12_bytes = (uint32_t)(s->oc_rec_bytes / 8 * 12);
     a.lds = onchip::lds_map(s->n);
     a.tc = s->oc_tcp;
     a.v0 = (float *)s->v[0];
@@ -1144,7 +1155,7 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     for (auto e : s->pool) (void)hipEventDestroy(e);
     void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->pc, s->ps, s->empty, s->inc, s->v[0], s->v[1], s->c[0],
                     s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
-                    s->sat_step, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec, s->oc_tcp, s->wv_rec4, s->wv_vst};
+                    s->sat_step, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec, s->oc_rec12, s->oc_tcp, s->wv_rec4, s->wv_vst};
     for (void *p : ptrs) dfree(p);
     void *snaps[] = {s->snap_par, s->snap_sat, s->snap_done, s->snap_dt, s->ck_v, s->ck_c, s->ck_dt, s->ck_par,
                      s->ck_act, s->ck_sat, s->ck_done, s->ck_stop};

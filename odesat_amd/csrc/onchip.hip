@@ -67,14 +67,26 @@ struct Stamps {};
 struct Slot {  // one lane's literal record for one tile
     uint32_t lo, hi;
 };
+#if ONCHIP_REC12
+struct SlotF {  // the fixed-step kernel's 12-byte record: one word per literal (address | sign << 31)
+    uint32_t w0, w1, w2;
+};
+#else
+typedef Slot SlotF;
+#endif
 
 struct Pend {  // a clause's three dv terms (LDS byte addresses of v; dv is at +DVC), applied one tile later
     uint32_t a0, a1, a2;
     float d0, d1, d2;
 };
 
-struct Gath {  // a clause's gathered inputs: LDS byte addresses of its voltages, sign word, voltages
-    uint32_t a0, a1, a2, hi;
+struct Gath {  // a clause's gathered inputs: LDS byte addresses of its voltages, sign word(s), voltages
+    uint32_t a0, a1, a2;
+#if ONCHIP_REC12
+    uint32_t s0, s1, s2;  // the literals' record words (sign at bit 31)
+#else
+    uint32_t hi;
+#endif
     float v0, v1, v2;
 };
 
@@ -91,6 +103,17 @@ __device__ __forceinline__ Slot load_rec(const Recs &R, int t) {
     const i2 r = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, R.voff, R.soff + (uint32_t)t * (NTH * 8), 0);
     return Slot{(uint32_t)r.x, (uint32_t)r.y};
 }
+#if ONCHIP_REC12
+constexpr uint32_t RECF_BYTES = 12;
+__device__ __forceinline__ SlotF load_recf(const Recs &R, int t) {
+    typedef int i3 __attribute__((ext_vector_type(3)));
+    const i3 r = __builtin_amdgcn_raw_buffer_load_b96(R.rsrc, R.voff, R.soff + (uint32_t)t * (NTH * 12), 0);
+    return SlotF{(uint32_t)r.x, (uint32_t)r.y, (uint32_t)r.z};
+}
+#else
+constexpr uint32_t RECF_BYTES = 8;
+__device__ __forceinline__ SlotF load_recf(const Recs &R, int t) { return load_rec(R, t); }
+#endif
 
 typedef __attribute__((address_space(3))) float lfloat;
 __device__ __forceinline__ float lds_f(uint32_t byte_addr) { return *reinterpret_cast<const lfloat *>(byte_addr); }
@@ -99,11 +122,20 @@ typedef __attribute__((address_space(3))) float2 lfloat2;
 __device__ __forceinline__ float2 *lds_f2(uint32_t byte_addr) { return (float2 *)(reinterpret_cast<lfloat2 *>(byte_addr)); }
 
 // The clause's three voltages (system.rs:46-48): LDS reads issued here, consumed by front().
-__device__ __forceinline__ void gather(const Slot &S, Gath &G) {
+__device__ __forceinline__ void gather(const SlotF &S, Gath &G) {
+#if ONCHIP_REC12
+    G.a0 = S.w0 & 0xffffu;
+    G.a1 = S.w1 & 0xffffu;
+    G.a2 = S.w2 & 0xffffu;
+    G.s0 = S.w0;
+    G.s1 = S.w1;
+    G.s2 = S.w2;
+#else
     G.a0 = S.lo & 0xffffu;
     G.a1 = S.lo >> 16;
     G.a2 = S.hi & 0xffffu;
     G.hi = S.hi;
+#endif
     G.v0 = lds_f(G.a0);
     G.v1 = lds_f(G.a1);
     G.v2 = lds_f(G.a2);
@@ -123,8 +155,10 @@ __device__ __forceinline__ void gather(const Slot &S, Gath &G) {
 //   exactly the min of the OTHER two literal values: the min when some other literal attains it,
 //   the second smallest (the scan's `sec`, ties included) when j does -- so sel_j = min(val_k, val_l)
 //   needs no compare and no select.
-struct Front {  // first half: the min (:49-55) and each literal's selected value
-    uint32_t a0, a1, a2, hi;
+//   the sign q_j of literal j's term rides on its selected value (q tt sel = tt (q sel): a sign
+//   flip, exact), so the second half needs no sign word.
+struct Front {  // first half: the min (:49-55) and each literal's signed selected value
+    uint32_t a0, a1, a2;
     float sel0, sel1, sel2, mn;
 };
 
@@ -132,31 +166,34 @@ __device__ __forceinline__ void front(const Gath &G, Front &F) {
     F.a0 = G.a0;
     F.a1 = G.a1;
     F.a2 = G.a2;
-    F.hi = G.hi;
+#if ONCHIP_REC12
+    const uint32_t s0 = G.s0 & 0x80000000u, s1 = G.s1 & 0x80000000u, s2 = G.s2 & 0x80000000u;
+#else
     const uint32_t s0 = G.hi & 0x80000000u, s1 = (G.hi << 1) & 0x80000000u, s2 = (G.hi << 2) & 0x80000000u;
+#endif
     const float val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
     const float val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
     const float val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
-    F.sel0 = fminf(val1, val2);
-    F.sel1 = fminf(val0, val2);
-    F.sel2 = fminf(val0, val1);
-    F.mn = fminf(F.sel2, val2);  // min (:49-55)
+    const float sel2 = fminf(val0, val1);
+    F.sel0 = __uint_as_float(__float_as_uint(fminf(val1, val2)) ^ s0);
+    F.sel1 = __uint_as_float(__float_as_uint(fminf(val0, val2)) ^ s1);
+    F.sel2 = __uint_as_float(__float_as_uint(sel2) ^ s2);
+    F.mn = fminf(sel2, val2);  // min (:49-55)
 }
 
 // Second half: the three dv terms into Q, the sat fold and the memory update in place
 // (:60-88, :94-95).
 __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem, float h, float hh, Pend &Q,
                                      uint32_t &cmax) {
-    const uint32_t s0 = F.hi & 0x80000000u, s1 = (F.hi << 1) & 0x80000000u, s2 = (F.hi << 2) & 0x80000000u;
     const float mn = F.mn;
     const float xs = mem.x, xl = mem.y;
     const float tt = xl * xs;
     Q.a0 = F.a0;
     Q.a1 = F.a1;
     Q.a2 = F.a2;
-    Q.d0 = __uint_as_float(__float_as_uint(tt * F.sel0) ^ s0);  // 2 xl xs G (:64-70, :80)
-    Q.d1 = __uint_as_float(__float_as_uint(tt * F.sel1) ^ s1);
-    Q.d2 = __uint_as_float(__float_as_uint(tt * F.sel2) ^ s2);
+    Q.d0 = tt * F.sel0;  // 2 xl xs G (:64-70, :80), the sign q in sel
+    Q.d1 = tt * F.sel1;
+    Q.d2 = tt * F.sel2;
     cmax = max(cmax, __float_as_uint(mn));  // :88 -- unsat iff max mn >= 0.5
     asm volatile("" : "+v"(cmax));          // fold now: deferred, it would keep every tile's mn live
     const float dxs2 = (20.0f * (xs + 0.001f)) * (mn - 0.5f);  // 2 dxs (:84)
@@ -174,7 +211,7 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
 // t+2's first half -- independent, so they interleave -- while the writes and the gathers drain.
 // After the second tile of a pair (bar), the barrier orders the pair's dv updates against the next
 // pair's; inside a pair the same-wave order suffices (see the header).
-__device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &slot3, float2 &mem1, Pend &P, Front &Fn,
+__device__ __forceinline__ void tile_step(const Args &a, const Recs &R, SlotF &slot3, float2 &mem1, Pend &P, Front &Fn,
                                           Gath &Gn, int t, float h, float hh, uint32_t &cmax, Stamps &S, bool bar) {
     const float o0 = lds_f(P.a0 + DVC), o1 = lds_f(P.a1 + DVC), o2 = lds_f(P.a2 + DVC);
     lds_st(P.a0 + DVC, o0 + P.d0);
@@ -187,7 +224,7 @@ __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, Slot &sl
 #endif
     Gath G3;
     gather(slot3, G3);
-    slot3 = load_rec(R, t + 7);
+    slot3 = load_recf(R, t + 7);
     __builtin_amdgcn_sched_barrier(0);
     back(a, Fn, mem1, h, hh, P, cmax);  // P <- tile t+1's terms (tile t's were written above)
     front(Gn, Fn);                      // Fn <- tile t+2's first half
@@ -217,7 +254,7 @@ __device__ __forceinline__ uint32_t mem_addr(const Args &a, int lt, int lane) {
 // (tiles past the last one are empty): an early exit would join TR paths after the sequence, and
 // the copies that merge mr[] there double its VGPR footprint.
 template <int TR, int OFF, int T>
-__device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&mr)[TR], Slot (&ring)[4], Pend &P,
+__device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&mr)[TR], SlotF (&ring)[4], Pend &P,
                                          Front &Fn, Gath &Gn, float h, float hh, int lane, uint32_t &cmax, Stamps &S) {
     constexpr bool bar = ((T + OFF) & 1) != 0;  // wave-paired tiles: a barrier after the second of a pair
     if constexpr (T + 1 < TR) {
@@ -232,7 +269,7 @@ __device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&
 
 template <int TR, int OFF, int... Ts>
 __device__ __forceinline__ void reg_tiles(std::integer_sequence<int, Ts...>, const Args &a, const Recs &R,
-                                          float2 (&mr)[TR], Slot (&ring)[4], Pend &P, Front &Fn, Gath &Gn, float h,
+                                          float2 (&mr)[TR], SlotF (&ring)[4], Pend &P, Front &Fn, Gath &Gn, float h,
                                           float hh, int lane, uint32_t &cmax, Stamps &S) {
     (reg_tile<TR, OFF, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S), ...);
 }
@@ -241,24 +278,28 @@ __device__ __forceinline__ void reg_tiles(std::integer_sequence<int, Ts...>, con
 template <int TR, int OFF>
 __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, int lane, uint32_t &cmax, Stamps &S) {
     Recs R;
+#if ONCHIP_REC12
+    R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec12, 0, (int)a.rec12_bytes, 0x00020000);
+#else
     R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec, 0, (int)a.rec_bytes, 0x00020000);
-    R.voff = (uint32_t)lane * 8u;
+#endif
+    R.voff = (uint32_t)lane * RECF_BYTES;
     // an opaque zero per pass keeps the record loads inside the step loop (hoisted out of it they
     // would pin hundreds of VGPRs)
     R.soff = 0u;
     asm volatile("" : "+s"(R.soff));
     const float hh = 0.5f * h;
-    Slot ring[4];
+    SlotF ring[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) ring[s] = load_rec(R, s);
+    for (int s = 0; s < 4; ++s) ring[s] = load_recf(R, s);
     Pend P;
     Gath G0, G1, Gn;
     gather(ring[0], G0);
-    ring[0] = load_rec(R, 4);
+    ring[0] = load_recf(R, 4);
     gather(ring[1], G1);
-    ring[1] = load_rec(R, 5);
+    ring[1] = load_recf(R, 5);
     gather(ring[2], Gn);
-    ring[2] = load_rec(R, 6);
+    ring[2] = load_recf(R, 6);
     Front F0, Fn;
     front(G0, F0);
     front(G1, Fn);

@@ -59,6 +59,8 @@ constexpr int ADA_MAX_N = (int)(ADA_D / 4) - SINKS - ADA_FLAGS;
 struct Args {
     const uint64_t *rec; // [tiles][NTH] slot-major clause records (make_rec), padded with empty tiles
     uint32_t rec_bytes;
+    const uint32_t *rec12;  // ONCHIP_REC12: the same records in 12 bytes (make_rec12), [tiles][NTH][3]
+    uint32_t rec12_bytes;
     const int32_t *tc;   // wave starts: wave w of tile t holds internal clauses [tc[8t+w], tc[8t+w+1]) in
                          // its lanes 0.. (the rest of its slots are empty); padded with m to at least
                          // 8 (TR + tl) + 1 entries (constant memory reads at static offsets)
@@ -95,6 +97,18 @@ inline uint64_t make_rec(uint32_t a0, uint32_t a1, uint32_t a2, bool n0, bool n1
     const uint32_t lo = a0 | (a1 << 16);
     const uint32_t hi = a2 | (n0 ? 0x80000000u : 0u) | (n1 ? 0x40000000u : 0u) | (n2 ? 0x20000000u : 0u);
     return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+// 12-byte records (the fixed-step kernel; ONCHIP_REC12=0 builds the 8-byte form, A/B: 12 bytes are
+// ~2 % faster, profiles/r03_rec12_ab.txt): one word per literal, its 16-bit LDS
+// address and its sign at bit 31, so no literal's sign needs a shift (the adaptive kernel keeps the
+// 8-byte records: its registers have no room for three sign words per clause in flight)
+#ifndef ONCHIP_REC12
+#define ONCHIP_REC12 1
+#endif
+inline void make_rec12(uint32_t a0, uint32_t a1, uint32_t a2, bool n0, bool n1, bool n2, uint32_t *w) {
+    w[0] = a0 | (n0 ? 0x80000000u : 0u);
+    w[1] = a1 | (n1 ? 0x80000000u : 0u);
+    w[2] = a2 | (n2 ? 0x80000000u : 0u);
 }
 
 // Launch over replicas [0, G) on `stream`; tr must be one of TR_CHOICES, off (0 / 1) the pair offset
