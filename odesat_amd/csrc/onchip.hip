@@ -11,8 +11,9 @@
 // lane l owns clause slot l of every tile, so its memories form a per-lane array indexed by the
 // tile number.  The first TR tiles keep theirs in VGPRs (the tile sequence is expanded at compile
 // time, so the index is static), the remaining tiles in LDS next to v and dv.  A step then moves
-// no state through the memory hierarchy at all; the only per-step reads are the 8-byte literal
-// records (slot-major, L2-resident and shared by every CU).
+// no state through the memory hierarchy at all; the only per-step reads are the literal records
+// (slot-major, L2-resident and shared by every CU): 12 bytes per clause slot for fixed steps, one
+// word per literal (ONCHIP_REC12, onchip.hpp), 8 bytes for adaptive steps.
 //
 // Exactness of the short arithmetic (the host launches this kernel only on "in-range" states:
 // v in [-1, 1], xs in [-1, 1], xl in [1, 1e30], |zeta| <= 1e6 -- every state after one step is, by
@@ -91,11 +92,11 @@ struct Gath {  // a clause's gathered inputs: LDS byte addresses of its voltages
 };
 
 // The records are read with buffer loads: the resource (SGPRs) holds the base, the per-lane offset
-// lane * 8 is one VGPR for the whole launch and the tile offset t * 4096 is a scalar, so a ring
-// refill costs no vector instruction.
+// lane * (8 or 12) is one VGPR for the whole launch and the tile offset a scalar, so a ring refill
+// costs no vector instruction.
 struct Recs {
     __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t voff;  // lane * 8
+    uint32_t voff;  // lane * record bytes
     uint32_t soff;  // opaque 0 (see pass())
 };
 __device__ __forceinline__ Slot load_rec(const Recs &R, int t) {
