@@ -121,6 +121,10 @@ __device__ __forceinline__ float lds_f(uint32_t byte_addr) { return *reinterpret
 __device__ __forceinline__ void lds_st(uint32_t byte_addr, float x) { *reinterpret_cast<lfloat *>(byte_addr) = x; }
 typedef __attribute__((address_space(3))) float2 lfloat2;
 __device__ __forceinline__ float2 *lds_f2(uint32_t byte_addr) { return (float2 *)(reinterpret_cast<lfloat2 *>(byte_addr)); }
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) f4v lf4v;
+__device__ __forceinline__ f4v lds_f4(uint32_t byte_addr) { return *reinterpret_cast<const lf4v *>(byte_addr); }
+__device__ __forceinline__ void lds_st4(uint32_t byte_addr, f4v x) { *reinterpret_cast<lf4v *>(byte_addr) = x; }
 
 // The clause's three voltages (system.rs:46-48): LDS reads issued here, consumed by front().
 __device__ __forceinline__ void gather(const SlotF &S, Gath &G) {
@@ -692,7 +696,20 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
 #endif
         pass<TR, OFF>(a, mr, h, lane, cmax, S);
         if (!(__uint_as_float(cmax) < 0.5f)) lds_st(UNS + 4u * (k & 1), 1.0f);
-        for (int i = lane; i < a.n; i += NTH) {  // :96 (h dv = (h/2) dv2), dv restarts at 0 (:33)
+        // :96 (h dv = (h/2) dv2), dv restarts at 0 (:33): four variables per lane and access (v and dv
+        // are 16-byte aligned), then the n % 4 last ones
+        for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
+            const uint32_t o = 16u * (uint32_t)i4;
+            const f4v d2 = lds_f4(o + DVC);
+            lds_st4(o + DVC, f4v{0.0f, 0.0f, 0.0f, 0.0f});
+            f4v v = lds_f4(o);
+            v.x = __builtin_amdgcn_fmed3f(v.x + hh * d2.x, -1.0f, 1.0f);
+            v.y = __builtin_amdgcn_fmed3f(v.y + hh * d2.y, -1.0f, 1.0f);
+            v.z = __builtin_amdgcn_fmed3f(v.z + hh * d2.z, -1.0f, 1.0f);
+            v.w = __builtin_amdgcn_fmed3f(v.w + hh * d2.w, -1.0f, 1.0f);
+            lds_st4(o, v);
+        }
+        for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) {
             const float d2 = lds_f(4u * i + DVC);
             lds_st(4u * i + DVC, 0.0f);
             lds_st(4u * i, __builtin_amdgcn_fmed3f(lds_f(4u * i) + hh * d2, -1.0f, 1.0f));
@@ -712,7 +729,18 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     }
 
     float *Vo = (q ? a.v1 : a.v0) + (size_t)g * a.n;
-    for (int i = lane; i < a.n; i += NTH) st_state(&Vo[i], lds_f(4u * i));  // written by this lane in the last update
+    if (ADA) {
+        for (int i = lane; i < a.n; i += NTH) st_state(&Vo[i], lds_f(4u * i));  // written by this lane in the last update
+    } else {  // (the fixed update's lane ownership: four variables per lane, then the tail)
+        for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
+            const f4v v = lds_f4(16u * (uint32_t)i4);
+            st_state(&Vo[4 * i4], v.x);
+            st_state(&Vo[4 * i4 + 1], v.y);
+            st_state(&Vo[4 * i4 + 2], v.z);
+            st_state(&Vo[4 * i4 + 3], v.w);
+        }
+        for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) st_state(&Vo[i], lds_f(4u * i));
+    }
     {   // opaque copies: the store addresses are recomputed here instead of being kept live (two
         // VGPRs per tile) across the step loop from the loads above
         float2 *CMs = reinterpret_cast<float2 *>((q ? a.c1 : a.c0) + (size_t)g * a.m * 2);

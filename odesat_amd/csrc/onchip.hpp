@@ -19,7 +19,7 @@ constexpr int NTH = 512;           // threads per workgroup = tile capacity in c
 constexpr int WAVES = NTH / 64;    // slots [64 w, 64 w + 64) of a tile are wave w's
 constexpr int TILE_LDS = NTH * 8;  // LDS bytes of one LDS-resident tile of memories (float2 per lane)
 constexpr int SINKS = 32;          // sink words after v and after dv (empty slots of lane l use l % 32)
-constexpr uint32_t DVC = 65532;    // LDS byte offset of dv[0] from v[0]: the ds instructions' 16-bit
+constexpr uint32_t DVC = 65520;    // LDS byte offset of dv[0] from v[0], 16-byte aligned: the ds instructions' 16-bit
                                    // immediate offset, so one address VGPR serves v and dv
 constexpr int MAX_N = (int)(DVC / 4) - SINKS;  // v and its sinks below DVC
 constexpr size_t LDS_MAX = 160 * 1024;
