@@ -648,7 +648,22 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                         for (int i = lane; i < a.n; i += NTH) lds_st(4u * i + ADA_D, 0.0f);
                         break;
                     }
-                    for (int i = lane; i < a.n; i += NTH) {  // full-step clone and first half step (:124-128)
+                    // full-step clone and first half step (:124-128), four variables per LDS access
+                    // (A, D, H and F are 16-byte aligned), then the n % 4 last ones
+                    for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
+                        const uint32_t o = 16u * (uint32_t)i4;
+                        const f4v d2 = lds_f4(o + ADA_D), y = lds_f4(o);
+                        lds_st4(o + ADA_D, f4v{0.0f, 0.0f, 0.0f, 0.0f});
+                        f4v vf, vh;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            vf[u] = __builtin_amdgcn_fmed3f(y[u] + hhk * d2[u], -1.0f, 1.0f);
+                            vh[u] = __builtin_amdgcn_fmed3f(y[u] + hqk * d2[u], -1.0f, 1.0f);
+                        }
+                        lds_st4(o + ADA_F, vf);
+                        lds_st4(o + ADA_H, vh);
+                    }
+                    for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) {
                         const float d2 = lds_f(4u * i + ADA_D), y = lds_f(4u * i);
                         lds_st(4u * i + ADA_D, 0.0f);
                         lds_st(4u * i + ADA_F, __builtin_amdgcn_fmed3f(y + hhk * d2, -1.0f, 1.0f));
@@ -656,7 +671,21 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                     }
                     __syncthreads();
                 } else {
-                    for (int i = lane; i < a.n; i += NTH) {  // second half step (:130), max_error (:101-108)
+                    // second half step (:130), max_error (:101-108); the same lane ownership as the
+                    // final store below
+                    for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
+                        const uint32_t o = 16u * (uint32_t)i4;
+                        const f4v d2 = lds_f4(o + ADA_D), vh = lds_f4(o + ADA_H), vf = lds_f4(o + ADA_F);
+                        lds_st4(o + ADA_D, f4v{0.0f, 0.0f, 0.0f, 0.0f});
+                        f4v vn;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            vn[u] = __builtin_amdgcn_fmed3f(vh[u] + hqk * d2[u], -1.0f, 1.0f);
+                            e = fmaxf(e, fabsf(vf[u] - vn[u]));
+                        }
+                        lds_st4(o, vn);
+                    }
+                    for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) {
                         const float d2 = lds_f(4u * i + ADA_D);
                         lds_st(4u * i + ADA_D, 0.0f);
                         const float vn = __builtin_amdgcn_fmed3f(lds_f(4u * i + ADA_H) + hqk * d2, -1.0f, 1.0f);
@@ -729,18 +758,15 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     }
 
     float *Vo = (q ? a.v1 : a.v0) + (size_t)g * a.n;
-    if (ADA) {
-        for (int i = lane; i < a.n; i += NTH) st_state(&Vo[i], lds_f(4u * i));  // written by this lane in the last update
-    } else {  // (the fixed update's lane ownership: four variables per lane, then the tail)
-        for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
-            const f4v v = lds_f4(16u * (uint32_t)i4);
-            st_state(&Vo[4 * i4], v.x);
-            st_state(&Vo[4 * i4 + 1], v.y);
-            st_state(&Vo[4 * i4 + 2], v.z);
-            st_state(&Vo[4 * i4 + 3], v.w);
-        }
-        for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) st_state(&Vo[i], lds_f(4u * i));
+    // written by this lane in the last update (four variables per lane, then the tail)
+    for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
+        const f4v v = lds_f4(16u * (uint32_t)i4);
+        st_state(&Vo[4 * i4], v.x);
+        st_state(&Vo[4 * i4 + 1], v.y);
+        st_state(&Vo[4 * i4 + 2], v.z);
+        st_state(&Vo[4 * i4 + 3], v.w);
     }
+    for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) st_state(&Vo[i], lds_f(4u * i));
     {   // opaque copies: the store addresses are recomputed here instead of being kept live (two
         // VGPRs per tile) across the step loop from the loads above
         float2 *CMs = reinterpret_cast<float2 *>((q ? a.c1 : a.c0) + (size_t)g * a.m * 2);
