@@ -19,12 +19,16 @@ var, neg = wl.random_ksat(c["n"], c["m"], c["k"], c["seed"])
 cp, v_, n_ = wl.formula_arrays(var, neg)
 f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
 B, K, W = int(os.environ.get("B", "1024")), int(os.environ.get("STEPS", "20")), 5
-rows = {True: [], False: []}
+rows = {}
 for rep in range(int(os.environ.get("REPS", "4"))):
-    for prof in (True, False):
+    for prof, split in ((True, False), (True, True), (False, False)):
         with Solver(f, B, "f32") as s:
             s.init_state(42)
-            s.simulate(dt=0.01, max_steps=W, stop=ODESAT_STOP_NONE, poll_interval=W)
+            if split:  # the W warmup steps as W one-step launches
+                for _ in range(W):
+                    s.simulate(dt=0.01, max_steps=1, stop=ODESAT_STOP_NONE, poll_interval=1)
+            else:
+                s.simulate(dt=0.01, max_steps=W, stop=ODESAT_STOP_NONE, poll_interval=W)
             s.profile(prof)
             s.synchronize()
             t0 = time.perf_counter()
@@ -33,8 +37,8 @@ for rep in range(int(os.environ.get("REPS", "4"))):
             s.synchronize()
             t2 = time.perf_counter()
             kern = s.profile_read()[0][0] * 1e3 if prof else None
-            rows[prof].append({"wall": (t2 - t0) * 1e6, "call": (t1 - t0) * 1e6, "sync": (t2 - t1) * 1e6,
+            rows.setdefault((prof, split), []).append({"wall": (t2 - t0) * 1e6, "call": (t1 - t0) * 1e6, "sync": (t2 - t1) * 1e6,
                                "kernel": kern, "value_M": B * K / (t2 - t0) / 1e6})
-for prof, rs in rows.items():
+for (prof, split), rs in rows.items():
     med = {k: round(statistics.median([r[k] for r in rs]), 1) for k in rs[0] if rs[0][k] is not None}
-    print(json.dumps({"profile_events": prof, "median": med, "runs": [{k: (round(v, 1) if v else v) for k, v in r.items()} for r in rs]}))
+    print(json.dumps({"profile_events": prof, "warmup_split": split, "median": med, "runs": [{k: (round(v, 1) if v else v) for k, v in r.items()} for r in rs]}))
