@@ -64,6 +64,21 @@ __device__ __forceinline__ uint64_t memtime() {
 #else
 struct Stamps {};
 #endif
+// Diagnostic build only (-DONCHIP_PHASES): per workgroup, wave 0 records s_memrealtime (100 MHz)
+// at kernel start, after the state load (its barrier), after the step loop and at the end, into
+// g_onchip_phases[g][4] (read by odesat_onchip_phases).
+#ifdef ONCHIP_PHASES
+__device__ unsigned long long g_onchip_phases[4096 * 4];
+__device__ __forceinline__ uint64_t realtime() {
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#define ONCHIP_PHASE(i) \
+    do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_onchip_phases[blockIdx.x * 4 + (i)] = realtime(); } while (0)
+#else
+#define ONCHIP_PHASE(i) do {} while (0)
+#endif
 
 struct Slot {  // one lane's literal record for one tile
     uint32_t lo, hi;
@@ -584,6 +599,7 @@ template <int TR, int OFF, bool ADA>
 __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     const int g = blockIdx.x, lane = threadIdx.x;
     const int wl = lane & 63;  // slot of this lane in its wave's share of a tile
+    ONCHIP_PHASE(0);
     int act = a.act[g];
     if (!act) return;  // frozen replica (uniform)
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
@@ -627,6 +643,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     }
     if (lane < 2) lds_st(UNS + 4u * lane, 0.0f);
     __syncthreads();
+    ONCHIP_PHASE(1);
 
     const float h = a.dt, hh = 0.5f * a.dt;
     Stamps S{};
@@ -757,6 +774,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         }
     }
 
+    ONCHIP_PHASE(2);
     float *Vo = (q ? a.v1 : a.v0) + (size_t)g * a.n;
     // written by this lane in the last update (four variables per lane, then the tail)
     for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
@@ -788,6 +806,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         o[3] = S.tiles;
     }
 #endif
+    ONCHIP_PHASE(3);
     if (lane == 0) {
         if (a.oop) a.par[g] = (uint8_t)q;
         a.act[g] = (uint8_t)act;
@@ -837,6 +856,14 @@ hipError_t launch(int tr, int off, const Args &a, int G, size_t lds, hipStream_t
 // tiles} of the last launches (replicas < 4096, 16 wave slots each).
 extern "C" int odesat_onchip_stamps(unsigned long long *out, int count) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(onchip::g_onchip_stamps), sizeof(unsigned long long) * (size_t)count, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef ONCHIP_PHASES
+// Diagnostic build only: the per-workgroup phase stamps of the last launch (4096 x 4, s_memrealtime).
+extern "C" int odesat_onchip_phases(unsigned long long *out, int count) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(onchip::g_onchip_phases), sizeof(unsigned long long) * (size_t)count, 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
