@@ -8,6 +8,7 @@ import socket
 from types import SimpleNamespace
 
 import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TINY4 = dict(n=60, m=150, k=3, seed=11)    # replicas 6..11 are allsat first, at step 205 (rank 1 of 2 x 6)
@@ -42,12 +43,13 @@ def _worker(rank, world, port, out, per):
     td.destroy_process_group()
 
 
-def test_bench_multi_gpu_legs_two_rank_gloo(tmp_path):
+@pytest.mark.parametrize("world,per", [(2, 6), (4, 3)])
+def test_bench_multi_gpu_legs_gloo(tmp_path, world, per):
+    """World 2 and 4 (the same 12 replicas: the first allsat ones on rank 1, resp. ranks 2-3)."""
     import torch.multiprocessing as mp
 
     from odesat_amd import workloads as wl
     from oracle.oracle import Oracle, init_voltages
-    world, per = 2, 6
     out = str(tmp_path / "legs.json")
     mp.spawn(_worker, args=(world, _free_port(), out, per), nprocs=world, join=True)
     res = json.load(open(out))
