@@ -354,7 +354,9 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
 // half step from y's memories and that C (:124-128), and in pass 2 takes the second half step
 // (:130) and its max_error terms (:101-108).  The arithmetic is k_resident's / k_wave's in the
 // exact rewritten forms of the header (h dxs = (h/2) (2 dxs), (h/2) dxs = (h/4) (2 dxs), ...).
-// Empty slots (REC_EMPTY, onchip.hpp) compute on stand-in memories: their error terms are masked.
+// Empty slots compute on stand-in memories (0.001, 1): their literals sit at sink words (v = 1.0, so
+// mn = 0 in both passes), where xs = 0.001 and xl = 1 are fixed points of both clamped half steps and
+// of the full step -- so their error terms are exactly 0 and need no mask.
 
 struct GathA {  // a clause's gathered inputs: addresses, sign word, voltages from S and from A (y)
     uint32_t a0, a1, a2, hi;
@@ -432,8 +434,7 @@ __device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &me
         const float dxl2 = 2.5f * (mn - 0.1f);
         const float xs_n = __builtin_amdgcn_fmed3f(xs_t + hq * dxs2, 0.001f, 1.0f - 0.001f);
         const float xl_n = __builtin_amdgcn_fmed3f(xl_t + hh * dxl2, 1.0f, a.xl_max);
-        const float ee = fmaxf(e, fmaxf(fabsf(xs_f - xs_n), fabsf(xl_f - xl_n)));
-        e = (F.hi & REC_EMPTY) ? e : ee;
+        e = fmaxf(e, fmaxf(fabsf(xs_f - xs_n), fabsf(xl_f - xl_n)));
         mem.x = xs_n;
         mem.y = xl_n;
     }
@@ -468,8 +469,8 @@ __device__ __forceinline__ void reg_tileA(const Args &a, const Recs &R, float2 (
     constexpr bool bar = ((T + OFF) & 1) != 0 && T + 1 < TR;
     if constexpr (T + 1 < TR) {
         tile_stepA(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, hq, sb, p2, cmax, e, bar);
-    } else {  // the (empty) tile after the last: stand-in memories, nothing stored
-        float2 m = make_float2(0.0f, 0.0f);
+    } else {  // the (empty) tile after the last: stand-in memories (zero error terms), nothing stored
+        float2 m = make_float2(0.001f, 1.0f);
         tile_stepA(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, hq, sb, p2, cmax, e, bar);
     }
 }
@@ -554,6 +555,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mem_rsrc(float *base, int m) {
 // range check), any other empty slot reads the next tile's clause -- neither is used, since an
 // empty slot's literals point at the sink words (its terms go to the dv sinks) and its update is
 // not stored.
+// Adaptive launches: every empty slot of a register tile gets the stand-in memories (0.001, 1) (see
+// backA), once per launch.
+template <int TR, int... Js>
+__device__ __forceinline__ void mem_standins(std::integer_sequence<int, Js...>, const cint32 *tcw, int wl,
+                                             float2 (&mr)[TR]) {
+    auto one = [&](auto J) {
+        constexpr int j = decltype(J)::value;
+        const bool empty = wl >= tcw[j * WAVES + 1] - tcw[j * WAVES];
+        mr[j].x = empty ? 0.001f : mr[j].x;
+        mr[j].y = empty ? 1.0f : mr[j].y;
+    };
+    (one(std::integral_constant<int, Js>{}), ...);
+}
+
 template <int TR, int... Js>
 __device__ __forceinline__ void mem_load(std::integer_sequence<int, Js...>, const cint32 *tcw,
                                          __amdgpu_buffer_rsrc_t rs, uint32_t lane8, float2 (&mr)[TR]) {
@@ -637,6 +652,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     float2 mr[TR];
     mem_load<TR>(std::make_integer_sequence<int, TR>{}, tcw, mem_rsrc((p ? a.c1 : a.c0) + (size_t)g * a.m * 2, a.m),
                  8u * (uint32_t)wl, mr);
+    if constexpr (ADA) mem_standins<TR>(std::make_integer_sequence<int, TR>{}, tcw, wl, mr);
     for (int t = 0; t < a.tl; ++t) {
         const int c0 = tcw[(TR + t) * WAVES];
         *lds_f2(mem_addr(a, t, lane)) = ld_state(&CM[min(c0 + wl, mlast)]);  // (empty slots: as mem_io)
