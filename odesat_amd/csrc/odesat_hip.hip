@@ -778,9 +778,9 @@ template <typename T, bool ADA, int CPL, int VPL, bool FAST> int launch_solo_k(o
                            s->stream, a);
     } else {
         const size_t lds = (size_t)(s->n + s->L) * sizeof(T);
-        HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_solo<T, ADA, CPL, VPL, false>), (int)RES_LDS_MAX));
+        HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_solo<T, ADA, CPL, VPL>), (int)RES_LDS_MAX));
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_solo<T, ADA, CPL, VPL, false>), dim3((unsigned)s->G), dim3((unsigned)s->solo_nl), lds,
+        hipLaunchKernelGGL((k_solo<T, ADA, CPL, VPL>), dim3((unsigned)s->G), dim3((unsigned)s->solo_nl), lds,
                            s->stream, a);
     }
     HIP_TRY(hipGetLastError());

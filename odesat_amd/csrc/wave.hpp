@@ -443,55 +443,6 @@ template <typename T> __device__ __forceinline__ T solo_fold(const T *tL, int s,
     return dv;
 }
 
-// One clause on an in-range state (FAST): the exact short forms of onchip.hip's header, in T.
-//   * the value literal j's term selects (val_j != mn ? mn : sec) is min(val_k, val_l) over the
-//     other two literals, and the rigidity term R only adds a signed zero, which dv absorbs;
-//   * the terms are 2 x the reference's (q sel xl xs instead of 0.5 q sel xl xs: an exact scaling;
-//     the fold's sums scale with them), so the voltage update takes h/2 (:96);
-//   * C = mn / 2, so C < 0.25 <=> mn < 0.5, C - 0.25 = (mn - 0.5) / 2 and C - 0.05 = (mn - 0.1) / 2
-//     (0.05 is exactly 0.1 / 2 in binary32 and binary64): h dxs = (h/2) (20 (xs + eps) (mn - 0.5))
-//     and dxl = 2.5 (mn - 0.1), each product rounded as the reference rounds it.
-// PK as clause_math: W_FIXED updates the memories; W_ADA1 keeps y's memories and mn1 = 2 C1; W_ADA2
-// rebuilds the full-step clone and the first half step of the memories from mn1 (:124-128), takes
-// the RHS at the half step and the second half step (:130) with its max_error terms (:132).
-template <typename T, int PK>
-__device__ __forceinline__ bool solo_fast(const T (&v)[3], const uint32_t (&sg)[3], T &xs, T &xl, T &mn1, T h, T xl_max,
-                                          T (&d)[3], T &e) {
-    const T one = (T)1.0, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
-    const T hh = (T)0.5 * h, hq = (T)0.25 * h;
-    T xs_m = xs, xl_m = xl, xs_f = xs, xl_f = xl;
-    if (PK == W_ADA2) {
-        const T dxs1 = ((T)20.0 * (xs + eps)) * (mn1 - (T)0.5);  // 2 dxs (:84)
-        const T dxl1 = (T)2.5 * (mn1 - (T)0.1);                  // :85
-        xs_f = dmin(dmax(xs + hh * dxs1, eps), xs_hi);
-        xl_f = dmin(dmax(xl + h * dxl1, one), xl_max);
-        xs_m = dmin(dmax(xs + hq * dxs1, eps), xs_hi);
-        xl_m = dmin(dmax(xl + hh * dxl1, one), xl_max);
-    }
-    const T val0 = one - sflip(v[0], sg[0]), val1 = one - sflip(v[1], sg[1]), val2 = one - sflip(v[2], sg[2]);  // :47
-    const T sel0 = dmin(val1, val2), sel1 = dmin(val0, val2), sel2 = dmin(val0, val1);
-    const T mn = dmin(sel2, val2);  // :49-57
-    const T tt = xl_m * xs_m;
-    d[0] = sflip(tt * sel0, sg[0]);  // 2 xl xs G (:64-70, :80)
-    d[1] = sflip(tt * sel1, sg[1]);
-    d[2] = sflip(tt * sel2, sg[2]);
-    const T dxs = ((T)20.0 * (xs_m + eps)) * (mn - (T)0.5);  // 2 dxs (:84)
-    const T dxl = (T)2.5 * (mn - (T)0.1);                    // :85
-    if (PK == W_FIXED) {
-        xs = dmin(dmax(xs_m + hh * dxs, eps), xs_hi);  // :94-95
-        xl = dmin(dmax(xl_m + h * dxl, one), xl_max);
-    } else if (PK == W_ADA1) {
-        mn1 = mn;
-    } else {
-        const T xs_n = dmin(dmax(xs_m + hq * dxs, eps), xs_hi);  // second half step (:130)
-        const T xl_n = dmin(dmax(xl_m + hh * dxl, one), xl_max);
-        e = dmax(e, dmax(dabs(xs_f - xs_n), dabs(xl_f - xl_n)));  // :132
-        xs = xs_n;
-        xl = xl_n;
-    }
-    return PK != W_ADA2 && !(mn < (T)0.5);  // :88 (unsat)
-}
-
 // Diagnostic build only (-DSOLO_STAMPS, scripts/build_variant.sh ... odesat_hip): per wave, s_memtime
 // stamps split each fixed step into the clause pass, the first barrier, the fold and the closing
 // barrier; sums in g_solo_stamps (read by odesat_solo_stamps).  Each stamp drains the wave's LDS
@@ -517,7 +468,7 @@ __device__ __forceinline__ uint64_t solo_memtime() {
     } while (0)
 #endif
 
-template <typename T, bool ADAPTIVE, int CPL, int VPL, bool FAST>
+template <typename T, bool ADAPTIVE, int CPL, int VPL>
 __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char wave_smem[];
     using U = typename Bits<T>::U;
@@ -535,7 +486,6 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
     const T *CM = (p ? a.c1 : a.c0) + (size_t)g * a.m * 2;
     const int mlast = a.m - 1, nlast = a.n - 1;
     int lit[CPL][3], pos[CPL][3];
-    uint32_t sg[CPL][3];
     T xs[CPL], xl[CPL], C1[CPL];
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {  // records and memories of this lane's clauses (clamped: loadable)
@@ -544,8 +494,6 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
         lit[k][0] = r4.x & 0xffff, lit[k][1] = r4.y & 0xffff, lit[k][2] = r4.z & 0xffff;
         pos[k][0] = (int)((uint32_t)r4.x >> 16), pos[k][1] = (int)((uint32_t)r4.y >> 16);
         pos[k][2] = (int)((uint32_t)r4.z >> 16);
-#pragma unroll
-        for (int j = 0; j < 3; ++j) sg[k][j] = (lit[k][j] & 1) ? 0x80000000u : 0u;
         xs[k] = CM[2 * c];
         xl[k] = CM[2 * c + 1];
         C1[k] = (T)0.0;
@@ -579,10 +527,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
         for (int k = 0; k < CPL; ++k) {
             if (l + k * NL < a.m) {
                 T d[3];
-                if constexpr (FAST)
-                    uns = solo_fast<T, PK>(vv[k], sg[k], xs[k], xl[k], C1[k], h, a.xl_max, d, e) || uns;
-                else
-                    uns = clause_math<T, PK>(lit[k], vv[k], xs[k], xl[k], C1[k], h, a.zeta, a.xl_max, d, e) || uns;
+                uns = clause_math<T, PK>(lit[k], vv[k], xs[k], xl[k], C1[k], h, a.zeta, a.xl_max, d, e) || uns;
 #pragma unroll
                 for (int j = 0; j < 3; ++j) tL[pos[k][j]] = d[j];
             }
@@ -608,8 +553,6 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
         for (int j = 0; j < SOLO_MAX_NL / 256; ++j) r |= r4[j].x | r4[j].y | r4[j].z | r4[j].w;
         return r != 0;
     };
-    // FAST: the terms are twice the reference's, so each h below is halved (exact)
-    constexpr T SC = FAST ? (T)0.5 : (T)1.0;
 #ifdef SOLO_STAMPS
     uint64_t st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = solo_memtime();
@@ -625,7 +568,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
             __syncthreads();  // the terms (and the votes) before the fold
             SOLO_STAMP(1);
             uns = votes(k);
-            const T hv = SC * h;
+            const T hv = h;
 #pragma unroll
             for (int j = 0; j < VPL; ++j)
                 if (l + j * NL < a.n) {
@@ -638,7 +581,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
             __syncthreads();
             uns = votes(k);
             go = uns;  // an allsat replica takes no step (:122)
-            const T half = (T)0.5 * h, hf = SC * h, hh = SC * half;
+            const T half = (T)0.5 * h, hf = h, hh = half;
             if (go) {
 #pragma unroll
                 for (int j = 0; j < VPL; ++j)
@@ -745,7 +688,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
     };
     __shared__ U errM[2];  // per step parity: the max_error bits of the step (the waves' LDS atomic max)
     __shared__ __attribute__((aligned(16))) int voteW[2][SOLO_MAX_NL / 64];
-    const int NL = (int)blockDim.x, l = (int)threadIdx.x, TW = NL / 64;
+    const int NL = (int)blockDim.x, l = (int)threadIdx.x;
     const int g = blockIdx.x;
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
     if (g >= a.G || a.act[g] == 0) return;                              // uniform per workgroup

@@ -43,3 +43,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/rocprof" -o run --ou
     python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu --profile-dir "$OUT/profile" \
     > "$OUT/rocprof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$OUT/rocprof.log"; exit 1; }
 echo "rocprof ok"
+cd "$ROOT"
+timeout -k 10 300 python -u scripts/bench_criterion.py > "$OUT/criterion.jsonl" 2>/dev/null || { echo "criterion failed"; exit 1; }
+echo "criterion ok"
+timeout -k 10 300 python -u scripts/bench_configs.py --configs config3,config3f --no-cpu > "$OUT/configs3.jsonl" 2>/dev/null || { echo "configs failed"; exit 1; }
+echo "configs ok"
