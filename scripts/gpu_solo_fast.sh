@@ -1,6 +1,6 @@
 #!/bin/bash
 # k_solo_fast -- parity suites (fuzz: every path, k_solo general and fast), then the criterion
-# benches, the product against the previous build (expt/libold.so), alternated.
+# benches, the product against the previous build (expt/libold.so), alternated, and a lane sweep.
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -11,4 +11,7 @@ tail -2 gpurun_out/solo_tests.log
 for r in 1 2; do
   echo "== new"; timeout -k 10 300 python -u scripts/bench_criterion.py --no-cpu 2>/dev/null || exit 1
   echo "== old"; ODESAT_LIB=$PWD/expt/libold.so timeout -k 10 300 python -u scripts/bench_criterion.py --no-cpu 2>/dev/null || exit 1
+done
+for nl in ${SWEEP:-}; do
+  echo "== lanes $nl"; ODESAT_SOLO_LANES=$nl timeout -k 10 300 python -u scripts/bench_criterion.py --no-cpu --calls 3 2>/dev/null || exit 1
 done
