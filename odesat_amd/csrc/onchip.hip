@@ -631,27 +631,49 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     int64_t sat = a.sat_step[g], done = a.steps_done[g];
     const cint32 *tcw = (const cint32 *)a.tc + __builtin_amdgcn_readfirstlane(lane >> 6);  // this wave's starts
 
-    {   // v (sinks = 1.0) into LDS, dv = 0 (:33): the loads of a pass issued together, then the stores
-        constexpr int U = 16;
-        for (int i0 = lane; i0 < n2; i0 += NTH * U) {
-            float x[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) x[u] = ld_state(&V[min(i0 + u * NTH, a.n - 1)]);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int i = i0 + u * NTH;
-                if (i < n2) {
-                    lds_st(4u * i, i < a.n ? x[u] : 1.0f);
-                    lds_st(4u * i + DV, 0.0f);
-                    if (ADA && i >= a.n) lds_st(4u * i + ADA_H, 1.0f);  // H's sinks (pass 2 gathers them)
-                }
-            }
-        }
-    }
+    // The clause memories first: their loads (one per register tile and lane) stay in flight while v
+    // streams into LDS behind them.
     const int mlast = a.m - 1;
     float2 mr[TR];
     mem_load<TR>(std::make_integer_sequence<int, TR>{}, tcw, mem_rsrc((p ? a.c1 : a.c0) + (size_t)g * a.m * 2, a.m),
                  8u * (uint32_t)wl, mr);
+    {   // v (sinks = 1.0) into LDS, dv = 0 (:33): the loads of a pass issued together, then the stores
+        if ((a.n & 3) == 0) {  // 16 bytes per access (V, v, dv and H are 16-byte aligned; n + SINKS % 4 == 0)
+            constexpr int U = 4;
+            const int n4 = n2 >> 2, nv4 = a.n >> 2;
+            for (int q0 = lane; q0 < n4; q0 += NTH * U) {
+                f4v x[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) x[u] = ld_state(reinterpret_cast<const f4v *>(V) + min(q0 + u * NTH, nv4 - 1));
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int q = q0 + u * NTH;
+                    if (q < n4) {
+                        const f4v one4 = {1.0f, 1.0f, 1.0f, 1.0f};
+                        lds_st4(16u * q, q < nv4 ? x[u] : one4);
+                        lds_st4(16u * q + DV, f4v{0.0f, 0.0f, 0.0f, 0.0f});
+                        if (ADA && q >= nv4) lds_st4(16u * q + ADA_H, one4);  // H's sinks (pass 2 gathers them)
+                    }
+                }
+            }
+        } else {
+            constexpr int U = 16;
+            for (int i0 = lane; i0 < n2; i0 += NTH * U) {
+                float x[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) x[u] = ld_state(&V[min(i0 + u * NTH, a.n - 1)]);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int i = i0 + u * NTH;
+                    if (i < n2) {
+                        lds_st(4u * i, i < a.n ? x[u] : 1.0f);
+                        lds_st(4u * i + DV, 0.0f);
+                        if (ADA && i >= a.n) lds_st(4u * i + ADA_H, 1.0f);  // H's sinks (pass 2 gathers them)
+                    }
+                }
+            }
+        }
+    }
     if constexpr (ADA) mem_standins<TR>(std::make_integer_sequence<int, TR>{}, tcw, wl, mr);
     for (int t = 0; t < a.tl; ++t) {
         const int c0 = tcw[(TR + t) * WAVES];
