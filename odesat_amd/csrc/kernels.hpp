@@ -1047,4 +1047,39 @@ __global__ void k_reset_replicas(uint8_t *act, uint32_t *unsat, int64_t *sat_ste
     else ((float *)dtr)[r] = 0.01f;
 }
 
+// The exact short forms of one 3-SAT clause on in-range states (the FAST launches of k_resident,
+// k_wave, k_solo_fast; onchip.hip's header states the exactness argument).
+// q v for q = -1 / +1: the sign bit of v flipped by the literal's sign word (0x80000000 or 0), on the
+// high dword in f64
+template <typename T> __device__ __forceinline__ T sflip(T x, uint32_t sg) {
+    if constexpr (sizeof(T) == 8) {
+        return __longlong_as_double((long long)((unsigned long long)__double_as_longlong(x) ^ ((unsigned long long)sg << 32)));
+    } else {
+        return __uint_as_float(__float_as_uint(x) ^ sg);
+    }
+}
+
+// the terms (2 x the reference's) of one clause at voltages v, memories product tt; returns mn
+template <typename T>
+__device__ __forceinline__ T solo_terms(const T (&v)[3], const uint32_t (&sg)[3], T tt, T (&d)[3]) {
+    const T one = (T)1.0;
+    const T val0 = one - sflip(v[0], sg[0]), val1 = one - sflip(v[1], sg[1]), val2 = one - sflip(v[2], sg[2]);  // :47
+    const T sel0 = dmin(val1, val2), sel1 = dmin(val0, val2), sel2 = dmin(val0, val1);
+    d[0] = sflip(tt * sel0, sg[0]);  // 2 xl xs G (:64-70, :80)
+    d[1] = sflip(tt * sel1, sg[1]);
+    d[2] = sflip(tt * sel2, sg[2]);
+    return dmin(sel2, val2);  // :49-57
+}
+
+// one memory step of length hx from (xs, xl) with the clause's mn: xs + hx/2 * (2 dxs), xl + hx * dxl
+// (:84-85, :94-95; hx2 = hx / 2)
+template <typename T>
+__device__ __forceinline__ void solo_mem(T xs, T xl, T mn, T hx2, T hx, T xl_max, T &xs_o, T &xl_o) {
+    const T eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
+    const T dxs = ((T)20.0 * (xs + eps)) * (mn - (T)0.5);  // 2 dxs
+    const T dxl = (T)2.5 * (mn - (T)0.1);
+    xs_o = dmin(dmax(xs + hx2 * dxs, eps), xs_hi);
+    xl_o = dmin(dmax(xl + hx * dxl, (T)1.0), xl_max);
+}
+
 }  // namespace odk

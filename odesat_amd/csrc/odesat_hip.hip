@@ -71,6 +71,7 @@ struct odesat_solver {
     int solo_nl = 64, solo_cpl = 1, solo_vpl = 1;  // k_solo: lanes per replica, clause / variable slots per lane
     bool solo_fast = true;      // k_solo's short arithmetic on in-range states (ODESAT_SOLO_FAST=0: the general form)
     bool wave_fast = true;      // k_wave's likewise (ODESAT_WAVE_FAST=0)
+    bool res_fast = true;       // k_resident's likewise, 3-SAT only (ODESAT_RES_FAST=0)
     int wv_tw = 1;              // k_wave: waves per replica, fixed steps
     int wv_tw_ada = 1;          // ... adaptive steps (four barriers per step instead of two: at most 4)
     bool res_ada = false; // adaptive steps run k_resident (else FUSED on the same layout)
@@ -742,14 +743,14 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
     return ODESAT_OK;
 }
 
-template <typename T, int R, bool ADA, bool K3, int NTHR = ResShape<R>::NTH, bool VFG = false>
+template <typename T, int R, bool ADA, bool K3, int NTHR = ResShape<R>::NTH, bool VFG = false, bool FAST = false>
 int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     const size_t lds = res_lds_bytes(s->n, R, sizeof(T), ADA && !VFG);
-    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR, VFG>),
+    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR, VFG, FAST>),
                                    (int)RES_LDS_MAX));
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR, VFG>), dim3(s->G), dim3(NTHR), lds, s->stream, a);
+        hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR, VFG, FAST>), dim3(s->G), dim3(NTHR), lds, s->stream, a);
     }
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
@@ -891,24 +892,35 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
     a.xl_max = (T)1e4 * (T)s->m;  // system.rs:95
     a.tol = tol;
     const bool k3 = s->uniform_k == 3;
+    // 3-SAT on in-range states: the short arithmetic (res_clause3's FAST forms)
+    const bool f3 = k3 && fast && s->res_fast;
     if (adaptive && s->res_vfg) {  // R = 1: the full-step clone in HBM
         if (s->res_narrow)
-            return k3 ? launch_resident_k<T, 1, true, true, RES_NARROW, true>(s, a)
-                      : launch_resident_k<T, 1, true, false, RES_NARROW, true>(s, a);
-        return k3 ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true>(s, a)
-                  : launch_resident_k<T, 1, true, false, ResShape<1>::NTH, true>(s, a);
+            return f3   ? launch_resident_k<T, 1, true, true, RES_NARROW, true, true>(s, a)
+                   : k3 ? launch_resident_k<T, 1, true, true, RES_NARROW, true>(s, a)
+                        : launch_resident_k<T, 1, true, false, RES_NARROW, true>(s, a);
+        return f3   ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true>(s, a)
+               : k3 ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true>(s, a)
+                    : launch_resident_k<T, 1, true, false, ResShape<1>::NTH, true>(s, a);
     }
     if (s->res_narrow) {
         if (adaptive)
-            return k3 ? launch_resident_k<T, 1, true, true, RES_NARROW>(s, a)
-                      : launch_resident_k<T, 1, true, false, RES_NARROW>(s, a);
-        return k3 ? launch_resident_k<T, 1, false, true, RES_NARROW>(s, a)
-                  : launch_resident_k<T, 1, false, false, RES_NARROW>(s, a);
+            return f3   ? launch_resident_k<T, 1, true, true, RES_NARROW, false, true>(s, a)
+                   : k3 ? launch_resident_k<T, 1, true, true, RES_NARROW>(s, a)
+                        : launch_resident_k<T, 1, true, false, RES_NARROW>(s, a);
+        return f3   ? launch_resident_k<T, 1, false, true, RES_NARROW, false, true>(s, a)
+               : k3 ? launch_resident_k<T, 1, false, true, RES_NARROW>(s, a)
+                    : launch_resident_k<T, 1, false, false, RES_NARROW>(s, a);
     }
     auto go = [&](auto rr) -> int {
-        constexpr int R = decltype(rr)::value;
-        if (adaptive) return k3 ? launch_resident_k<T, R, true, true>(s, a) : launch_resident_k<T, R, true, false>(s, a);
-        return k3 ? launch_resident_k<T, R, false, true>(s, a) : launch_resident_k<T, R, false, false>(s, a);
+        constexpr int R = decltype(rr)::value, NT = ResShape<R>::NTH;
+        if (adaptive)
+            return f3   ? launch_resident_k<T, R, true, true, NT, false, true>(s, a)
+                   : k3 ? launch_resident_k<T, R, true, true>(s, a)
+                        : launch_resident_k<T, R, true, false>(s, a);
+        return f3   ? launch_resident_k<T, R, false, true, NT, false, true>(s, a)
+               : k3 ? launch_resident_k<T, R, false, true>(s, a)
+                    : launch_resident_k<T, R, false, false>(s, a);
     };
     switch (s->res_R) {
         case 1: return go(IC<1>{});
@@ -1395,6 +1407,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
         s->res_R = res_r;
         s->res_ada = res_fits(n, res_r, s->tsize, true);
+        if (const char *ev = std::getenv("ODESAT_RES_FAST")) s->res_fast = std::atoi(ev) != 0;
         // adaptive steps whose clone of v does not fit beside v and dv (f64 at n > 6.7 k, the CLI's
         // default precision and mode on config 2): k_resident with the clone in HBM instead of FUSED
         // on the one-replica layout.  ODESAT_RES_VFG=0 keeps FUSED.

@@ -192,12 +192,55 @@ template <typename T> struct Pend {
 // One 3-SAT clause of tile t from its prefetched loads: C, the memories' update and the three dv
 // terms (system.rs:43-88).  Voltages are read-only during a pass, so this runs one tile ahead of
 // the dv updates.
-template <typename T, int R, int PK>
+template <typename T, int R, int PK, bool FAST = false>
 __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t,
                                             const TileLoad<T> &ld, Pend<T> &P, bool on, T h, bool &uns, T &e,
                                             bool copy) {
     P.ok = ld.ok;
     if (!ld.ok) return;
+    if constexpr (FAST) {
+        // On in-range states (the host's `fast` launches) the exact short forms of k_solo_fast
+        // (kernels.hpp solo_terms): each term tt min(other two values) with the literal's sign, R omitted,
+        // 2 x the reference's terms (the variable phases halve h), the memory update from mn
+        // (solo_mem); the first adaptive pass keeps mn (= 2 C) in the C scratch.
+        const int c = ldc(a.tc, t) + x.lc;
+        const int lit[3] = {ld.lit.x, ld.lit.y, ld.lit.z};
+        T v[3];
+        uint32_t sg[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            P.idx[j] = (lit[j] >> 1) * R + x.r;
+            sg[j] = (uint32_t)lit[j] << 31;
+            v[j] = x.vL[P.idx[j]];
+        }
+        const uint32_t ci = (uint32_t)(c * R + x.r) * 2u;
+        const T hh = (T)0.5 * h, hq = (T)0.25 * h;
+        T xs = ld.mem.e[0], xl = ld.mem.e[1], xs_f = xs, xl_f = xl;
+        if (PK == P_ADA2) {  // y's memories -> the full-step clone and the first half step (:124-128)
+            const T mn1 = ld.full.e[0];
+            solo_mem<T>(xs, xl, mn1, hh, h, a.xl_max, xs_f, xl_f);
+            solo_mem<T>(ld.mem.e[0], ld.mem.e[1], mn1, hq, hh, a.xl_max, xs, xl);
+        }
+        const T mn = solo_terms<T>(v, sg, xl * xs, P.d);
+        if (PK != P_ADA2) uns = uns || (on && !(mn < (T)0.5));  // :88
+        if (!on) {
+            if (PK == P_FIXED && copy) stv<T, 2>(at(CM, ci), ld.mem);
+            return;
+        }
+        if (PK == P_FIXED) {
+            Vec<T, 2> o;
+            solo_mem<T>(xs, xl, mn, hh, h, a.xl_max, o.e[0], o.e[1]);
+            res_stm<T>(at(CM, ci), o);
+        } else if (PK == P_ADA1) {
+            *at(x.cf, ci / 2u) = mn;
+        } else {
+            Vec<T, 2> o;
+            solo_mem<T>(xs, xl, mn, hq, hh, a.xl_max, o.e[0], o.e[1]);  // second half step (:130)
+            e = dmax(e, dmax(dabs(xs_f - o.e[0]), dabs(xl_f - o.e[1])));  // :132
+            stv<T, 2>(at(CM, ci), o);
+        }
+        return;
+    }
     const T one = (T)1.0, halfc = (T)0.5;
     const int c = ldc(a.tc, t) + x.lc;
     const int lit[3] = {ld.lit.x, ld.lit.y, ld.lit.z};
@@ -288,11 +331,11 @@ __device__ __forceinline__ void res_clause_any(const RArgs<T> &a, const ResCtx<T
 // One step of the 3-SAT tile pipeline: the terms of tile t+1 are computed from slot S (which is
 // then refilled with tile t+1+RES_DEPTH), tile t's terms P are applied to dv, barrier (tile t+1
 // may touch the same dv entries).
-template <typename T, int R, int PK>
+template <typename T, int R, int PK, bool FAST = false>
 __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, int t,
                                           TileLoad<T> &S, Pend<T> &P, bool on, T h, bool &uns, T &e) {
     Pend<T> Q;
-    res_clause3<T, R, PK>(a, x, CM, t + 1, S, Q, on, h, uns, e, CMr != CM);  // Q.ok = false past the last tile
+    res_clause3<T, R, PK, FAST>(a, x, CM, t + 1, S, Q, on, h, uns, e, CMr != CM);  // Q.ok = false past the last tile
     res_apply3<T, R>(x, P);
     res_load3<T, R, PK>(a, x, CMr, t + 1 + res_depth<T>(), S);
 #ifdef RES_TIMING_PAIRS  // timing-only diagnostic build (results race): a barrier after odd tiles only
@@ -304,7 +347,7 @@ __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> 
 
 // One RHS pass over all tiles: dv (LDS) accumulates; memories are read from CMr (or the adaptive
 // scratch) and written by kind (P_FIXED: to CM).  Ends with a barrier (dv complete).
-template <typename T, int R, int PK, bool K3>
+template <typename T, int R, int PK, bool K3, bool FAST = false>
 __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, bool on, T h,
                                          bool &uns, T &e) {
     const int NT_ = a.ntiles;
@@ -321,17 +364,17 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
         Pend<T> P;
 #pragma unroll
         for (int i = 0; i < D; ++i) res_load3<T, R, PK>(a, x, CMr, i, b[i]);
-        res_clause3<T, R, PK>(a, x, CM, 0, b[0], P, on, h, uns, e, CMr != CM);
+        res_clause3<T, R, PK, FAST>(a, x, CM, 0, b[0], P, on, h, uns, e, CMr != CM);
         res_load3<T, R, PK>(a, x, CMr, D, b[0]);
         int t0 = 0;
         for (; t0 + D <= NT_; t0 += D) {  // iteration t computes tile t+1 from slot (t+1) % D
 #pragma unroll
-            for (int i = 0; i < D; ++i) res_iter3<T, R, PK>(a, x, CMr, CM, t0 + i, b[(i + 1) % D], P, on, h, uns, e);
+            for (int i = 0; i < D; ++i) res_iter3<T, R, PK, FAST>(a, x, CMr, CM, t0 + i, b[(i + 1) % D], P, on, h, uns, e);
         }
         if constexpr (D == 8) {
             if (t0 < NT_) {  // four tiles left: slots 1 .. 4
 #pragma unroll
-                for (int i = 0; i < 4; ++i) res_iter3<T, R, PK>(a, x, CMr, CM, t0 + i, b[i + 1], P, on, h, uns, e);
+                for (int i = 0; i < 4; ++i) res_iter3<T, R, PK, FAST>(a, x, CMr, CM, t0 + i, b[i + 1], P, on, h, uns, e);
             }
         }
     } else {
@@ -349,8 +392,11 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
 // the clone lives in HBM (a.vf, the replica's own n words), written and read back by the same thread
 // in the two variable phases of a step -- 2 n words of traffic per replica-step on top of the memories.
 constexpr int RES_NARROW = 64;
-template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR, bool VFG = false>
+// FAST (3-SAT, in-range states): res_clause3's short forms; the terms are 2 x the reference's, so every
+// h of the variable phases is halved.
+template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR, bool VFG = false, bool FAST = false>
 __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
+    static_assert(!FAST || K3, "the short forms are 3-SAT only (res_clause_any has none)");
     extern __shared__ __attribute__((aligned(16))) unsigned char res_smem[];
     using U = typename Bits<T>::U;
     constexpr int NTH = NTHR, NL = NTHR / R;
@@ -407,14 +453,15 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
         bool uns = false;
         T e = (T)0.0;
         if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154)
-            res_pass<T, R, P_FIXED, K3>(a, x, CMr, CMo, on, h, uns, e);
+            res_pass<T, R, P_FIXED, K3, FAST>(a, x, CMr, CMo, on, h, uns, e);
             CMr = CMo;
             if (uns) unsL[x.r] = 1u;
+            const T hv = FAST ? (T)0.5 * h : h;
             for (int i = x.lc; i < a.n; i += NL) {  // :96, dv restarts at 0 (:33)
                 const int idx = i * R + x.r;
                 const T d = x.dvL[idx];
                 x.dvL[idx] = (T)0.0;
-                if (on) x.vL[idx] = dmin(dmax(x.vL[idx] + h * d, (T)-1.0), (T)1.0);
+                if (on) x.vL[idx] = dmin(dmax(x.vL[idx] + hv * d, (T)-1.0), (T)1.0);
             }
             __syncthreads();
             if (tid < R && act) {
@@ -426,18 +473,18 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
                 }
             }
         } else {  // euler_step (system.rs:111-139), per-replica dt
-            res_pass<T, R, P_ADA1, K3>(a, x, CM, CM, on, h, uns, e);
+            res_pass<T, R, P_ADA1, K3, FAST>(a, x, CM, CM, on, h, uns, e);
             if (uns) unsL[x.r] = 1u;
             __syncthreads();
             const bool st = on && unsL[x.r] != 0u;  // allsat replicas take no step (:122)
-            const T half = (T)0.5 * h;
+            const T half = FAST ? (T)0.25 * h : (T)0.5 * h, hf = FAST ? (T)0.5 * h : h;
             for (int i = x.lc; i < a.n; i += NL) {
                 const int idx = i * R + x.r;
                 const T d = x.dvL[idx];
                 x.dvL[idx] = (T)0.0;
                 if (st) {
                     const T v = x.vL[idx];
-                    x.vfL[idx] = dmin(dmax(v + h * d, (T)-1.0), (T)1.0);    // full-step clone
+                    x.vfL[idx] = dmin(dmax(v + hf * d, (T)-1.0), (T)1.0);   // full-step clone
                     x.vL[idx] = dmin(dmax(v + half * d, (T)-1.0), (T)1.0);  // first half step
                 }
             }
@@ -447,7 +494,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
             for (int j = 0; j < R; ++j) any_st = any_st || (actL[j] != 0 && unsL[j] != 0u);
             if (any_st) {  // uniform
                 bool u2 = false;
-                res_pass<T, R, P_ADA2, K3>(a, x, CM, CM, st, h, u2, e);
+                res_pass<T, R, P_ADA2, K3, FAST>(a, x, CM, CM, st, h, u2, e);
                 for (int i = x.lc; i < a.n; i += NL) {
                     const int idx = i * R + x.r;
                     const T d = x.dvL[idx];

@@ -90,6 +90,13 @@ def variants(prec, uniform3, distinct):
         # k_solo's general arithmetic (the fast kernel, k_solo_fast, is the default on in-range states)
         v.append(("solo-general", {"ODESAT_WAVE": "1", "ODESAT_SOLO": "1", "ODESAT_SOLO_FAST": "0"},
                   _lib.ODESAT_ALG_RESIDENT))
+        # k_resident on 3-SAT (ODESAT_WAVE=0: its short forms on in-range states, and the general
+        # arithmetic with ODESAT_RES_FAST=0)
+        for lab, extra in (("r1", {"ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "0"}),
+                           ("narrow", {"ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "1"}),
+                           ("r4", {"ODESAT_GROUP_WIDTH": "4"}),
+                           ("general", {"ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "0", "ODESAT_RES_FAST": "0"})):
+            v.append((f"resident-k3-{lab}", {"ODESAT_WAVE": "0", **extra}, _lib.ODESAT_ALG_RESIDENT))
         if prec == "f32" and distinct:
             v.append(("onchip", {"ODESAT_WAVE": "0", "ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "0"},
                       _lib.ODESAT_ALG_ONCHIP))
@@ -166,7 +173,7 @@ def test_fuzz_every_path_matches_oracle(seed, prec):
 
 def test_fuzz_covered_every_path():
     """The cases above reached every kernel family: FUSED (W = 64 and 8), TWOPASS, the RESIDENT
-    tile kernels (512-lane, one-wave and R = 4 tiles), k_wave with teams of 1, 2 and 4 waves, k_solo
+    tile kernels (512-lane, one-wave and R = 4 tiles; on 3-SAT in their short and general forms), k_wave with teams of 1, 2 and 4 waves, k_solo
     with teams of 64, 128 and the default lanes (k_solo_fast) and in its general form, and ONCHIP."""
     if not COVERED:
         pytest.skip("run together with test_fuzz_every_path_matches_oracle")
@@ -177,7 +184,9 @@ def test_fuzz_covered_every_path():
             ("wave-t4", _lib.ODESAT_ALG_RESIDENT), ("onchip", _lib.ODESAT_ALG_ONCHIP),
             ("solo-l64", _lib.ODESAT_ALG_RESIDENT), ("solo-l128", _lib.ODESAT_ALG_RESIDENT),
             ("solo-l0", _lib.ODESAT_ALG_RESIDENT), ("solo-general", _lib.ODESAT_ALG_RESIDENT),
-            ("wave-general", _lib.ODESAT_ALG_RESIDENT)]
+            ("wave-general", _lib.ODESAT_ALG_RESIDENT), ("resident-k3-r1", _lib.ODESAT_ALG_RESIDENT),
+            ("resident-k3-narrow", _lib.ODESAT_ALG_RESIDENT), ("resident-k3-r4", _lib.ODESAT_ALG_RESIDENT),
+            ("resident-k3-general", _lib.ODESAT_ALG_RESIDENT)]
     print(sorted(COVERED.items()))
     missing = [k for k in need if COVERED.get(k, 0) < 4]
     assert not missing, (missing, COVERED)
