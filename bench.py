@@ -9,12 +9,15 @@ Multi-GPU: `python bench.py --gpus N` starts N ranks itself (torch.distributed.r
 GPU) when WORLD_SIZE is unset; under the driver's own `torch.distributed.run --nproc-per-node N` the
 ranks are already there.  Each rank steps its own B replicas (global replica index rank*B + b) with
 no collective in the data path -- weak scaling; barrier + max-over-ranks timing via
-torch.distributed (RCCL).
+torch.distributed (RCCL): a timed region opens after sync + barrier and closes at this rank's device
+sync, BEFORE the closing barrier, so no collective's latency is inside it.
 
 Beside the headline, the same JSON line carries one object per further leg, each timed
 the same way (barrier + device sync around K steps, max over ranks) with its own roofline:
   f64            config 2, B=1024, fixed step in the reference's own precision (the CLI default dtype)
   adaptive       config 2, B=1024, adaptive step tol 1e-3 (the reference's default mode, system.rs:111-139)
+  f64_adaptive   config 2, B=1024, f64 and adaptive steps together (the reference CLI's defaults)
+  config3        BASELINE configs[2]: uf250-1065-style n=250 m=1065, adaptive tol 1e-3, B=1024 (k_wave)
   inter          config 2 under STOP_ANY (simulate_inter)
   inter_config4  config 4 (n=50k, m=210k), B=1024 per rank, the sharded inter protocol
                  (sharding.run_inter: lock-step chunks, MIN all-reduce of the stop step, rollback) --
@@ -47,9 +50,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level
 # VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles per SIMD (SIMD-32),
 # at the 2.4 GHz max clock (MI355X_MICROARCH.md, wave scheduling / chip-level parameters)
 VALU_PEAK_GINST = 1024 * 2.4e9 / 2 / 1e9
-LEGS = ("f64", "adaptive", "f64_adaptive", "inter", "config4", "config5", "extra", "ab")
+# LDS instruction issue: one LDS (DS) wave instruction per CU per cycle at 2.4 GHz (an upper bound: a
+# wave64 DS access of 4-byte words moves 256 B, two cycles of the 128 B/clk LDS, MI355X_MICROARCH.md)
+LDS_PEAK_GINST = 256 * 2.4e9 / 1e9
+LEGS = ("f64", "adaptive", "f64_adaptive", "config3", "inter", "config4", "config5", "extra", "ab")
 CLAUSES_TOL = 1e-5       # the CLAUSES partitions' stated tolerance against a world-1 run
 DIGEST_REPLICAS = 4      # inter_config4: replicas per rank re-integrated by rank 0
+WATCHDOG_EXIT = 3        # exit status of a job ended by the leg watchdog (after rank 0 printed its line)
 
 
 def parse():
@@ -165,24 +172,44 @@ def dist_setup(args):
             local %= max(1, ndev)
             if ndev > 0:
                 torch.cuda.set_device(local)
-        td.init_process_group(backend=backend)
+        if backend == "nccl":  # bind the communicator to this rank's GPU (no guessing from the rank)
+            td.init_process_group(backend=backend, device_id=torch.device("cuda", local))
+        else:
+            td.init_process_group(backend=backend)
         dist = td
     elif args.gpus != 1:
         raise SystemExit("bench.py: --gpus N > 1 needs N ranks (run without a launcher to spawn them)")
     return world, rank, local, dist, devices
 
 
-def barrier_sync(dist, solver, local):
-    """Device sync (the solver's stream carries all of its work) + barrier across ranks.  At N = 1
-    the headline legs never import torch before the config-5 leg, so the process holds one HIP
-    runtime, torch's (odesat_amd/_lib.py)."""
+def device_sync(dist, solver, local):
+    """Device sync: the solver's stream carries all of its work (and torch's, under a process group).
+    At N = 1 the headline legs never import torch before the config-5 leg, so the process holds one
+    HIP runtime, torch's (odesat_amd/_lib.py)."""
     if solver is not None:
         solver.synchronize()
     if dist is not None:
         import torch
         if torch.cuda.is_available():
             torch.cuda.synchronize(local)
+
+
+def barrier_sync(dist, solver, local):
+    """Device sync + barrier across ranks: the start of a timed region.  A region ENDS with
+    device_sync, the clock read, and only then the barrier (`end_region`), so the collective's own
+    latency is never timed; the max over ranks of the per-rank durations is the job's time."""
+    device_sync(dist, solver, local)
+    if dist is not None:
         dist.barrier()
+
+
+def end_region(dist, solver, local, t0):
+    """Close a timed region opened after barrier_sync: this rank's duration, then the barrier."""
+    device_sync(dist, solver, local)
+    t = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    return t
 
 
 def time_gpu(solver, steps, warmup, dist, local, profile, stop, adaptive=False):
@@ -196,13 +223,12 @@ def time_gpu(solver, steps, warmup, dist, local, profile, stop, adaptive=False):
     barrier_sync(dist, solver, local)
     t0 = time.perf_counter()
     r = solver.simulate(max_steps=steps, poll_interval=steps, **kw)
-    barrier_sync(dist, solver, local)
-    t1 = time.perf_counter()
+    wall = end_region(dist, solver, local, t0)
     ms, launches = solver.profile_read() if profile else (None, None)
     solver.profile(False)
     if stop == ODESAT_STOP_NONE:
         assert r["steps_run"] == steps and (r["steps_done"] == steps).all(), "a replica did not take every step"
-    return t1 - t0, ms, launches, int(r["steps_run"])
+    return wall, ms, launches, int(r["steps_run"])
 
 
 def cpu_threads():
@@ -308,19 +334,29 @@ def roofline(args, short, ms, launches, clause_bytes_step, batch=None, dtype=Non
          "steps_per_launch": steps_per_launch, "algorithmic_bytes_per_launch": per_launch_bytes,
          "profile": pj["file"] if pj else None}
     hbm = {"achieved": hbm_alg, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_alg / HBM_PEAK_GBS}
-    if short == "k_onchip" and valu is not None:
+    if short in ("k_onchip", "k_wave") and valu is not None:
         achieved = valu / per_launch_s / 1e9
         r.update({"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_GINST,
                   "unit": "G VALU wave-instructions/s", "frac": achieved / VALU_PEAK_GINST,
                   "valu_insts_per_launch": valu, "hbm_algorithmic": hbm,
-                  "note": "k_onchip keeps v, dv and the clause memories on the CU for a whole launch: HBM "
-                          "moves the state once per launch (traffic), so the HBM-algorithmic rate exceeds "
-                          "the HBM peak and the binding resource is the CU's VALU issue (plus LDS/barrier "
-                          "latency; DESIGN.md §4.0).  ab_hbm_streaming is the HBM-bound kernel on the same "
-                          "workload."})
+                  "note": ONCHIP_NOTE if short == "k_onchip" else WAVE_NOTE})
+        if pj.get("lds_insts_per_step") is not None:  # LDS instruction issue beside it (one per CU per cycle)
+            lds = pj["lds_insts_fixed"] + pj["lds_insts_per_step"] * steps_per_launch
+            r["lds_issue"] = {"achieved": lds / per_launch_s / 1e9, "peak": LDS_PEAK_GINST,
+                              "unit": "G LDS wave-instructions/s",
+                              "frac": lds / per_launch_s / 1e9 / LDS_PEAK_GINST, "lds_insts_per_launch": lds}
     else:
         r.update({"bound": "hbm", **hbm})
     return r
+
+
+ONCHIP_NOTE = ("k_onchip keeps v, dv and the clause memories on the CU for a whole launch: HBM moves the state "
+               "once per launch (traffic), so the HBM-algorithmic rate exceeds the HBM peak and the binding "
+               "resource is the CU's VALU issue (plus LDS/barrier latency; DESIGN.md §4.0).  ab_hbm_streaming is "
+               "the HBM-bound kernel on the same workload.")
+WAVE_NOTE = ("k_wave keeps a replica's v, memories, terms and topology in LDS for a whole launch (HBM moves the "
+             "state once per launch): the CU's VALU and LDS issue bound it (DESIGN.md §4.3b); lds_issue gives "
+             "the LDS instruction rate against one LDS instruction per CU per cycle.")
 
 
 class Watchdog:
@@ -358,7 +394,7 @@ class Watchdog:
         if ok:
             sys.stderr.write("bench.py: leg deadline passed, ending the job\n")
             sys.stderr.flush()
-            os._exit(0)
+            os._exit(WATCHDOG_EXIT)  # the line is printed, but the job did not finish: not a clean exit
 
     def cancel(self):
         self.timer.cancel()
@@ -473,6 +509,20 @@ def main():
         # the reference CLI's defaults together (f64, adaptive steps: system.rs:111-139)
         leg("f64_adaptive", lambda: simple_leg("f64_adaptive", dtype="f64", adaptive=True))
 
+    def config3_leg():  # BASELINE configs[2]: uf250-1065-style random 3-SAT, adaptive steps, B = 1024
+        c3, _, _, _, f3 = formula_of("config3")
+        w, ms_, l_, b_, a_, ran = run_batch(B, True, adaptive=True, formula=f3)
+        w = max_over_ranks(dist, w)
+        res["config3"] = {
+            "value": B * world * ran / w, "unit": "replica-steps/s", "ms_per_step": w * 1e3 / ran, "steps_run": ran,
+            "dtype": "fp32", "step": "adaptive tol 1e-3 (per-replica dt)", "batch_per_gpu": B, "kernel": a_,
+            "workload": f"config3: uf250-1065-style random 3-SAT n={c3['n']} m={c3['m']} seed={c3['seed']}, "
+                        "adaptive Euler (half-step error estimate), all replicas stepped (no early exit)",
+            "roofline": roofline(args, a_, ms_, l_, b_, config="config3", mode="adaptive", steps=ran)}
+
+    if "config3" in legs and args.config == "config2" and args.dtype == "f32":
+        leg("config3", config3_leg)
+
     def inter_leg():  # simulate_inter (STOP_ANY): multi-step launches with replay at the stop step
         ri = run_batch(B, False, stop=ODESAT_STOP_ANY)
         wi, ran = max_over_ranks(dist, ri[0]), ri[5]  # a stop before `steps` ends the run early
@@ -541,8 +591,7 @@ def config4_leg(args, world, rank, local, dist, solver_cls=None, config="config4
         barrier_sync(dist, s, local)
         t0 = time.perf_counter()
         (wstep, wrep), ran = run_inter(dist, s, r0, max_steps=args.steps, chunk=INTER_LOCKSTEP_CHUNK, **kw)
-        barrier_sync(dist, s, local)
-        w_inter = max_over_ranks(dist, time.perf_counter() - t0)
+        w_inter = max_over_ranks(dist, end_region(dist, s, local, t0))
         ms4, l4 = s.profile_read()
         s.profile(False)
         kern4 = s.step_kernel()
@@ -554,8 +603,7 @@ def config4_leg(args, world, rank, local, dist, solver_cls=None, config="config4
         barrier_sync(dist, s, local)
         t0 = time.perf_counter()
         s.simulate(max_steps=ran, stop=ODESAT_STOP_NONE, **kw)
-        barrier_sync(dist, s, local)
-        w_none = max_over_ranks(dist, time.perf_counter() - t0)
+        w_none = max_over_ranks(dist, end_region(dist, s, local, t0))
     digest = None
     if rank == 0:  # every replica on every rank ran exactly `ran` steps (the inter stop included)
         ok = []
@@ -601,9 +649,12 @@ def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5")
     if gpu:
         torch.cuda.set_device(local)
 
-    def sync():
+    def dev_sync():
         if gpu:
             torch.cuda.synchronize(local)
+
+    def sync():
+        dev_sync()
         if dist is not None:
             dist.barrier()
 
@@ -651,8 +702,9 @@ def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5")
                 ps.step(dt, zeta, stop=False)
         if gpu:
             e1.record(stream)
+        dev_sync()
+        t1 = time.perf_counter()  # read before the barrier: its latency is not the step's
         sync()
-        t1 = time.perf_counter()
         wall = max_over_ranks(dist, t1 - t0)
         gpu_ms = e0.elapsed_time(e1) if gpu else (t1 - t0) * 1e3
         st = ps.status(stop=False)

@@ -1567,7 +1567,17 @@ extern "C" int odesat_set_state(odesat_solver *s, int64_t r0, int64_t count, con
             if (!(x[i] >= lo && x[i] <= hi)) return false;  // NaN fails too
         return true;
     };
-    s->in_range = s->in_range && within(v, count * s->n, -1.0, 1.0) && within(xs, count * s->m, -1.0, 1.0) &&
+    // xs: 0 or 1e-3 <= |xs| <= 1, so |xl xs| is 0 or >= 1e-3 and no term of the short forms
+    // (onchip.hip header) can round through a subnormal
+    auto within_xs = [](const double *x, int64_t cnt) {
+        if (!x) return true;
+        for (int64_t i = 0; i < cnt; ++i) {
+            const double a = std::fabs(x[i]);
+            if (!(a == 0.0 || (a >= 1e-3 && a <= 1.0))) return false;  // NaN fails too
+        }
+        return true;
+    };
+    s->in_range = s->in_range && within(v, count * s->n, -1.0, 1.0) && within_xs(xs, count * s->m) &&
                   within(xl, count * s->m, 1.0, 1e30);
     s->t_base = 0;
     HIP_TRY(hipStreamSynchronize(s->stream));
@@ -1760,9 +1770,11 @@ static int simulate_resident(odesat_solver *s, const odesat_params *p, bool adap
     const bool finite = std::fabs(zeta) <= 1e6 && adt >= 1e-30 && adt <= 1e30;  // (k_solo's short arithmetic)
     auto launch = [&](int64_t t0, int k, bool oop) -> int {
         const bool use_oc = oc && (t0 > 0 || s->in_range);
+        // the RESIDENT stand-in step of an ONCHIP solver on an out-of-range state is a one-step launch
+        // (nothing to replay), and adaptive k_resident updates in place: it never runs out of place
         return use_oc ? launch_onchip(s, (int)(base + t0), k, p->dt, zeta, p->stop, oop, adaptive, tol)
-                      : dispatch_resident(s, (int)(base + t0), k, adaptive, p->dt, zeta, tol, p->stop, oop,
-                                          finite && (t0 > 0 || s->in_range));
+                      : dispatch_resident(s, (int)(base + t0), k, adaptive, p->dt, zeta, tol, p->stop,
+                                          oop && (s->res_wave || !adaptive), finite && (t0 > 0 || s->in_range));
     };
     int64_t t = 0, next_poll = poll;
     while (t < p->max_steps) {

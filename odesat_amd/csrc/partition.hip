@@ -248,8 +248,9 @@ __global__ __launch_bounds__(256) void k_part_var(const int32_t *__restrict__ cs
                                                   float dt, int apply, float *__restrict__ out,
                                                   const PartStat *__restrict__ st, int32_t RG, int32_t bpr,
                                                   int32_t S, int32_t world) {
-    if (apply == 2 && blockIdx.x == 0 && (int32_t)threadIdx.x < world - 1)
-        out[(int64_t)(threadIdx.x + 1) * (S + 1) + S] = out[S];  // the clause kernel has finished
+    if (apply == 2 && blockIdx.x == 0)
+        for (int32_t r = (int32_t)threadIdx.x + 1; r < world; r += (int32_t)blockDim.x)
+            out[(int64_t)r * (S + 1) + S] = out[S];  // the clause kernel has finished
     int32_t k;
     if (REGION) {
         const int32_t nv = v1 - v0, x = (int32_t)(blockIdx.x % 8), kk = (int32_t)(blockIdx.x / 8);
@@ -567,6 +568,8 @@ extern "C" int odesat_part_rhs(odesat_part *p, const float *v, float *out, doubl
     if (apply < 0 || apply > 2) return fail(ODESAT_EINVAL, "apply must be 0 (CLAUSES), 1 (VARIABLES) or 2 (CLAUSES_RS)");
     if (apply != 0 && p->S == 0) return fail(ODESAT_EINVAL, "VARIABLES / CLAUSES_RS need a block size");
     if (apply == 2 && (p->v0 != 0 || p->v1 != p->n)) return fail(ODESAT_EINVAL, "CLAUSES_RS folds every variable");
+    // VARIABLES writes out[0 .. v1 - v0) and its flag at out[S]: the slice must fit its send block
+    if (apply == 1 && p->v1 - p->v0 > p->S) return fail(ODESAT_EINVAL, "VARIABLES slice wider than its block");
     PART_TRY(hipSetDevice(p->device));
     hipStream_t st = (hipStream_t)stream;
     const float *f;

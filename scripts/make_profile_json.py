@@ -55,6 +55,8 @@ def main():
     res["hbm_bytes_fixed"], res["hbm_bytes_per_step"] = fit("hbm_bytes")
     if all("SQ_INSTS_VALU" in p for p in (p1, p2)):
         res["valu_insts_fixed"], res["valu_insts_per_step"] = fit("SQ_INSTS_VALU")
+    if all("SQ_INSTS_LDS" in p for p in (p1, p2)):
+        res["lds_insts_fixed"], res["lds_insts_per_step"] = fit("SQ_INSTS_LDS")
     res["note"] = ("per launch of k steps: fixed + k * per_step; HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 "
                    "FETCH_SIZE correction), one --pmc pass per counter group, kernel trace only")
     json.dump(res, open(out, "w"), indent=1)

@@ -26,6 +26,26 @@ def _args(steps, warmup):
                            dtype="f32", config="config2", config5_graph=0)
 
 
+BARRIER_DELAY = 0.25  # seconds every barrier of the legs' process group sleeps first (test_bench_multi_gpu_legs_gloo)
+
+
+class _SlowBarrier:
+    """torch.distributed with a barrier that sleeps first: a timed region that reads its clock after
+    the closing barrier would grow by the delay."""
+
+    def __init__(self, td, delay):
+        self._td, self._delay, self.barriers = td, delay, 0
+
+    def barrier(self):
+        import time
+        time.sleep(self._delay)
+        self.barriers += 1
+        self._td.barrier()
+
+    def __getattr__(self, name):
+        return getattr(self._td, name)
+
+
 def _worker(rank, world, port, out, per):
     import torch.distributed as td
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -35,8 +55,10 @@ def _worker(rank, world, port, out, per):
     from odesat_amd import workloads as wl
     from tests.host_standins import HostPart, HostSolver
     wl.CONFIGS["tiny4"], wl.CONFIGS["tiny5"] = TINY4, TINY5
-    r4 = bench.config4_leg(_args(300, 3), world, rank, 0, td, solver_cls=HostSolver, config="tiny4", batch=per)
-    r5 = bench.config5_leg(_args(12, 3), world, rank, 0, td, part_cls=HostPart, config="tiny5")
+    slow = _SlowBarrier(td, BARRIER_DELAY)
+    r4 = bench.config4_leg(_args(300, 3), world, rank, 0, slow, solver_cls=HostSolver, config="tiny4", batch=per)
+    r5 = bench.config5_leg(_args(12, 3), world, rank, 0, slow, part_cls=HostPart, config="tiny5")
+    r4["barriers"] = slow.barriers
     if rank == 0:
         with open(out, "w") as fh:
             json.dump({"c4": r4, "c5": r5}, fh)
@@ -68,6 +90,10 @@ def test_bench_multi_gpu_legs_gloo(tmp_path, world, per):
     assert c4["steps_run"] == t and c4["winner"] == {"step": t - 1, "replica": win}
     assert c4["digest"]["match"] and c4["digest"]["ranks_checked"] == world
     assert c4["global_batch"] == B and c4["value"] > 0 and c4["roofline"]["bound"] == "hbm"
+    # every barrier slept BARRIER_DELAY, and none of that is in a timed region
+    assert c4["barriers"] >= 4
+    assert c4["ms_per_step"] * c4["steps_run"] < 1e3 * BARRIER_DELAY
+    assert c4["steps_run"] / c4["stop_none_value"] * B * 1e3 < 1e3 * BARRIER_DELAY
 
     # config 5: VARIABLES bit-exact against rank 0's world-1 run, the CLAUSES forms within tolerance
     c5 = res["c5"]
@@ -76,12 +102,14 @@ def test_bench_multi_gpu_legs_gloo(tmp_path, world, per):
     assert d["steps"] == 15
     for name in ("clauses", "clauses_rs", "variables"):
         assert c5[name]["value"] > 0 and c5[name]["exchange_bytes_per_rank"] > 0
+        assert c5[name]["ms_per_step"] * 12 < 1e3 * BARRIER_DELAY  # the barrier is not timed
     assert c5["variables"]["local_clauses_rank0"] < TINY5["m"]  # a share of the clauses
 
 
 def test_watchdog_prints_the_line_and_ends_the_job_past_the_deadline():
     """A leg that never returns (a collective stuck on one node) costs only that leg: past
-    --leg-deadline rank 0 prints the line built so far, marked, and the process exits 0."""
+    --leg-deadline rank 0 prints the line built so far, marked, and the process exits with
+    bench.WATCHDOG_EXIT (not 0: a driver checking the status sees the job did not finish)."""
     import subprocess
     import sys
     import time
@@ -92,7 +120,7 @@ def test_watchdog_prints_the_line_and_ends_the_job_past_the_deadline():
             "time.sleep(30)\n" % ROOT)
     t0 = time.time()
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 0 and time.time() - t0 < 25
+    assert r.returncode == 3 and time.time() - t0 < 25
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])
@@ -115,3 +143,44 @@ def test_watchdog_emits_once_when_the_legs_finish():
         assert w1.emit()
     lines = buf.getvalue().splitlines()
     assert lines == [json.dumps({"value": 3.0})]
+
+
+class _FakeSolver:
+    """The calls time_gpu makes, doing nothing: the timed region then holds only harness cost."""
+
+    def simulate(self, max_steps, poll_interval, **kw):
+        return {"steps_run": max_steps, "steps_done": np.full(4, max_steps)}
+
+    def profile(self, on):
+        pass
+
+    def profile_read(self):
+        return [0.0, 0.0, 0.0], [1, 0, 0]
+
+    def synchronize(self):
+        pass
+
+
+class _SleepDist:
+    def __init__(self, delay):
+        self.delay, self.barriers = delay, 0
+
+    def barrier(self):
+        import time
+        time.sleep(self.delay)
+        self.barriers += 1
+
+
+def test_time_gpu_excludes_the_closing_barrier():
+    """the headline's timed region ends at the device sync, before the barrier
+    (a barrier that sleeps 50 ms must not change the measured time)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    from odesat_amd.system import ODESAT_STOP_NONE
+    d = _SleepDist(0.05)
+    wall, _, _, ran = bench.time_gpu(_FakeSolver(), 20, 5, d, 0, False, ODESAT_STOP_NONE)
+    assert d.barriers == 2 and ran == 20  # one barrier opens the region, one follows it
+    assert wall < 0.02
+    wall0, _, _, _ = bench.time_gpu(_FakeSolver(), 20, 5, None, 0, False, ODESAT_STOP_NONE)
+    assert abs(wall - wall0) < 0.02

@@ -162,6 +162,55 @@ def test_config2_f32_tracks_f64_reference_at_bench_horizon():
         assert np.array_equal(gv > 0, ov > 0)
 
 
+@pytest.mark.parametrize("leg,prec,adaptive,kernel", [
+    ("adaptive", "f32", True, "k_onchip"),       # k_onchip<90, 1, true>
+    ("f64", "f64", False, "k_resident"),         # short forms, ring of 8 (§4.1)
+    ("f64_adaptive", "f64", True, "k_resident"),  # VFG: the full-step clone in HBM (§4.1)
+])
+def test_config2_bench_leg_kernels_bitexact(leg, prec, adaptive, kernel):
+    """bench.py's `adaptive`, `f64` and `f64_adaptive` legs at the configuration they time: n=10k,
+    m=42k, B=1024, the bench's call shape (a 5-step warm-up call, then a 15-step call, each ONE
+    persistent launch, STOP_NONE).  The solver runs the kernel the leg names; replicas {0, 517, 1023}
+    are bit-exact against the oracle's simulate of the same two calls (state, per-replica dt --
+    restarting at 0.01 per call, system.rs:205 -- and step counts); every replica stays finite and in
+    the clamp ranges (system.rs:94-96).  Reference: system.rs:111-139, :141-154, :204-234."""
+    f, (cp, v_, n_), n, m = instance("config2")
+    T = np.float32 if prec == "f32" else np.float64
+    o = Oracle(cp, v_, n_, n, prec)
+    B, calls = 1024, (5, 15)
+    pick = [0, 517, 1023]
+    with Solver(f, B, prec) as s:
+        assert s.step_kernel(adaptive) == kernel
+        s.init_state(42)
+        rs = []
+        for K in calls:
+            r = s.simulate(adaptive=adaptive, dt=0.01, tol=1e-3, max_steps=K, poll_interval=K, stop=ODESAT_STOP_NONE)
+            assert r["steps_run"] == K and np.all(r["steps_done"] == K)
+            rs.append(r)
+        states = {b: s.get_state(b, 1) for b in pick}
+        eps = T(0.001)
+        for r0 in range(0, B, 256):
+            v, xs, xl = s.get_state(r0, 256)
+            assert np.isfinite(v).all() and np.isfinite(xs).all() and np.isfinite(xl).all()
+            assert v.min() >= -1 and v.max() <= 1
+            assert xs.min() >= eps and xs.max() <= T(1) - eps
+            assert xl.min() >= 1 and xl.max() <= T(1e4) * T(m)
+        if adaptive:
+            assert np.all(rs[-1]["dt"][:B] >= 2.0 ** -7) and np.all(rs[-1]["dt"][:B] <= 1e3)
+    for b in pick:
+        ov = init_voltages(42, b, 1, n)[0].astype(T)
+        oxs, oxl = o.init_short_term_memory(), np.ones(m, T)
+        for K, r in zip(calls, rs):
+            if adaptive:
+                t, _, _, h, _ = o.simulate(ov, oxs, oxl, tol=T(1e-3), steps=K, zeta=T(0.001))
+                assert same(T(h), T(r["dt"][b])), (b, h, r["dt"][b])
+            else:
+                t, _, _, _, _ = o.simulate(ov, oxs, oxl, dt=T(0.01), steps=K, zeta=T(0.001))
+            assert t == K and r["steps_done"][b] == K
+        gv, gxs, gxl = states[b]
+        assert same(gv[0], ov) and same(gxs[0], oxs) and same(gxl[0], oxl), b
+
+
 # ----------------------------------------------------------------------------------- config 1 ---
 def test_config1_cli_solve_easy_adaptive_matches_oracle(tmp_path):
     """`odesat solve -f easy.cnf` exactly as BASELINE states config 1 (adaptive step, tol 1e-3,

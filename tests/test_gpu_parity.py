@@ -595,6 +595,33 @@ def test_onchip_adaptive_matches_resident_and_oracle(stop, monkeypatch):
     assert same(s1[0][0], ov) and same(s1[1][0], oxs) and same(s1[2][0], oxl)
 
 
+def test_onchip_adaptive_inter_after_out_of_range_set_state():
+    """adaptive STOP_ANY (simulate_inter) on an ONCHIP solver whose caller state is
+    out of range.  The first step runs RESIDENT's adaptive step in place (one step, nothing to
+    replay), the rest k_onchip's multi-step launches with replay.  Every replica's state, dt and the
+    stop equal the oracle's simulate_inter with per-replica dt (the declared deviation)."""
+    from odesat_amd import _lib
+    n, m = 3000, 12600
+    f, (cp, v_, n_) = _instance(n, m, 5)
+    o = Oracle(cp, v_, n_, n, "f32")
+    B, K = 6, 40
+    v, xs, xl = init_states(o, B, seed=9, T=np.float32)
+    v[0, :50] *= 1.7        # voltages outside [-1, 1]
+    xs[1, :40] = 0.0005      # short-term memories below the clamp
+    xl[2, :30] = 0.5        # long-term memories below the clamp
+    with Solver(f, B, "f32") as s:
+        assert s.algorithm == _lib.ODESAT_ALG_ONCHIP and s.step_kernel(True) == "k_onchip"
+        s.set_state(v.astype(np.float64), xs.astype(np.float64), xl.astype(np.float64))
+        r = s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=K, stop=ODESAT_STOP_ANY, poll_interval=10)
+        gv, gxs, gxl = s.get_state()
+    t, win, _, dts = o.simulate_inter(v, xs, xl, tol=np.float32(1e-3), steps=K, zeta=np.float32(0.001),
+                                      shared_dt=False)
+    assert r["steps_run"] == t and np.all(r["steps_done"] == t)
+    if win >= 0:
+        assert int(np.flatnonzero(r["first_sat_step"] >= 0)[0]) == win
+    assert same(gv, v) and same(gxs, xs) and same(gxl, xl) and same(r["dt"].astype(np.float32), dts)
+
+
 @pytest.mark.parametrize("narrow", ["0", "1"])
 @pytest.mark.parametrize("stop", ["each", "any", "none"])
 def test_resident_adaptive_clone_in_hbm_matches_fused_and_oracle(stop, narrow, monkeypatch):
