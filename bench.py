@@ -56,6 +56,8 @@ LDS_PEAK_GINST = 256 * 2.4e9 / 1e9
 LEGS = ("f64", "adaptive", "f64_adaptive", "config3", "inter", "config4", "config5", "extra", "ab")
 CLAUSES_TOL = 1e-5       # the CLAUSES partitions' stated tolerance against a world-1 run
 DIGEST_REPLICAS = 4      # inter_config4: replicas per rank re-integrated by rank 0
+# config 5: the measured floor of a step's random accesses at world 1
+GATHER_FLOOR_US_C5 = 128.0
 WATCHDOG_EXIT = 3        # exit status of a job ended by the leg watchdog (after rank 0 printed its line)
 
 
@@ -158,6 +160,12 @@ def dist_setup(args):
     if world > 1 or os.environ.get("ODESAT_BENCH_DIST") == "1":
         import torch
         import torch.distributed as td
+        if "RANK" not in os.environ:  # ODESAT_BENCH_DIST=1 without a launcher: a one-rank group
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(port))
         ndev = torch.cuda.device_count()
         # RCCL ("nccl") on GPU boxes, one rank per GPU; ODESAT_DIST_BACKEND=gloo rehearses N ranks on
         # fewer GPUs (RCCL refuses two ranks on one device): ranks then share devices round-robin.
@@ -674,6 +682,12 @@ def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5")
                        f"partitioned over {world} rank(s)", "scaling": "strong", "unit": "steps/s",
            "backend": dist.get_backend() if dist is not None else None}
     finals = {}
+    prof5 = None  # PMC bytes per step at world 1 (scripts/make_part_profile.py)
+    try:
+        with open(os.path.join(args.profile_dir, "profile_k_part_config5.json")) as fh:
+            prof5 = json.load(fh)
+    except (OSError, ValueError):
+        pass
     for name, mode in (("clauses", CLAUSES), ("clauses_rs", CLAUSES_RS), ("variables", VARIABLES)):
         t0 = time.perf_counter()
         ps = part_cls(cp, v_, n_, n, mode, comm=comm, device=local)
@@ -716,6 +730,11 @@ def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5")
         alg_bytes = 8 * n + 16 * mloc
         per_step_s = gpu_ms / 1e3 / args.steps
         achieved = alg_bytes / per_step_s / 1e9
+        traffic = None
+        if prof5 is not None and world == 1 and config == prof5.get("config"):
+            # the CLAUSES_RS kernels at world 1 are CLAUSES' (the gathered layout is the identity)
+            ent = prof5["partitions"].get("clauses" if name == "clauses_rs" else name)
+            traffic = ent["hbm_bytes_per_step"] if ent else None
         out[name] = {
             "value": args.steps / wall, "ms_per_step": wall * 1e3 / args.steps,
             "collective": {"clauses": "all_reduce", "clauses_rs": "reduce_scatter + all_gather",
@@ -725,7 +744,13 @@ def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5")
             "roofline": {"bound": "hbm", "kernel": "k_part_clause3 + k_part_var (+ collective), per step",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_step": alg_bytes, "gpu_ms_per_step": per_step_s * 1e3,
-                         "traffic": None,
+                         "traffic": traffic, "traffic_profile": "profiles/profile_k_part_config5.json (world 1)"
+                         if traffic is not None else None,
+                         "gather_floor": {"us_per_step": GATHER_FLOOR_US_C5 / world,
+                                          "frac": GATHER_FLOOR_US_C5 / world / (per_step_s * 1e6),
+                                          "source": "scripts/micro/gather_ceiling.hip, profiles/r02_gather_ceiling.jsonl: "
+                                                    "12.6M voltage gathers + 12.6M term reads at the L2-resident "
+                                                    "random 4-byte rate (2 x 64 us), divided over the ranks"},
                          "note": "bytes = SURVEY.md §8d (v and the rank's clause memories read and written once); "
                                  "the step is bound by 12.6M/world random 4-byte gathers and the term hand-off, "
                                  "not streaming: see DESIGN.md §5.1 for the measured random-access ceiling"}}
