@@ -195,8 +195,10 @@ def device_sync(dist, solver, local):
     At N = 1 the headline legs never import torch before the config-5 leg, so the process holds one
     HIP runtime, torch's (odesat_amd/_lib.py)."""
     if solver is not None:
-        solver.synchronize()
-    if dist is not None:
+        solver.synchronize()  # the solver's stream: all of its work (no device-wide sync, see below)
+    elif dist is not None:
+        # no solver: torch's stream (and a device-wide sync, which under an RCCL process group costs
+        # ~100 us more than the solver's stream sync -- profiles/r04b_bench_dist_world1.json)
         import torch
         if torch.cuda.is_available():
             torch.cuda.synchronize(local)

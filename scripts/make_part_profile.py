@@ -13,6 +13,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import sys
 
 
@@ -20,10 +21,10 @@ def per_kernel(root):
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"]
-            if "k_part" not in name:
+            mt = re.search(r"k_part\w*", r["Kernel_Name"])
+            if mt is None:
                 continue
-            short = name.split("(")[0].split("<")[0].replace("void ", "").strip()
+            short = mt.group(0)
             vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
     for k, d in vals.items():

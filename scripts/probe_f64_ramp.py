@@ -6,7 +6,12 @@ management) or first-touch / TLB cost of a fresh solver's buffers.  The probe se
   B  the same solver after 1.5 s idle, then 4 more back-to-back launches (buffers already touched:
      a slow first launch here is a clock effect, not first touch);
   C  a second fresh solver right after B (hot GPU, untouched buffers: a fast first launch here rules
-     first touch out).
+     first touch out);
+  D  after 1.5 s idle, 60 launches of 4 f64 steps (the ramp's time course, ~1 ms resolution);
+  E  after 1.5 s idle, 60 launches of 4 steps of the f32 headline kernel (k_onchip: compute-bound,
+     the state on the CU -- does a kernel that barely touches HBM ramp too?);
+  F  after 1.5 s idle, ~100 ms of k_onchip launches, then D's f64 launches (does compute load prime
+     the memory-bound kernel?).
 
 Each launch: HIP-event kernel time (the solver's stream) and the host time window.  A sampler thread
 reads the current DPM levels (sysfs pp_dpm_sclk / pp_dpm_mclk / pp_dpm_fclk, the '*' line) every
@@ -113,6 +118,31 @@ def main():
         s.simulate(dt=0.01, max_steps=5, stop=ODESAT_STOP_NONE, poll_interval=5)
         for i in range(4):
             launch(s, "C_fresh_hot", i)
+    def series(s, phase, k, count):
+        out = []
+        for i in range(count):
+            s.profile(True)
+            s.simulate(dt=0.01, max_steps=k, stop=ODESAT_STOP_NONE, poll_interval=k)
+            ms, _ = s.profile_read()
+            s.profile(False)
+            out.append(round(ms[0] * 1e3 / k, 2))
+        row = {"phase": phase, "steps_per_launch": k, "us_per_step": out}
+        print(json.dumps(row), flush=True)
+        return row
+
+    with Solver(f, 1024, "f64") as s64, Solver(f, 1024, "f32") as s32:
+        s64.init_state(42)
+        s32.init_state(42)
+        s64.simulate(dt=0.01, max_steps=5, stop=ODESAT_STOP_NONE, poll_interval=5)
+        s32.simulate(dt=0.01, max_steps=5, stop=ODESAT_STOP_NONE, poll_interval=5)
+        s64.synchronize()
+        time.sleep(1.5)
+        series(s64, "D_f64_after_idle", 4, 60)
+        time.sleep(1.5)
+        series(s32, "E_onchip_after_idle", 4, 60)
+        time.sleep(1.5)
+        series(s32, "F_onchip_primer", 4, 30)
+        series(s64, "F_f64_after_onchip", 4, 60)
     smp.stop = True
     summ = {}
     for r in rows:

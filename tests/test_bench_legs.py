@@ -92,8 +92,8 @@ def test_bench_multi_gpu_legs_gloo(tmp_path, world, per):
     assert c4["global_batch"] == B and c4["value"] > 0 and c4["roofline"]["bound"] == "hbm"
     # every barrier slept BARRIER_DELAY, and none of that is in a timed region
     assert c4["barriers"] >= 4
-    assert c4["ms_per_step"] * c4["steps_run"] < 1e3 * BARRIER_DELAY
-    assert c4["steps_run"] / c4["stop_none_value"] * B * 1e3 < 1e3 * BARRIER_DELAY
+    assert c4["ms_per_step"] * c4["steps_run"] < 1e3 * BARRIER_DELAY, c4["ms_per_step"] * c4["steps_run"]
+    assert c4["steps_run"] / c4["stop_none_value"] * B * 1e3 < 1e3 * BARRIER_DELAY, c4["stop_none_value"]
 
     # config 5: VARIABLES bit-exact against rank 0's world-1 run, the CLAUSES forms within tolerance
     c5 = res["c5"]
@@ -102,7 +102,7 @@ def test_bench_multi_gpu_legs_gloo(tmp_path, world, per):
     assert d["steps"] == 15
     for name in ("clauses", "clauses_rs", "variables"):
         assert c5[name]["value"] > 0 and c5[name]["exchange_bytes_per_rank"] > 0
-        assert c5[name]["ms_per_step"] * 12 < 1e3 * BARRIER_DELAY  # the barrier is not timed
+        assert c5[name]["ms_per_step"] * 12 < 1e3 * BARRIER_DELAY, (name, c5[name]["ms_per_step"])  # not timed
     assert c5["variables"]["local_clauses_rank0"] < TINY5["m"]  # a share of the clauses
 
 
