@@ -55,6 +55,8 @@ struct odesat_solver {
     void *w = nullptr;
     void *vh = nullptr, *vf = nullptr, *ch = nullptr, *cf = nullptr;
     void *dtr = nullptr, *err = nullptr;
+    void *tt[2] = {nullptr, nullptr};  // FUSED owner-TT: clause products xl xs [G][m][W], double-buffered (lazy)
+    bool fused_tt = true;              // ODESAT_FUSED_TT=0: every incidence reads the clause's memories (A/B)
     uint32_t *unsat = nullptr;
     uint8_t *act = nullptr;
     int64_t *sat_step = nullptr, *steps_done = nullptr;
@@ -228,6 +230,8 @@ template <typename T> KArgs<T> make_args(odesat_solver *s) {
     a.ch = (T *)s->ch;
     a.cf = (T *)s->cf;
     a.dtr = (T *)s->dtr;
+    a.tt0 = (T *)s->tt[0];
+    a.tt1 = (T *)s->tt[1];
     a.err = (typename Bits<T>::U *)s->err;
     a.unsat = s->unsat;
     a.act = s->act;
@@ -284,7 +288,7 @@ template <typename T> unsigned geometry(const odesat_solver *s, KArgs<T> &a, int
 }
 
 template <typename T, int LW, int VEC, int MODE>
-int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which) {
+int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which, bool tt = false) {
     const int64_t items = which == K_CLAUSE ? s->m : s->n;
     const unsigned blocks = geometry<T>(s, a, items, LW);
     if (blocks == 0) return ODESAT_OK;
@@ -292,6 +296,15 @@ int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which) {
     {
         Timed tm(s, which == K_VARIABLE ? 1 : 0);
         if (which == K_STEP) {
+            if constexpr (LW == 64 && MODE == M_FIXED) {
+                if (tt) {  // owner-TT (kernels.hpp stream_rows3): the caller checked the conditions
+                    if (s->rb == 8)
+                        hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 3, 8, true>), grid, block, 0, s->stream, a);
+                    else
+                        hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 3, 4, true>), grid, block, 0, s->stream, a);
+                    goto launched;
+                }
+            }
             if (s->uniform_k == 3 && s->rb == 8)
                 hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 3, 8>), grid, block, 0, s->stream, a);
             else if (s->uniform_k == 3)
@@ -306,6 +319,7 @@ int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which) {
         } else {
             hipLaunchKernelGGL((k_variable<T, LW, VEC, MODE>), grid, block, 0, s->stream, a);
         }
+    launched:;
     }
     HIP_TRY(hipGetLastError());
     if (which == K_STEP && s->n_empty > 0) {  // clauses with no literal (no owning variable)
@@ -318,9 +332,10 @@ int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which) {
     return ODESAT_OK;
 }
 
-// One RHS(+update) of `MODE` for the groups [gA, gB).
+// One RHS(+update) of `MODE` for the groups [gA, gB).  tt: FUSED fixed step with owner-TT (the
+// current products are valid: ensure_tt).
 template <typename T, int LW, int VEC, int MODE>
-int step_groups(odesat_solver *s, int step, T dt, T zeta, int gA, int gB) {
+int step_groups(odesat_solver *s, int step, T dt, T zeta, int gA, int gB, bool tt = false) {
     KArgs<T> a = make_args<T>(s);
     a.step = step;
     a.dt = dt;
@@ -329,7 +344,7 @@ int step_groups(odesat_solver *s, int step, T dt, T zeta, int gA, int gB) {
     if (s->alg != ODESAT_ALG_TWOPASS) {  // FUSED (RESIDENT's single steps too)
         a.g0 = gA;
         a.ng = gB - gA;
-        return launch_kernel<T, LW, VEC, MODE>(s, a, K_STEP);
+        return launch_kernel<T, LW, VEC, MODE>(s, a, K_STEP, tt);
     }
     for (int g0 = gA; g0 < gB; g0 += s->chunk_groups) {  // TWOPASS: one contribution buffer per chunk
         a.g0 = g0;
@@ -373,11 +388,11 @@ int launch_status(odesat_solver *s, int step, int stop_mode, bool adaptive, doub
 // One full euler step (fixed or adaptive) for the replica groups [gA, gB), enqueued on the stream.
 template <typename T>
 int enqueue_step(odesat_solver *s, int step, bool adaptive, double dt, double zeta, double tol, int stop_mode,
-                 int gA, int gB) {
+                 int gA, int gB, bool tt = false) {
     int rc = with_layout<T>(s, [&](auto lw, auto vec) -> int {
         constexpr int LW = decltype(lw)::value, VEC = decltype(vec)::value;
         int r;
-        if (!adaptive) return step_groups<T, LW, VEC, M_FIXED>(s, step, (T)dt, (T)zeta, gA, gB);
+        if (!adaptive) return step_groups<T, LW, VEC, M_FIXED>(s, step, (T)dt, (T)zeta, gA, gB, tt);
         const int span = s->alg == ODESAT_ALG_TWOPASS ? s->chunk_groups : gB - gA;
         for (int g0 = gA; g0 < gB; g0 += span) {  // both half steps of one contribution-buffer chunk
             const int g1 = std::min(gB, g0 + span);
@@ -391,9 +406,35 @@ int enqueue_step(odesat_solver *s, int step, bool adaptive, double dt, double ze
 }
 
 int dispatch_step(odesat_solver *s, int step, bool adaptive, double dt, double zeta, double tol, int stop_mode,
-                  int gA, int gB) {
-    return s->dtype == ODESAT_F64 ? enqueue_step<double>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB)
-                                  : enqueue_step<float>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB);
+                  int gA, int gB, bool tt = false) {
+    return s->dtype == ODESAT_F64 ? enqueue_step<double>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB, tt)
+                                  : enqueue_step<float>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB, tt);
+}
+
+// FUSED owner-TT (kernels.hpp stream_rows3) applies to fixed steps of the 3-SAT incidence stream
+// (64 replicas per group, one per lane) on in-range states with a finite zeta and a finite, normal
+// dt -- where the rigidity term is +-0 (onchip.hip's header).
+bool tt_layout(const odesat_solver *s) {
+    return s->fused_tt && s->alg == ODESAT_ALG_FUSED && s->uniform_k == 3 && s->LW == 64 && s->VEC == 1;
+}
+
+// The clause products of the groups' current buffers (once per call that steps with owner-TT).
+int ensure_tt(odesat_solver *s) {
+    int rc;
+    const size_t elems = state_elems(s, s->m);
+    if (!s->tt[0] && ((rc = dmalloc(s, &s->tt[0], elems * s->tsize)) || (rc = dmalloc(s, &s->tt[1], elems * s->tsize))))
+        return rc;
+    const int64_t per_group = s->m * (int64_t)s->W, total = per_group * s->G;
+    const int threads = 256;
+    const unsigned blocks = (unsigned)std::min<int64_t>((total + threads - 1) / threads, 65536);
+    if (s->dtype == ODESAT_F64)
+        hipLaunchKernelGGL(k_tt_init<double>, dim3(blocks), dim3(threads), 0, s->stream, (const double *)s->c[0],
+                           (const double *)s->c[1], s->par, (double *)s->tt[0], (double *)s->tt[1], per_group, total);
+    else
+        hipLaunchKernelGGL(k_tt_init<float>, dim3(blocks), dim3(threads), 0, s->stream, (const float *)s->c[0],
+                           (const float *)s->c[1], s->par, (float *)s->tt[0], (float *)s->tt[1], per_group, total);
+    HIP_TRY(hipGetLastError());
+    return ODESAT_OK;
 }
 
 // ---- RESIDENT ---------------------------------------------------------------------------------
@@ -1172,6 +1213,8 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     void *snaps[] = {s->snap_par, s->snap_sat, s->snap_done, s->snap_dt, s->ck_v, s->ck_c, s->ck_dt, s->ck_par,
                      s->ck_act, s->ck_sat, s->ck_done, s->ck_stop};
     for (void *p : snaps) dfree(p);
+    dfree(s->tt[0]);
+    dfree(s->tt[1]);
     void *pinned[] = {s->h_sat, s->h_dt, s->h_stop, s->h_act};  // (h_done lies inside h_sat's block)
     for (void *p : pinned)
         if (p) (void)hipHostFree(p);
@@ -1317,6 +1360,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         if (res_r == 0 && lw == 64 && (std::atoi(ev) == 2 || (std::atoi(ev) == 4 && s->dtype == ODESAT_F32)))
             s->VEC = std::atoi(ev);
     if (const char *ev = std::getenv("ODESAT_RB")) s->rb = std::atoi(ev) == 8 ? 8 : 4;
+    if (const char *ev = std::getenv("ODESAT_FUSED_TT")) s->fused_tt = std::atoi(ev) != 0;
     s->W = s->LW * s->VEC;
     s->Bp = (batch + s->W - 1) / s->W * s->W;
     s->G = (int)(s->Bp / s->W);
@@ -1864,12 +1908,21 @@ static int simulate_impl(odesat_solver *s, const odesat_params *p, bool cont, in
     const int span = chunk_major ? chunk : s->G;
     const int64_t base = s->t_base;
     int64_t t_run = 0;
+    const double adt = std::fabs(p->dt);
+    const bool use_tt = !adaptive && tt_layout(s) && std::fabs(zeta) <= 1e6 && adt >= 1e-30 && adt <= 1e30;
     for (int gA = 0; gA < s->G; gA += span) {
         const int gB = std::min(s->G, gA + span);
         const int64_t r0 = (int64_t)gA * s->W, r1 = std::min<int64_t>((int64_t)gB * s->W, s->B);
         int64_t t = 0;
+        bool tt_ready = false;
         for (; t < p->max_steps; ++t) {
-            if ((rc = dispatch_step(s, (int)(base + t), adaptive, p->dt, zeta, tol, p->stop, gA, gB))) return rc;
+            // owner-TT from the first step whose state is in range (after one clamped step at the latest)
+            const bool tt = use_tt && (t > 0 || s->in_range);
+            if (tt && !tt_ready) {
+                if ((rc = ensure_tt(s))) return rc;
+                tt_ready = true;
+            }
+            if ((rc = dispatch_step(s, (int)(base + t), adaptive, p->dt, zeta, tol, p->stop, gA, gB, tt))) return rc;
             if (p->stop != ODESAT_STOP_NONE && (t + 1) % poll == 0 && t + 1 < p->max_steps) {
                 // poll the stop condition (results are exact regardless: later launches are no-ops)
                 HIP_TRY(hipMemcpyAsync(s->h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream));
@@ -2108,3 +2161,15 @@ extern "C" int odesat_debug_pair_tiles(const odesat_cnf *f, int off, int32_t *ti
     *ntiles = (int32_t)fill.size();
     return ODESAT_OK;
 }
+
+#ifdef RES_STAMPS
+// Diagnostic build only: the per-workgroup k_resident stamps of the last launch (4096 x 64, resident.hpp).
+extern "C" int odesat_res_stamps(unsigned long long *out, int count) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(odk::g_res_stamps), sizeof(unsigned long long) * (size_t)count, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int odesat_res_clk(unsigned long long *out, int count) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(odk::g_res_clk), sizeof(unsigned long long) * (size_t)count, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -67,15 +67,19 @@ struct Stamps {};
 // Diagnostic build only (-DONCHIP_PHASES): per workgroup, wave 0 records s_memrealtime (100 MHz)
 // at kernel start, after the state load (its barrier), after the step loop and at the end, into
 // g_onchip_phases[g][4] (read by odesat_onchip_phases).
+// g_onchip_clk holds s_memtime (shader clock) at the same points: their ratio is the effective clock.
 #ifdef ONCHIP_PHASES
 __device__ unsigned long long g_onchip_phases[4096 * 4];
-__device__ __forceinline__ uint64_t realtime() {
-    uint64_t t;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    return t;
-}
-#define ONCHIP_PHASE(i) \
-    do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_onchip_phases[blockIdx.x * 4 + (i)] = realtime(); } while (0)
+__device__ unsigned long long g_onchip_clk[4096 * 4];
+#define ONCHIP_PHASE(i)                                                                                   \
+    do {                                                                                                  \
+        if (threadIdx.x == 0 && blockIdx.x < 4096) {                                                      \
+            uint64_t t_, c_;                                                                              \
+            asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_), "=s"(c_)::"memory"); \
+            g_onchip_phases[blockIdx.x * 4 + (i)] = t_;                                                   \
+            g_onchip_clk[blockIdx.x * 4 + (i)] = c_;                                                      \
+        }                                                                                                 \
+    } while (0)
 #else
 #define ONCHIP_PHASE(i) do {} while (0)
 #endif
@@ -902,6 +906,10 @@ extern "C" int odesat_onchip_stamps(unsigned long long *out, int count) {
 // Diagnostic build only: the per-workgroup phase stamps of the last launch (4096 x 4, s_memrealtime).
 extern "C" int odesat_onchip_phases(unsigned long long *out, int count) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(onchip::g_onchip_phases), sizeof(unsigned long long) * (size_t)count, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int odesat_onchip_clk(unsigned long long *out, int count) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(onchip::g_onchip_clk), sizeof(unsigned long long) * (size_t)count, 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -394,6 +394,25 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
 constexpr int RES_NARROW = 64;
 // FAST (3-SAT, in-range states): res_clause3's short forms; the terms are 2 x the reference's, so every
 // h of the variable phases is halved.
+// Diagnostic build only (-DRES_STAMPS, scripts/build_variant.sh ... odesat_hip): per workgroup g < 4096,
+// thread 0 records s_memrealtime (100 MHz) at entry, after v is in LDS, after each step k < 60 and
+// at the end: g_res_stamps[g][0], [1], [2 + k], [63] (read by odesat_res_stamps; 0 = not reached).
+// g_res_clk holds s_memtime (shader clock) at the same points: their ratio is the effective clock.
+#ifdef RES_STAMPS
+__device__ unsigned long long g_res_stamps[4096 * 64];
+__device__ unsigned long long g_res_clk[4096 * 64];
+#define RES_STAMP(i)                                                                                \
+    do {                                                                                            \
+        if (threadIdx.x == 0 && blockIdx.x < 4096) {                                                \
+            uint64_t t_, c_;                                                                        \
+            asm volatile("s_memrealtime %0\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_), "=s"(c_)::"memory"); \
+            g_res_stamps[blockIdx.x * 64 + (i)] = t_;                                               \
+            g_res_clk[blockIdx.x * 64 + (i)] = c_;                                                  \
+        }                                                                                           \
+    } while (0)
+#else
+#define RES_STAMP(i) do {} while (0)
+#endif
 template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR, bool VFG = false, bool FAST = false>
 __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     static_assert(!FAST || K3, "the short forms are 3-SAT only (res_clause_any has none)");
@@ -407,6 +426,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     __shared__ int skipL;
     const int g = blockIdx.x;
     const int tid = threadIdx.x;
+    RES_STAMP(0);
     ResCtx<T, R> x;
     x.r = tid % R;
     x.lc = tid / R;
@@ -446,6 +466,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     copy_to_lds<8>(x.vL, V, tid, (int)nR, NTH);
     for (size_t i = tid; i < nR; i += NTH) x.dvL[i] = (T)0.0;  // :33
     __syncthreads();
+    RES_STAMP(1);
     for (int k = 0; k < a.nsteps; ++k) {
         const int step = a.step0 + k;
         const bool on = actL[x.r] != 0;
@@ -527,6 +548,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
             dtL[tid] = dtr;
         }
         __syncthreads();
+        if (k < 60) RES_STAMP(2 + k);
         bool still = false;
 #pragma unroll
         for (int j = 0; j < R; ++j) still = still || actL[j] != 0;
@@ -545,6 +567,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
         a.steps_done[rg] = done;
         if (ADAPTIVE) a.dtr[rg] = dtr;
     }
+    RES_STAMP(63);
 }
 
 }  // namespace odk

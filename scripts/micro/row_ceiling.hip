@@ -12,6 +12,11 @@
 //   owner_mem  3 voltage rows, the memory row only at the owning incidence (a design that reads
 //              each clause's memories once -- the best any re-layout of the memory reads could do)
 //   owner_min  2 voltage rows + the memory row at the owner only
+//   owner_tt   a realisable owner-only design (round 4): 3 voltage rows; the owning
+//              incidence reads the memory row, stores it and stores the clause's product row
+//              tt = xl xs (256 B, a buffer of its own); the other two incidences read that product
+//              row (written by the previous step's owner) instead of the memory row
+//   owner_tt_min  the same with the two OTHER voltage rows only
 //   stream     the compulsory bytes as one coalesced read + write pass over v and the memories
 //              (SURVEY.md §8d's 3.85 GB per step: the HBM-streaming floor)
 //   hipcc --offload-arch=gfx950 -O3 -o row_ceiling row_ceiling.hip && ./row_ceiling
@@ -40,10 +45,11 @@ struct alignas(16) Inc {
     int32_t x, y, z, w;  // clause << 2 | own position, the clause's three variables
 };
 
-template <bool OWNV, bool MEMALL>
+template <bool OWNV, bool MEMALL, bool TT = false>
 __global__ __launch_bounds__(256) void k_rows(const Inc *__restrict__ inc, const int32_t *__restrict__ vptr,
                                               const float *__restrict__ V, float *__restrict__ Vn,
-                                              const f2 *__restrict__ CM, f2 *__restrict__ CMn) {
+                                              const f2 *__restrict__ CM, f2 *__restrict__ CMn,
+                                              const float *__restrict__ TTr = nullptr, float *__restrict__ TTw = nullptr) {
     const int wave = (int)(blockIdx.x * 4 + (threadIdx.x >> 6)), lane = threadIdx.x & 63;
     const int tiles = (N + ROWS - 1) / ROWS;
     // XCD-aware like k_step's xmode 1: group g's waves on blocks b with b % 8 == g % 8
@@ -74,6 +80,7 @@ __global__ __launch_bounds__(256) void k_rows(const Inc *__restrict__ inc, const
             a[j][2] = (OWNV || own != 2) ? Vg[(size_t)r[j].w * W] : 0.0f;
             mm[j] = (MEMALL || own == 0) ? __builtin_nontemporal_load(&Cg[(size_t)(r[j].x >> 2) * W])
                                          : f2{0.0f, 0.0f};
+            if (TT && own != 0) mm[j].x = TTr[(size_t)g * M * W + (size_t)(r[j].x >> 2) * W + lane];
         }
 #pragma unroll
         for (int j = 0; j < RB; ++j) {
@@ -83,6 +90,7 @@ __global__ __launch_bounds__(256) void k_rows(const Inc *__restrict__ inc, const
                 f2 o = mm[j];
                 o.y += acc;
                 __builtin_nontemporal_store(o, &Cn[(size_t)(r[j].x >> 2) * W]);
+                if (TT) TTw[(size_t)g * M * W + (size_t)(r[j].x >> 2) * W + lane] = o.x * o.y;
             }
         }
         // voltage rows of the variables finished so far (one store per variable, as k_step)
@@ -149,6 +157,11 @@ int main() {
     CK(hipMemset(V1, 0, vbytes));
     CK(hipMemset(C0, 0, cbytes));
     CK(hipMemset(C1, 0, cbytes));
+    float *T0, *T1;
+    CK(hipMalloc(&T0, cbytes / 2));
+    CK(hipMalloc(&T1, cbytes / 2));
+    CK(hipMemset(T0, 0, cbytes / 2));
+    CK(hipMemset(T1, 0, cbytes / 2));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -179,6 +192,13 @@ int main() {
     if (run("other_v", ROWS_LAUNCH(false, true))) return 1;
     if (run("owner_mem", ROWS_LAUNCH(true, false))) return 1;
     if (run("owner_min", ROWS_LAUNCH(false, false))) return 1;
+#define TT_LAUNCH(OWNV)                                                                                         \
+    [&](int par) {                                                                                               \
+        hipLaunchKernelGGL((k_rows<OWNV, false, true>), grid, block, 0, 0, dinc, dvptr, par ? V1 : V0,          \
+                           par ? V0 : V1, par ? C1 : C0, par ? C0 : C1, par ? T1 : T0, par ? T0 : T1);         \
+    }
+    if (run("owner_tt", TT_LAUNCH(true))) return 1;
+    if (run("owner_tt_min", TT_LAUNCH(false))) return 1;
     if (run("stream", [&](int par) {
             const int64_t v4 = (int64_t)(vbytes / 16), c4 = (int64_t)(cbytes / 16);
             hipLaunchKernelGGL(k_stream, dim3(4096), block, 0, 0, (const f4 *)(par ? V1 : V0),

@@ -1,0 +1,41 @@
+"""Probe: what a simulate() call costs beyond its kernel (the headline's shape: config 2, B = 1024,
+f32, one 20-step launch per call).  N calls back to back, each timed on the host as bench.py times
+it (perf_counter around simulate + the solver's stream sync) beside its HIP-event kernel time.  Run
+it under `rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace` to see where the rest
+goes (the per-call kernel, the launch, the copy of the results, the synchronisation)."""
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from odesat_amd import cnf  # noqa: E402
+from odesat_amd import workloads as wl  # noqa: E402
+from odesat_amd.system import ODESAT_STOP_NONE, Solver  # noqa: E402
+
+K = int(os.environ.get("STEPS", "20"))
+N = int(os.environ.get("CALLS", "30"))
+c = wl.CONFIGS["config2"]
+var, neg = wl.random_ksat(c["n"], c["m"], c["k"], c["seed"])
+cp, v_, n_ = wl.formula_arrays(var, neg)
+f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
+with Solver(f, int(os.environ.get("B", "1024")), "f32") as s:
+    s.init_state(42)
+    s.simulate(dt=0.01, max_steps=5, stop=ODESAT_STOP_NONE, poll_interval=5)
+    walls, kerns = [], []
+    for i in range(N):
+        s.profile(True)
+        s.synchronize()
+        t0 = time.perf_counter()
+        s.simulate(dt=0.01, max_steps=K, stop=ODESAT_STOP_NONE, poll_interval=K)
+        s.synchronize()
+        walls.append((time.perf_counter() - t0) * 1e6)
+        ms, _ = s.profile_read()
+        s.profile(False)
+        kerns.append(ms[0] * 1e3)
+    over = [w - k for w, k in zip(walls, kerns)]
+    print(json.dumps({"steps": K, "calls": N, "wall_us_median": statistics.median(walls),
+                      "kernel_us_median": statistics.median(kerns), "overhead_us_median": statistics.median(over),
+                      "overhead_us": [round(x, 1) for x in over]}), flush=True)

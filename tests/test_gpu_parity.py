@@ -595,6 +595,44 @@ def test_onchip_adaptive_matches_resident_and_oracle(stop, monkeypatch):
     assert same(s1[0][0], ov) and same(s1[1][0], oxs) and same(s1[2][0], oxl)
 
 
+@pytest.mark.parametrize("prec", ["f32", "f64"])
+@pytest.mark.parametrize("stop", ["each", "any", "none"])
+def test_fused_owner_tt_matches_general_and_oracle(stop, prec, monkeypatch):
+    """FUSED owner-TT (round 4, kernels.hpp stream_rows3): only a clause's owning incidence reads its
+    memories and stores the next step's product xl xs for the other two.  Bit-exact against the
+    general FUSED step (ODESAT_FUSED_TT=0) on every stop policy, from a caller state with voltages
+    out of range (the first step of the call runs the general form, the rest owner-TT), and replica 0
+    against the oracle's fixed-step simulate."""
+    from odesat_amd import _lib
+    n, m = 900, 3780
+    f, (cp, v_, n_) = _instance(n, m, 21)
+    T = T_OF[prec]
+    o = Oracle(cp, v_, n_, n, prec)
+    pol = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[stop]
+    B, K = 70, 40
+    v, xs, xl = init_states(o, B, seed=5, T=T)
+    v[3, :20] *= 1.5  # out of range: the call's first step must take the general form
+    out = []
+    for tt in ("1", "0"):
+        monkeypatch.setenv("ODESAT_FUSED_TT", tt)
+        with Solver(f, B, prec) as s:
+            s.set_algorithm(_lib.ODESAT_ALG_FUSED)
+            s.set_state(v.astype(np.float64), xs.astype(np.float64), xl.astype(np.float64))
+            r1 = s.simulate(dt=0.05, max_steps=K, stop=pol, poll_interval=7)
+            r2 = s.simulate(dt=0.05, max_steps=K, stop=pol, poll_interval=7, resume=True)  # in range from the start
+            out.append((r1, r2, s.get_state()))
+    (a1, a2, sa), (b1, b2, sb) = out
+    for x, y in ((a1, b1), (a2, b2)):
+        assert np.array_equal(x["first_sat_step"], y["first_sat_step"]) and np.array_equal(x["steps_done"], y["steps_done"])
+        assert x["steps_run"] == y["steps_run"]
+    for x, y in zip(sa, sb):
+        assert same(x, y)
+    if stop == "none":  # every replica took both calls' 2K steps
+        ov, oxs, oxl = v[0].copy(), xs[0].copy(), xl[0].copy()
+        o.simulate(ov, oxs, oxl, dt=T(0.05), steps=2 * K, zeta=T(0.001))
+        assert same(sa[0][0], ov) and same(sa[1][0], oxs) and same(sa[2][0], oxl)
+
+
 def test_onchip_adaptive_inter_after_out_of_range_set_state():
     """adaptive STOP_ANY (simulate_inter) on an ONCHIP solver whose caller state is
     out of range.  The first step runs RESIDENT's adaptive step in place (one step, nothing to
