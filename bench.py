@@ -381,6 +381,17 @@ def roofline(args, short, ms, launches, clause_bytes_step, batch=None, dtype=Non
                   "unit": "G VALU wave-instructions/s", "frac": achieved / VALU_PEAK_GINST,
                   "valu_insts_per_launch": valu, "hbm_algorithmic": hbm,
                   "note": ONCHIP_NOTE if short == "k_onchip" else WAVE_NOTE})
+        if pj.get("grbm_cycles_per_step"):  # the step in cycles against its two issue floors
+            cyc = pj["grbm_cycles_per_step"] / 8.0  # GRBM_GUI_ACTIVE sums the 8 XCDs
+            vf = pj["valu_insts_per_step"] / 1024 * 2.0  # 1024 SIMDs, a wave64 VALU op issues in 2 cycles
+            lf = pj["lds_insts_per_step"] / 256 * 2.0 if pj.get("lds_insts_per_step") else None  # >= 2 LDS cycles each
+            r["cycle_model"] = {
+                "cycles_per_step": cyc, "valu_issue_floor": vf, "valu_floor_frac": vf / cyc,
+                "lds_issue_floor": lf, "lds_floor_frac": lf / cyc if lf else None,
+                "note": "PMC GRBM_GUI_ACTIVE per step (profile fit, per XCD) against the VALU and LDS issue "
+                        "floors of the same step: neither issue resource binds; the rest is the dependency "
+                        "chain of the dv read-modify-writes and barriers (DESIGN.md §4.0, §6.0: the cycle "
+                        "count is clock-independent, the launch time is not)"}
         if pj.get("lds_insts_per_step") is not None:  # LDS instruction issue beside it (one per CU per cycle)
             lds = pj["lds_insts_fixed"] + pj["lds_insts_per_step"] * steps_per_launch
             r["lds_issue"] = {"achieved": lds / per_launch_s / 1e9, "peak": LDS_PEAK_GINST,

@@ -57,6 +57,8 @@ def main():
         res["valu_insts_fixed"], res["valu_insts_per_step"] = fit("SQ_INSTS_VALU")
     if all("SQ_INSTS_LDS" in p for p in (p1, p2)):
         res["lds_insts_fixed"], res["lds_insts_per_step"] = fit("SQ_INSTS_LDS")
+    if all("GRBM_GUI_ACTIVE" in p for p in (p1, p2)):  # busy GPU cycles, summed over the 8 XCDs
+        res["grbm_cycles_fixed"], res["grbm_cycles_per_step"] = fit("GRBM_GUI_ACTIVE")
     res["note"] = ("per launch of k steps: fixed + k * per_step; HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 "
                    "FETCH_SIZE correction), one --pmc pass per counter group, kernel trace only")
     json.dump(res, open(out, "w"), indent=1)
