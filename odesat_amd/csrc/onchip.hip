@@ -227,6 +227,58 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
     asm volatile("" : "+v"(mem.x), "+v"(mem.y));  // update now: sunk into later tiles it keeps mn live
 }
 
+// Split barriers between the pairs of register tiles (ONCHIP_SPLITBAR, round 4): instead of a
+// workgroup barrier after the second tile of a pair, each wave adds 1 to an LDS counter right after
+// that tile's dv writes, and waits -- polling the counter -- only before the NEXT pair's first dv
+// read-modify-write.  The independent work of the tile (the gathers of tile t+3, the halves of tiles
+// t+1 and t+2) runs between the two, so a wave that finished early no longer idles at a barrier.
+// Ordering: a wave's LDS operations are performed in issue order, so a counter increment is performed
+// after that wave's dv writes; a wave that has read the counter at its target issues its dv reads
+// after that read returned, i.e. after every wave's writes of the pair.
+#ifndef ONCHIP_SPLITBAR
+#define ONCHIP_SPLITBAR 0
+#endif
+typedef __attribute__((address_space(3))) uint32_t lu32;
+// (The counter is one word per wave -- the number of pairs it has signalled -- written by all of the
+// wave's lanes (one address: no lane branch, which would cost the unrolled tile code its registers);
+// a waiting wave's lane l reads wave l % 8's word and the wave proceeds once every word is at the
+// target.)
+__device__ __forceinline__ void pair_signal(uint32_t cnt, uint32_t ep) {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
+    *reinterpret_cast<volatile lu32 *>(cnt + 4u * (threadIdx.x >> 6)) = ep;
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+// The poll is one inline-assembly loop, invisible to the compiler's control flow: a loop in the
+// unrolled tile sequence cost it 40-65 spilled VGPRs.  (All 64 lanes are active here.)  It gives up
+// after 2^22 polls (~0.1 s), so a broken count can never hang the GPU (the results would then be
+// wrong, which the parity tests see).
+__device__ __forceinline__ void pair_wait(uint32_t cnt, uint32_t target) {
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t addr = cnt + 4u * (threadIdx.x & 7);
+    uint32_t tmp, it;
+    uint64_t msk;
+    asm volatile(
+        "s_mov_b32 %2, 0\n"
+        "L_pw%=:\n\t"
+        "ds_read_b32 %0, %3\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_ge_u32_e64 %1, %0, %4\n\t"
+        "s_cmp_eq_u64 %1, exec\n\t"
+        "s_cbranch_scc1 L_pd%=\n\t"
+        "s_add_u32 %2, %2, 1\n\t"
+        "s_cmp_gt_u32 %2, 0x400000\n\t"
+        "s_cbranch_scc1 L_pd%=\n\t"
+        "s_sleep 1\n\t"
+        "s_branch L_pw%=\n"
+        "L_pd%=:"
+        : "=&v"(tmp), "=&s"(msk), "=&s"(it)
+        : "v"(addr), "s"(target)
+        : "memory", "scc");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // One tile step.  In flight: P = tile t's dv terms, Fn = tile t+1's first half, Gn = tile t+2's
 // gathered voltages, ring = the records of tiles t+3 .. t+6.  The critical chain of a step is tile
 // t's dv read-modify-write (:80; three distinct variables per clause, so the updates are
@@ -235,13 +287,17 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
 // t+2's first half -- independent, so they interleave -- while the writes and the gathers drain.
 // After the second tile of a pair (bar), the barrier orders the pair's dv updates against the next
 // pair's; inside a pair the same-wave order suffices (see the header).
+template <bool SPL = false>
 __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, SlotF &slot3, float2 &mem1, Pend &P, Front &Fn,
-                                          Gath &Gn, int t, float h, float hh, uint32_t &cmax, Stamps &S, bool bar) {
+                                          Gath &Gn, int t, float h, float hh, uint32_t &cmax, Stamps &S, bool bar,
+                                          bool first = false, uint32_t cnt = 0, uint32_t *ep = nullptr) {
+    if (SPL && first) pair_wait(cnt, *ep);  // every wave's dv writes of the previous pair are performed
     const float o0 = lds_f(P.a0 + DVC), o1 = lds_f(P.a1 + DVC), o2 = lds_f(P.a2 + DVC);
     lds_st(P.a0 + DVC, o0 + P.d0);
     lds_st(P.a1 + DVC, o1 + P.d1);
     lds_st(P.a2 + DVC, o2 + P.d2);
     __builtin_amdgcn_sched_barrier(0);
+    if (SPL && bar) pair_signal(cnt, ++*ep);
 #if defined(ONCHIP_STAMPS) && ONCHIP_STAMPS == 2
     const uint64_t t_rmw = memtime();
     S.rmw += t_rmw - S.last;
@@ -257,7 +313,7 @@ __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, SlotF &s
     const uint64_t t_pre = memtime();
     S.work += t_pre - S.last;
 #endif
-    if (bar) __syncthreads();  // static: only after the second tile of a pair
+    if (bar && !SPL) __syncthreads();  // static: only after the second tile of a pair
     __builtin_amdgcn_sched_barrier(0);
 #ifdef ONCHIP_STAMPS
     S.last = memtime();
@@ -279,14 +335,17 @@ __device__ __forceinline__ uint32_t mem_addr(const Args &a, int lt, int lane) {
 // the copies that merge mr[] there double its VGPR footprint.
 template <int TR, int OFF, int T>
 __device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&mr)[TR], SlotF (&ring)[4], Pend &P,
-                                         Front &Fn, Gath &Gn, float h, float hh, int lane, uint32_t &cmax, Stamps &S) {
+                                         Front &Fn, Gath &Gn, float h, float hh, int lane, uint32_t &cmax, Stamps &S,
+                                         uint32_t cnt, uint32_t *ep) {
     constexpr bool bar = ((T + OFF) & 1) != 0;  // wave-paired tiles: a barrier after the second of a pair
+    constexpr bool first = T > 0 && ((T - 1 + OFF) & 1) != 0;  // the first tile of a pair after another pair
+    constexpr bool SPL = ONCHIP_SPLITBAR != 0;
     if constexpr (T + 1 < TR) {
-        tile_step(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, cmax, S, bar);
+        tile_step<SPL>(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, cmax, S, bar, first, cnt, ep);
     } else {  // tile TR is the first LDS tile (if any)
         float2 m = make_float2(0.0f, 0.0f);
         if (a.tl > 0) m = *lds_f2(mem_addr(a, 0, lane));
-        tile_step(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, cmax, S, bar);
+        tile_step<SPL>(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, cmax, S, bar, first, cnt, ep);
         if (a.tl > 0) *lds_f2(mem_addr(a, 0, lane)) = m;
     }
 }
@@ -294,13 +353,14 @@ __device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&
 template <int TR, int OFF, int... Ts>
 __device__ __forceinline__ void reg_tiles(std::integer_sequence<int, Ts...>, const Args &a, const Recs &R,
                                           float2 (&mr)[TR], SlotF (&ring)[4], Pend &P, Front &Fn, Gath &Gn, float h,
-                                          float hh, int lane, uint32_t &cmax, Stamps &S) {
-    (reg_tile<TR, OFF, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S), ...);
+                                          float hh, int lane, uint32_t &cmax, Stamps &S, uint32_t cnt, uint32_t *ep) {
+    (reg_tile<TR, OFF, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S, cnt, ep), ...);
 }
 
 // One RHS pass + memory update over every tile; ends with a barrier (dv complete).
 template <int TR, int OFF>
-__device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, int lane, uint32_t &cmax, Stamps &S) {
+__device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, int lane, uint32_t &cmax, Stamps &S,
+                                     uint32_t cnt, uint32_t &ep) {
     Recs R;
 #if ONCHIP_REC12
     R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec12, 0, (int)a.rec12_bytes, 0x00020000);
@@ -328,8 +388,9 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
     front(G0, F0);
     front(G1, Fn);
     back(a, F0, mr[0], h, hh, P, cmax);
-    reg_tiles<TR, OFF>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S);
-    // LDS tiles [TR, TR + tl): tl is a multiple of 4 (the host pads the tiling)
+    reg_tiles<TR, OFF>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S, cnt, &ep);
+    // LDS tiles [TR, TR + tl): tl is a multiple of 4 (the host pads the tiling); they keep plain barriers
+    if (ONCHIP_SPLITBAR && a.tl > 0) __syncthreads();
     const int NT = TR + a.tl;
     const int last = a.tl - 1;
     for (int t0 = TR; t0 < NT; t0 += 4) {
@@ -345,7 +406,7 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
             if (lt <= last) *lds_f2(ma) = m;
         }
     }
-    if constexpr (OFF == 1) __syncthreads();  // the last tile (TR + tl - 1, odd) ends no pair
+    if constexpr (OFF == 1 || ONCHIP_SPLITBAR) __syncthreads();  // the last tile (TR + tl - 1, odd) ends no pair
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -447,12 +508,16 @@ __device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &me
 
 __device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &slot3, float2 &mem1, Pend &P,
                                            FrontA &Fn, GathA &Gn, int t, float h, float hh, float hq, uint32_t sb,
-                                           bool p2, uint32_t &cmax, float &e, bool bar) {
+                                           bool p2, uint32_t &cmax, float &e, bool bar, bool first, uint32_t cnt,
+                                           uint32_t &ep) {
+    constexpr bool SPL = ONCHIP_SPLITBAR != 0;
+    if (SPL && first) pair_wait(cnt, ep);  // (split barriers: see tile_step)
     const float o0 = lds_f(P.a0 + ADA_D), o1 = lds_f(P.a1 + ADA_D), o2 = lds_f(P.a2 + ADA_D);
     lds_st(P.a0 + ADA_D, o0 + P.d0);
     lds_st(P.a1 + ADA_D, o1 + P.d1);
     lds_st(P.a2 + ADA_D, o2 + P.d2);
     __builtin_amdgcn_sched_barrier(0);
+    if (SPL && bar) pair_signal(cnt, ++ep);
     GathA G3;
     gatherA(slot3, G3, sb);
     slot3 = load_rec(R, t + 7);
@@ -460,7 +525,7 @@ __device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &s
     backA(a, Fn, mem1, h, hh, hq, p2, P, cmax, e);
     frontA(Gn, Fn);
     __builtin_amdgcn_sched_barrier(0);
-    if (bar) __syncthreads();
+    if (bar && !SPL) __syncthreads();
     __builtin_amdgcn_sched_barrier(0);
     Gn = G3;
 }
@@ -469,21 +534,23 @@ __device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &s
 template <int TR, int OFF, int T>
 __device__ __forceinline__ void reg_tileA(const Args &a, const Recs &R, float2 (&mr)[TR], Slot (&ring)[4], Pend &P,
                                           FrontA &Fn, GathA &Gn, float h, float hh, float hq, uint32_t sb, bool p2,
-                                          uint32_t &cmax, float &e) {
+                                          uint32_t &cmax, float &e, uint32_t cnt, uint32_t &ep) {
     constexpr bool bar = ((T + OFF) & 1) != 0 && T + 1 < TR;
+    constexpr bool first = T > 0 && ((T - 1 + OFF) & 1) != 0;  // the first tile of a pair after another pair
     if constexpr (T + 1 < TR) {
-        tile_stepA(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, hq, sb, p2, cmax, e, bar);
+        tile_stepA(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, hq, sb, p2, cmax, e, bar, first, cnt, ep);
     } else {  // the (empty) tile after the last: stand-in memories (zero error terms), nothing stored
         float2 m = make_float2(0.001f, 1.0f);
-        tile_stepA(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, hq, sb, p2, cmax, e, bar);
+        tile_stepA(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, hq, sb, p2, cmax, e, bar, first, cnt, ep);
     }
 }
 
 template <int TR, int OFF, int... Ts>
 __device__ __forceinline__ void reg_tilesA(std::integer_sequence<int, Ts...>, const Args &a, const Recs &R,
                                            float2 (&mr)[TR], Slot (&ring)[4], Pend &P, FrontA &Fn, GathA &Gn, float h,
-                                           float hh, float hq, uint32_t sb, bool p2, uint32_t &cmax, float &e) {
-    (reg_tileA<TR, OFF, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, hq, sb, p2, cmax, e), ...);
+                                           float hh, float hq, uint32_t sb, bool p2, uint32_t &cmax, float &e,
+                                           uint32_t cnt, uint32_t &ep) {
+    (reg_tileA<TR, OFF, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, hq, sb, p2, cmax, e, cnt, ep), ...);
 }
 
 // One adaptive pass over every tile (all in registers): the RHS at the source sb (0: A, ADA_H: H)
@@ -491,7 +558,7 @@ __device__ __forceinline__ void reg_tilesA(std::integer_sequence<int, Ts...>, co
 // (:88).  Ends with a barrier.
 template <int TR, int OFF>
 __device__ __forceinline__ void passA(const Args &a, float2 (&mr)[TR], float h, int lane, uint32_t sb, bool p2,
-                                      uint32_t flag, float &e) {
+                                      uint32_t flag, float &e, uint32_t cnt, uint32_t &ep) {
     Recs R;
     R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec, 0, (int)a.rec_bytes, 0x00020000);
     R.voff = (uint32_t)lane * 8u;
@@ -514,7 +581,8 @@ __device__ __forceinline__ void passA(const Args &a, float2 (&mr)[TR], float h, 
     frontA(G0, F0);
     frontA(G1, Fn);
     backA(a, F0, mr[0], h, hh, hq, p2, P, cmax, e);
-    reg_tilesA<TR, OFF>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, hq, sb, p2, cmax, e);
+    reg_tilesA<TR, OFF>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, hq, sb, p2, cmax, e,
+                        cnt, ep);
     if (!p2 && !(__uint_as_float(cmax) < 0.5f)) lds_st(flag, 1.0f);
     __syncthreads();
 }
@@ -683,9 +751,13 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         const int c0 = tcw[(TR + t) * WAVES];
         *lds_f2(mem_addr(a, t, lane)) = ld_state(&CM[min(c0 + wl, mlast)]);  // (empty slots: as mem_io)
     }
+    // the waves' pair counts (split barriers): after the unsat flags (adaptive: and the error words)
+    const uint32_t CNT = UNS + 8u + (ADA ? 4u * WAVES : 0u);
     if (lane < 2) lds_st(UNS + 4u * lane, 0.0f);
+    if (ONCHIP_SPLITBAR && lane < WAVES) lds_st(CNT + 4u * lane, 0.0f);
     __syncthreads();
     ONCHIP_PHASE(1);
+    uint32_t ep = 0u;  // the pairs every wave has signalled so far
 
     const float h = a.dt, hh = 0.5f * a.dt;
     Stamps S{};
@@ -700,7 +772,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
 #pragma clang loop unroll(disable)
             for (int ps = 0; ps < 2; ++ps) {
                 const bool p2 = ps == 1;
-                passA<TR, OFF>(a, mr, hk, lane, p2 ? ADA_H : 0u, p2, flag, e);  // RHS at y, then at the half step
+                passA<TR, OFF>(a, mr, hk, lane, p2 ? ADA_H : 0u, p2, flag, e, CNT, ep);  // RHS at y, then at the half step
                 if (!p2) {
                     uns = lds_f(flag) != 0.0f;  // uniform
                     if (!uns) {  // an allsat replica takes no step (:122): drop pass 1's terms
@@ -782,7 +854,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
 #ifdef ONCHIP_STAMPS
         S.last = memtime();
 #endif
-        pass<TR, OFF>(a, mr, h, lane, cmax, S);
+        pass<TR, OFF>(a, mr, h, lane, cmax, S, CNT, ep);
         if (!(__uint_as_float(cmax) < 0.5f)) lds_st(UNS + 4u * (k & 1), 1.0f);
         // :96 (h dv = (h/2) dv2), dv restarts at 0 (:33): four variables per lane and access (v and dv
         // are 16-byte aligned), then the n % 4 last ones

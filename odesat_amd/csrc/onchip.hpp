@@ -25,7 +25,8 @@ constexpr int MAX_N = (int)(DVC / 4) - SINKS;  // v and its sinks below DVC
 constexpr size_t LDS_MAX = 160 * 1024;
 
 // LDS map (bytes): v[n + SINKS] at 0 (sinks = 1.0), memory tiles in the gap up to DVC, 2 dv[n +
-// SINKS] (twice dv: see onchip.hip) at DVC, two unsat flags, then the remaining memory tiles.
+// SINKS] (twice dv: see onchip.hip) at DVC, two unsat flags, the waves' pair counts (ONCHIP_SPLITBAR),
+// then the remaining memory tiles.
 struct Lds {
     uint32_t gap_base, gap_tiles, after_base, after_tiles;
 };
@@ -34,7 +35,7 @@ inline Lds lds_map(int64_t n) {
     const uint32_t vend = (uint32_t)(4 * (n + SINKS));
     L.gap_base = (vend + 7u) & ~7u;
     L.gap_tiles = L.gap_base < DVC ? (DVC - L.gap_base) / TILE_LDS : 0;
-    L.after_base = ((DVC + vend + 8u) + 7u) & ~7u;
+    L.after_base = ((DVC + vend + 8u + 4u * WAVES) + 7u) & ~7u;  // after dv: two unsat flags, the waves' pair counts
     L.after_tiles = L.after_base < LDS_MAX ? (uint32_t)((LDS_MAX - L.after_base) / TILE_LDS) : 0;
     return L;
 }
@@ -53,7 +54,7 @@ inline int tl_max(int64_t n) {
 // the ds instructions' 16-bit immediate of A, as DVC), H = the half step, F = the full-step clone,
 // n + SINKS floats each; A's region also holds the unsat flags and the waves' error words.
 constexpr uint32_t ADA_D = 40960, ADA_H = 81920, ADA_F = 122880;
-constexpr int ADA_FLAGS = 2 + WAVES;
+constexpr int ADA_FLAGS = 2 + 2 * WAVES;  // two unsat flags, the waves' error words, their pair counts
 constexpr int ADA_MAX_N = (int)(ADA_D / 4) - SINKS - ADA_FLAGS;
 
 struct Args {
