@@ -25,6 +25,7 @@
 #include <cstdint>
 
 #include "../../include/odesat.h"
+#include "callio.hpp"
 
 namespace odk {
 

@@ -57,6 +57,10 @@ struct odesat_solver {
     void *dtr = nullptr, *err = nullptr;
     void *tt[2] = {nullptr, nullptr};  // FUSED owner-TT: clause products xl xs [G][m][W], double-buffered (lazy)
     bool fused_tt = true;              // ODESAT_FUSED_TT=0: every incidence reads the clause's memories (A/B)
+    // per-call bookkeeping of the persistent kernels (callio.hpp): io_begin -- the next launch starts the
+    // call (no k_begin_call); io_mirror -- launches store the results in the pinned host buffers
+    bool io_begin = false, io_mirror = false;
+    bool io_fold = true;               // ODESAT_CALL_FOLD=0: k_begin_call and the result copy (A/B)
     uint32_t *unsat = nullptr;
     uint8_t *act = nullptr;
     int64_t *sat_step = nullptr, *steps_done = nullptr;
@@ -409,6 +413,20 @@ int dispatch_step(odesat_solver *s, int step, bool adaptive, double dt, double z
                   int gA, int gB, bool tt = false) {
     return s->dtype == ODESAT_F64 ? enqueue_step<double>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB, tt)
                                   : enqueue_step<float>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB, tt);
+}
+
+// The CallIO of the next persistent launch: `begin` for the first launch of a folded call only.
+CallIO take_io(odesat_solver *s) {
+    CallIO io;
+    io.B = (int32_t)s->B;
+    io.begin = s->io_begin ? 1 : 0;
+    s->io_begin = false;
+    if (s->io_mirror) {
+        io.h_sat = s->h_sat;
+        io.h_done = s->h_done;
+        io.h_dt = s->h_dt;
+    }
+    return io;
 }
 
 // FUSED owner-TT (kernels.hpp stream_rows3) applies to fixed steps of the 3-SAT incidence stream
@@ -856,6 +874,7 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     a.zeta = (T)zeta;
     a.xl_max = (T)1e4 * (T)s->m;  // system.rs:95
     a.tol = tol;
+    a.io = take_io(s);
     a.G = s->G;
     if (s->solo) {
         auto so = [&](auto cc, auto vv) -> int {
@@ -932,6 +951,7 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
     a.zeta = (T)zeta;
     a.xl_max = (T)1e4 * (T)s->m;  // system.rs:95
     a.tol = tol;
+    a.io = take_io(s);
     const bool k3 = s->uniform_k == 3;
     // 3-SAT on in-range states: the short arithmetic (res_clause3's FAST forms)
     const bool f3 = k3 && fast && s->res_fast;
@@ -1004,6 +1024,7 @@ int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zet
     a.stop_mode = stop_mode;
     a.dt = (float)dt;
     a.xl_max = 1e4f * (float)s->m;  // system.rs:95, as (T)1e4 * (T)m
+    a.io = take_io(s);
     {
         Timed tm(s, 0);
         const size_t lds = adaptive ? onchip::LDS_MAX : onchip::lds_bytes(s->n, s->oc_tl);
@@ -1361,6 +1382,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             s->VEC = std::atoi(ev);
     if (const char *ev = std::getenv("ODESAT_RB")) s->rb = std::atoi(ev) == 8 ? 8 : 4;
     if (const char *ev = std::getenv("ODESAT_FUSED_TT")) s->fused_tt = std::atoi(ev) != 0;
+    if (const char *ev = std::getenv("ODESAT_CALL_FOLD")) s->io_fold = std::atoi(ev) != 0;
     s->W = s->LW * s->VEC;
     s->Bp = (batch + s->W - 1) / s->W * s->W;
     s->G = (int)(s->Bp / s->W);
@@ -1730,14 +1752,18 @@ extern "C" int odesat_euler_step(odesat_solver *s, double tol, double *dt, doubl
 // Results of a simulate call: per-replica bookkeeping through the pinned staging buffers, one sync.
 static int finish_simulate(odesat_solver *s, const odesat_params *p, bool adaptive, int64_t t_run,
                            int64_t *first_sat_step, int64_t *steps_done, double *dt_out, int64_t *steps_run) {
-    if (first_sat_step && steps_done)  // one copy: the two arrays are adjacent (Bp apart)
-        HIP_TRY(hipMemcpyAsync(s->h_sat, s->sat_step, (s->Bp + s->B) * 8, hipMemcpyDeviceToHost, s->stream));
-    else if (first_sat_step)
-        HIP_TRY(hipMemcpyAsync(s->h_sat, s->sat_step, s->B * 8, hipMemcpyDeviceToHost, s->stream));
-    else if (steps_done)
-        HIP_TRY(hipMemcpyAsync(s->h_done, s->steps_done, s->B * 8, hipMemcpyDeviceToHost, s->stream));
-    if (dt_out && adaptive)
-        HIP_TRY(hipMemcpyAsync(s->h_dt, s->dtr, s->B * s->tsize, hipMemcpyDeviceToHost, s->stream));
+    const bool mirrored = s->io_mirror;  // the launches stored the results in the pinned buffers themselves
+    s->io_mirror = s->io_begin = false;
+    if (!mirrored) {
+        if (first_sat_step && steps_done)  // one copy: the two arrays are adjacent (Bp apart)
+            HIP_TRY(hipMemcpyAsync(s->h_sat, s->sat_step, (s->Bp + s->B) * 8, hipMemcpyDeviceToHost, s->stream));
+        else if (first_sat_step)
+            HIP_TRY(hipMemcpyAsync(s->h_sat, s->sat_step, s->B * 8, hipMemcpyDeviceToHost, s->stream));
+        else if (steps_done)
+            HIP_TRY(hipMemcpyAsync(s->h_done, s->steps_done, s->B * 8, hipMemcpyDeviceToHost, s->stream));
+        if (dt_out && adaptive)
+            HIP_TRY(hipMemcpyAsync(s->h_dt, s->dtr, s->B * s->tsize, hipMemcpyDeviceToHost, s->stream));
+    }
     if (p->stop == ODESAT_STOP_ANY) HIP_TRY(hipMemcpyAsync(s->h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
     // simulate_inter runs T + 1 steps when step T is the first allsat one (system.rs:291): launches
@@ -1877,7 +1903,17 @@ static int simulate_impl(odesat_solver *s, const odesat_params *p, bool cont, in
     const double zeta = p->zeta < 0 ? default_zeta(s) : p->zeta;
     if ((rc = ensure_w(s))) return rc;
     if (adaptive && (rc = ensure_scratch(s))) return rc;
-    if (!cont) {  // per-call bookkeeping restarts; adaptive dt restarts at 0.01 (:205) -- one async kernel
+    // the persistent kernels (simulate_resident) take the call's first-launch bookkeeping reset and, on
+    // STOP_NONE calls, the copy of the results into their own launches (callio.hpp); STOP_ANY keeps
+    // k_begin_call (its stop word must be reset before any workgroup reads it)
+    const bool persistent = (s->alg == ODESAT_ALG_ONCHIP && (!adaptive || s->oc_ada)) ||
+                            ((s->alg == ODESAT_ALG_RESIDENT || s->alg == ODESAT_ALG_ONCHIP) && (!adaptive || s->res_ada));
+    s->io_begin = s->io_mirror = false;
+    if (!cont && persistent && s->io_fold && p->stop != ODESAT_STOP_ANY) {
+        s->t_base = 0;
+        s->io_begin = true;
+        s->io_mirror = p->stop == ODESAT_STOP_NONE;
+    } else if (!cont) {  // per-call bookkeeping restarts; adaptive dt restarts at 0.01 (:205) -- one async kernel
         s->t_base = 0;
         const int threads = 256;
         hipLaunchKernelGGL(k_begin_call, dim3((unsigned)((s->Bp + threads - 1) / threads)), dim3(threads), 0,

@@ -687,7 +687,8 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     const int g = blockIdx.x, lane = threadIdx.x;
     const int wl = lane & 63;  // slot of this lane in its wave's share of a tile
     ONCHIP_PHASE(0);
-    int act = a.act[g];
+    if (lane == 0) io_begin_store<float>(a.io, g, a.act, a.sat_step, a.steps_done, a.dtr, ADA, a.stop);
+    int act = io_active(a.io, a.act, g);
     if (!act) return;  // frozen replica (uniform)
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
     const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
@@ -700,7 +701,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     constexpr uint32_t DV = ADA ? ADA_D : DVC;
     // two unsat flags (adaptive: after A's sinks, then the waves' error words)
     const uint32_t UNS = ADA ? 4u * (uint32_t)n2 : DVC + 4u * (uint32_t)n2;
-    int64_t sat = a.sat_step[g], done = a.steps_done[g];
+    int64_t sat = io_sat(a.io, a.sat_step, g), done = io_done(a.io, a.steps_done, g);
     const cint32 *tcw = (const cint32 *)a.tc + __builtin_amdgcn_readfirstlane(lane >> 6);  // this wave's starts
 
     // The clause memories first: their loads (one per register tile and lane) stay in flight while v
@@ -761,7 +762,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
 
     const float h = a.dt, hh = 0.5f * a.dt;
     Stamps S{};
-    float dtr = ADA ? a.dtr[g] : a.dt;
+    float dtr = ADA ? io_dt<float>(a.io, a.dtr, g) : a.dt;
     if constexpr (ADA) {
         for (int k = 0; k < a.nsteps; ++k) {  // euler_step (system.rs:111-139)
             const float hk = dtr, hhk = 0.5f * dtr, hqk = 0.25f * dtr;
@@ -927,6 +928,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         a.sat_step[g] = sat;
         a.steps_done[g] = done;
         if (ADA) a.dtr[g] = dtr;
+        io_mirror<float>(a.io, g, sat, done, dtr, ADA);
     }
 }
 

@@ -13,6 +13,8 @@
 #include <cstddef>
 #include <cstdint>
 
+#include "callio.hpp"
+
 namespace onchip {
 
 constexpr int NTH = 512;           // threads per workgroup = tile capacity in clauses
@@ -78,6 +80,7 @@ struct Args {
     Lds lds;
     float *dtr;          // [B] per-replica adaptive dt (adaptive launches)
     float tol;           // adaptive tolerance, as the solver's f32
+    CallIO io;           // per-call bookkeeping (callio.hpp)
 };
 
 // Register-tile counts compiled (template instantiations; VGPRs ~ 50 + 2 TR, ~245 at TR = 96).

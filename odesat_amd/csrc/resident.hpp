@@ -58,6 +58,7 @@ template <typename T> struct RArgs {
                   // launch's starting state survives for a STOP_ANY replay), then par flips
     T dt, zeta, xl_max;
     double tol;
+    CallIO io;  // per-call bookkeeping (callio.hpp)
 };
 
 // Pass kinds: P_FIXED one fixed step in place; P_ADA1 each clause's C to scratch (the memories stay
@@ -448,10 +449,11 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     int act = 0;
     if (tid < R) {
         const int rg = g * R + tid;
-        act = a.act[rg];
-        sat = a.sat_step[rg];
-        done = a.steps_done[rg];
-        if (ADAPTIVE) dtr = a.dtr[rg];
+        io_begin_store<T>(a.io, rg, a.act, a.sat_step, a.steps_done, a.dtr, ADAPTIVE, a.stop);
+        act = io_active(a.io, a.act, rg);
+        sat = io_sat(a.io, a.sat_step, rg);
+        done = io_done(a.io, a.steps_done, rg);
+        if (ADAPTIVE) dtr = io_dt<T>(a.io, a.dtr, rg);
         actL[tid] = act;
         dtL[tid] = dtr;
         unsL[tid] = 0u;
@@ -566,6 +568,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
         a.sat_step[rg] = sat;
         a.steps_done[rg] = done;
         if (ADAPTIVE) a.dtr[rg] = dtr;
+        io_mirror<T>(a.io, rg, sat, done, dtr, ADAPTIVE);
     }
     RES_STAMP(63);
 }

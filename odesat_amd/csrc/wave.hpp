@@ -44,6 +44,7 @@ template <typename T> struct WArgs {
     int32_t oop;  // 1: the final state goes to the other buffer and par flips (STOP_ANY replay)
     T dt, zeta, xl_max;
     double tol;
+    CallIO io;  // per-call bookkeeping (callio.hpp)
 };
 
 // LDS bytes of one replica: v, its full-step clone (adaptive), the terms, the memories and (adaptive)
@@ -275,12 +276,13 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
     copy_to_lds<8>(rec4, a.rec4, (int)threadIdx.x, a.m, NL * WPW);
     copy_to_lds<8>(vst, a.vst, (int)threadIdx.x, a.n + 1, NL * WPW);
     __syncthreads();
+    if (l == 0 && g < a.G) io_begin_store<T>(a.io, g, a.act, a.sat_step, a.steps_done, a.dtr, ADAPTIVE, a.stop);
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
-    const bool live = g < a.G && a.act[g] != 0;  // uniform per team
+    const bool live = g < a.G && io_active(a.io, a.act, g);  // uniform per team
     if (TW == 1 ? !live : !__syncthreads_or(live)) return;
     int act = live;
-    int64_t sat = live ? a.sat_step[g] : -1, done = live ? a.steps_done[g] : 0;
-    T dtr = ADAPTIVE && live ? a.dtr[g] : a.dt;
+    int64_t sat = live ? io_sat(a.io, a.sat_step, g) : -1, done = live ? io_done(a.io, a.steps_done, g) : 0;
+    T dtr = ADAPTIVE && live ? io_dt<T>(a.io, a.dtr, g) : a.dt;
     // the replica's LDS: memories first (16-byte aligned: read and written as (xs, xl) pairs), the
     // first pass's C (adaptive), v, its full-step clone (adaptive), the terms
     T *cmL = reinterpret_cast<T *>(wave_smem + a.topo_bytes + (size_t)w * a.rep_bytes);
@@ -377,6 +379,7 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
         a.sat_step[g] = sat;
         a.steps_done[g] = done;
         if (ADAPTIVE) a.dtr[g] = dtr;
+        io_mirror<T>(a.io, g, sat, done, dtr, ADAPTIVE);
     }
 }
 
@@ -444,8 +447,9 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
     __shared__ __attribute__((aligned(16))) int voteW[2][SOLO_MAX_NL / 64];
     const int NL = (int)blockDim.x, l = (int)threadIdx.x, TW = NL / 64;
     const int g = blockIdx.x;  // this workgroup's replica (group width 1)
+    if (l == 0 && g < a.G) io_begin_store<T>(a.io, g, a.act, a.sat_step, a.steps_done, a.dtr, ADAPTIVE, a.stop);
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
-    if (g >= a.G || a.act[g] == 0) return;                              // uniform per workgroup
+    if (g >= a.G || !io_active(a.io, a.act, g)) return;                // uniform per workgroup
     T *vL = reinterpret_cast<T *>(wave_smem);
     T *tL = vL + a.n;
     const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
@@ -479,8 +483,8 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
     if (l < 2 * (SOLO_MAX_NL / 64)) voteW[l >> 4][l & 15] = 0;
     __syncthreads();
     int act = 1;
-    int64_t sat = a.sat_step[g], done = a.steps_done[g];
-    T dtr = ADAPTIVE ? a.dtr[g] : a.dt;
+    int64_t sat = io_sat(a.io, a.sat_step, g), done = io_done(a.io, a.steps_done, g);
+    T dtr = ADAPTIVE ? io_dt<T>(a.io, a.dtr, g) : a.dt;
     // phase 1 over this lane's clauses: the voltage gathers of every slot first, then the arithmetic
     auto clauses = [&](auto pk, T h, T &e) -> bool {
         constexpr int PK = decltype(pk)::value;
@@ -620,6 +624,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
         a.sat_step[g] = sat;
         a.steps_done[g] = done;
         if (ADAPTIVE) a.dtr[g] = dtr;
+        io_mirror<T>(a.io, g, sat, done, dtr, ADAPTIVE);
     }
 }
 
@@ -657,8 +662,9 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
     __shared__ __attribute__((aligned(16))) int voteW[2][SOLO_MAX_NL / 64];
     const int NL = (int)blockDim.x, l = (int)threadIdx.x;
     const int g = blockIdx.x;
+    if (l == 0 && g < a.G) io_begin_store<T>(a.io, g, a.act, a.sat_step, a.steps_done, a.dtr, ADAPTIVE, a.stop);
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
-    if (g >= a.G || a.act[g] == 0) return;                              // uniform per workgroup
+    if (g >= a.G || !io_active(a.io, a.act, g)) return;                // uniform per workgroup
     const int n = a.n;
     T *vL = reinterpret_cast<T *>(wave_smem);
     T *pL = vL + (n + PER16 - 1) / PER16 * PER16;  // padded blocks, then the overflow area
@@ -706,8 +712,8 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
     if (l < 2) errM[l] = 0;
     __syncthreads();
     int act = 1;
-    int64_t sat = a.sat_step[g], done = a.steps_done[g];
-    T dtr = ADAPTIVE ? a.dtr[g] : a.dt;
+    int64_t sat = io_sat(a.io, a.sat_step, g), done = io_done(a.io, a.steps_done, g);
+    T dtr = ADAPTIVE ? io_dt<T>(a.io, a.dtr, g) : a.dt;
     const int w = l >> 6;
     auto vote = [&](bool u, int k) {
         const bool wu = __any(u);
@@ -890,6 +896,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
         a.sat_step[g] = sat;
         a.steps_done[g] = done;
         if (ADAPTIVE) a.dtr[g] = dtr;
+        io_mirror<T>(a.io, g, sat, done, dtr, ADAPTIVE);
     }
 }
 
