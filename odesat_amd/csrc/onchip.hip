@@ -245,6 +245,9 @@ typedef __attribute__((address_space(3))) uint32_t lu32;
 // target.)
 __device__ __forceinline__ void pair_signal(uint32_t cnt, uint32_t ep) {
     __builtin_amdgcn_sched_barrier(0);
+#if ONCHIP_SPLITBAR == 2  // (A/B: the wave's dv writes performed before its count is stored)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
     asm volatile("" ::: "memory");
     *reinterpret_cast<volatile lu32 *>(cnt + 4u * (threadIdx.x >> 6)) = ep;
     asm volatile("" ::: "memory");
