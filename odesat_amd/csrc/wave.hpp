@@ -642,6 +642,9 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
 // Bit-identical to k_solo, k_wave and the oracle (tests/test_gpu_parity.py, tests/test_gpu_fuzz.py).
 // ------------------------------------------------------------------------------------------------
 constexpr int SOLO_DPAD = 8;
+#ifndef SOLO_FOLD_EARLY
+#define SOLO_FOLD_EARLY 1
+#endif
 
 // LDS elements of k_solo_fast: v (rounded up to 16 bytes), the padded term blocks, the overflow area
 inline size_t solo_fast_elems(int64_t n, int64_t L, size_t tsize) {
@@ -803,10 +806,17 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
             SOLO_STAMP(0);
             __syncthreads();
             SOLO_STAMP(1);
+            // the fold's reads go out with the vote's (one LDS round trip, not two); an allsat
+            // replica discards them (SOLO_FOLD_EARLY=0: after the vote, A/B)
+#if SOLO_FOLD_EARLY
+            const Terms t = fold();
+#endif
             uns = votes(k);
             go = uns;  // an allsat replica takes no step (:122)
             if (go) {
+#if !SOLO_FOLD_EARLY
                 const Terms t = fold();
+#endif
 #pragma unroll
                 for (int c = 0; c < CPL; ++c)
                     if (l + c * NL < a.m) {  // the memories' full-step clone and first half step (:124-128)

@@ -20,4 +20,8 @@ val() { python -c 'import json,sys; d=json.loads([l for l in sys.stdin if l.star
 for i in 1 2; do for fold in 1 0; do
   echo "fold=$fold $(ODESAT_CALL_FOLD=$fold $B --steps 20 --warmup 5 2>/dev/null | val)" || exit 1
 done; done
+for i in 1 2; do for v in prod foldlate; do
+  L=""; [ $v = prod ] || L="ODESAT_LIB=$PWD/expt/lib$v.so"
+  echo "criterion $v $(env $L timeout -k 10 200 python -u scripts/bench_criterion.py --no-cpu 2>/dev/null | tr '\n' ' ')" || exit 1
+done; done
 echo done
