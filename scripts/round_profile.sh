@@ -42,6 +42,7 @@ prof res_f64 k_resident f64 fixed config2 profile_k_resident_f64.json 10 30 ALG=
 prof res_f64_ada k_resident f64 adaptive config2 profile_k_resident_f64_adaptive.json 5 15 ALG=2 DTYPE=f64 ADAPTIVE=1 || exit 1
 prof res k_resident f32 fixed config2 profile_k_resident.json 10 50 ALG=2 || exit 1
 prof wave_c3 k_wave f32 adaptive config3 profile_k_wave.json 20 100 ADAPTIVE=1 || exit 1
+prof step_c4 k_step f32 fixed config4 profile_k_step_config4.json 2 4 || exit 1  # one launch per step: per-dispatch means
 if want part; then  # config 5's partitioned step at world 1: per-kernel counter bytes per step
   pargs=()
   for mode in clauses variables; do
