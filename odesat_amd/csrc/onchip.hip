@@ -235,9 +235,17 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
 // Ordering: a wave's LDS operations are performed in issue order, so a counter increment is performed
 // after that wave's dv writes; a wave that has read the counter at its target issues its dv reads
 // after that read returned, i.e. after every wave's writes of the pair.
+// ONCHIP_SPLITBAR is a mask: 1 = the fixed-step kernel, 2 = the adaptive one.  Measured (round 4,
+// profiles/r04i_splitbar_ab.txt): adaptive 2.5-3.5 % faster, fixed 2-3 % slower -- the default is the
+// adaptive kernel only.
 #ifndef ONCHIP_SPLITBAR
-#define ONCHIP_SPLITBAR 0
+#define ONCHIP_SPLITBAR 2
 #endif
+#ifndef ONCHIP_POLL_SLEEP  // s_sleep between polls (0: none)
+#define ONCHIP_POLL_SLEEP 1
+#endif
+#define POLL_STR2(x) #x
+#define POLL_STR(x) POLL_STR2(x)
 typedef __attribute__((address_space(3))) uint32_t lu32;
 // (The counter is one word per wave -- the number of pairs it has signalled -- written by all of the
 // wave's lanes (one address: no lane branch, which would cost the unrolled tile code its registers);
@@ -245,9 +253,6 @@ typedef __attribute__((address_space(3))) uint32_t lu32;
 // target.)
 __device__ __forceinline__ void pair_signal(uint32_t cnt, uint32_t ep) {
     __builtin_amdgcn_sched_barrier(0);
-#if ONCHIP_SPLITBAR == 2  // (A/B: the wave's dv writes performed before its count is stored)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
     asm volatile("" ::: "memory");
     *reinterpret_cast<volatile lu32 *>(cnt + 4u * (threadIdx.x >> 6)) = ep;
     asm volatile("" ::: "memory");
@@ -273,7 +278,9 @@ __device__ __forceinline__ void pair_wait(uint32_t cnt, uint32_t target) {
         "s_add_u32 %2, %2, 1\n\t"
         "s_cmp_gt_u32 %2, 0x400000\n\t"
         "s_cbranch_scc1 L_pd%=\n\t"
-        "s_sleep 1\n\t"
+#if ONCHIP_POLL_SLEEP > 0
+        "s_sleep " POLL_STR(ONCHIP_POLL_SLEEP) "\n\t"
+#endif
         "s_branch L_pw%=\n"
         "L_pd%=:"
         : "=&v"(tmp), "=&s"(msk), "=&s"(it)
@@ -342,7 +349,7 @@ __device__ __forceinline__ void reg_tile(const Args &a, const Recs &R, float2 (&
                                          uint32_t cnt, uint32_t *ep) {
     constexpr bool bar = ((T + OFF) & 1) != 0;  // wave-paired tiles: a barrier after the second of a pair
     constexpr bool first = T > 0 && ((T - 1 + OFF) & 1) != 0;  // the first tile of a pair after another pair
-    constexpr bool SPL = ONCHIP_SPLITBAR != 0;
+    constexpr bool SPL = (ONCHIP_SPLITBAR & 1) != 0;
     if constexpr (T + 1 < TR) {
         tile_step<SPL>(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, cmax, S, bar, first, cnt, ep);
     } else {  // tile TR is the first LDS tile (if any)
@@ -393,7 +400,7 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
     back(a, F0, mr[0], h, hh, P, cmax);
     reg_tiles<TR, OFF>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, lane, cmax, S, cnt, &ep);
     // LDS tiles [TR, TR + tl): tl is a multiple of 4 (the host pads the tiling); they keep plain barriers
-    if (ONCHIP_SPLITBAR && a.tl > 0) __syncthreads();
+    if ((ONCHIP_SPLITBAR & 1) && a.tl > 0) __syncthreads();
     const int NT = TR + a.tl;
     const int last = a.tl - 1;
     for (int t0 = TR; t0 < NT; t0 += 4) {
@@ -409,7 +416,7 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
             if (lt <= last) *lds_f2(ma) = m;
         }
     }
-    if constexpr (OFF == 1 || ONCHIP_SPLITBAR) __syncthreads();  // the last tile (TR + tl - 1, odd) ends no pair
+    if constexpr (OFF == 1 || (ONCHIP_SPLITBAR & 1)) __syncthreads();  // the last tile (TR + tl - 1, odd) ends no pair
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -513,7 +520,7 @@ __device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &s
                                            FrontA &Fn, GathA &Gn, int t, float h, float hh, float hq, uint32_t sb,
                                            bool p2, uint32_t &cmax, float &e, bool bar, bool first, uint32_t cnt,
                                            uint32_t &ep) {
-    constexpr bool SPL = ONCHIP_SPLITBAR != 0;
+    constexpr bool SPL = (ONCHIP_SPLITBAR & 2) != 0;
     if (SPL && first) pair_wait(cnt, ep);  // (split barriers: see tile_step)
     const float o0 = lds_f(P.a0 + ADA_D), o1 = lds_f(P.a1 + ADA_D), o2 = lds_f(P.a2 + ADA_D);
     lds_st(P.a0 + ADA_D, o0 + P.d0);
@@ -758,7 +765,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     // the waves' pair counts (split barriers): after the unsat flags (adaptive: and the error words)
     const uint32_t CNT = UNS + 8u + (ADA ? 4u * WAVES : 0u);
     if (lane < 2) lds_st(UNS + 4u * lane, 0.0f);
-    if (ONCHIP_SPLITBAR && lane < WAVES) lds_st(CNT + 4u * lane, 0.0f);
+    if ((ONCHIP_SPLITBAR & (ADA ? 2 : 1)) && lane < WAVES) lds_st(CNT + 4u * lane, 0.0f);
     __syncthreads();
     ONCHIP_PHASE(1);
     uint32_t ep = 0u;  // the pairs every wave has signalled so far
