@@ -56,7 +56,7 @@ struct odesat_solver {
     void *vh = nullptr, *vf = nullptr, *ch = nullptr, *cf = nullptr;
     void *dtr = nullptr, *err = nullptr;
     void *tt[2] = {nullptr, nullptr};  // FUSED owner-TT: clause products xl xs [G][m][W], double-buffered (lazy)
-    bool fused_tt = true;              // ODESAT_FUSED_TT=0: every incidence reads the clause's memories (A/B)
+    bool fused_tt = false;             // ODESAT_FUSED_TT=1: FUSED owner-TT (measured 7 % slower on config 4: off)
     // per-call bookkeeping of the persistent kernels (callio.hpp): io_begin -- the next launch starts the
     // call (no k_begin_call); io_mirror -- launches store the results in the pinned host buffers
     bool io_begin = false, io_mirror = false;
