@@ -537,6 +537,51 @@ def test_onchip_lds_tiles_match_resident_and_oracle(stop, monkeypatch, pair_off)
     assert same(v[0], ov) and same(xs[0], oxs) and same(xl[0], oxl)
 
 
+@pytest.mark.parametrize("path", ["onchip", "wave", "resident", "solo"])
+def test_call_sequences_fold_and_mirror_match_fused(monkeypatch, path):
+    """Round 4 (callio.hpp): the persistent kernels reset a call's bookkeeping themselves (STOP_NONE /
+    STOP_EACH) and store STOP_NONE results straight into the pinned host buffers.  A sequence of calls
+    that mixes every kind -- fresh STOP_NONE (reset + mirror), continued STOP_EACH, fresh STOP_ANY
+    (k_begin_call), fresh adaptive STOP_EACH (reset, dt restarts at 0.01), a continued STOP_NONE (no
+    mirror) -- returns the same results and states as FUSED (which never folds), call by call, with
+    replicas freezing on easy.cnf."""
+    from odesat_amd import _lib
+    f = product_formula("easy")
+    env = {"onchip": ("0", "0", "0"), "wave": ("1", "0", "0"), "resident": ("0", "1", "0"),
+           "solo": ("1", "0", "1")}[path]
+    monkeypatch.setenv("ODESAT_WAVE", env[0])
+    monkeypatch.setenv("ODESAT_RES_NARROW", env[1])
+    monkeypatch.setenv("ODESAT_SOLO", env[2])
+    seq = [dict(stop=ODESAT_STOP_NONE, max_steps=40, resume=False),
+           dict(stop=ODESAT_STOP_EACH, max_steps=900, resume=True),
+           dict(stop=ODESAT_STOP_ANY, max_steps=900, resume=False),
+           dict(stop=ODESAT_STOP_EACH, max_steps=300, resume=False, adaptive=True),
+           dict(stop=ODESAT_STOP_NONE, max_steps=30, resume=True, adaptive=True)]
+    B = 3 if path == "solo" else 40
+    out = []
+    for alg in (None, _lib.ODESAT_ALG_FUSED):
+        runs = []
+        with Solver(f, B, "f32") as s:
+            s.set_algorithm(alg if alg is not None else
+                            (_lib.ODESAT_ALG_ONCHIP if path == "onchip" else _lib.ODESAT_ALG_RESIDENT))
+            kern = s.step_kernel(False)
+            s.init_state(4)
+            for kw in seq:
+                r = s.simulate(dt=0.1, tol=1e-3, poll_interval=64, **kw)
+                runs.append((r, s.get_state()))
+        out.append((kern, runs))
+    (k1, a), (k2, b) = out
+    assert k2 == "k_step" and k1 == {"onchip": "k_onchip", "wave": "k_wave", "resident": "k_resident",
+                                     "solo": "k_solo"}[path]
+    for (ra, sa), (rb, sb) in zip(a, b):
+        assert ra["steps_run"] == rb["steps_run"]
+        assert np.array_equal(ra["first_sat_step"], rb["first_sat_step"])
+        assert np.array_equal(ra["steps_done"], rb["steps_done"]) and same(ra["dt"], rb["dt"])
+        for x, y in zip(sa, sb):
+            assert same(x, y)
+    assert (a[1][0]["first_sat_step"] >= 0).any()  # replicas froze on the way
+
+
 @pytest.mark.parametrize("adaptive", [False, True])
 def test_onchip_long_launches_sat_and_freeze(monkeypatch, adaptive):
     """STOP_EACH over launches of many steps: replicas that satisfy easy.cnf freeze at their own
