@@ -413,10 +413,12 @@ __device__ __forceinline__ void stream_rows3(const KArgs<T> &a, const Bufs<T> &b
         }
 #pragma unroll
         for (int b = 0; b < RB; ++b) {
-            if (TT && (r[b].x & 3) != 0) {  // uniform (LW = 64: the wave walks one incidence at a time)
-                const Vec<T, VEC> tp = ldv<T, VEC>(bf.tcur + tbase + (size_t)(r[b].x >> 2) * W);
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) B.mem[b].e[k] = tp.e[k];
+            if constexpr (TT) {  // (VEC == 1) no branch: the owner's (xs, xl), the others' product twice
+                const size_t c = (size_t)(r[b].x >> 2);
+                const bool own0 = (r[b].x & 3) == 0;  // uniform (LW = 64: one incidence per wave)
+                const T *pa = own0 ? CM + cbase + c * W * 2 : bf.tcur + tbase + c * W;
+                B.mem[b].e[0] = __builtin_nontemporal_load(pa);
+                B.mem[b].e[1] = __builtin_nontemporal_load(own0 ? pa + 1 : pa);
             } else {
                 B.mem[b] = ldv_nt<T, 2 * VEC>(CM + cbase + (size_t)(r[b].x >> 2) * W * 2);
             }
@@ -446,12 +448,11 @@ __device__ __forceinline__ void stream_rows3(const KArgs<T> &a, const Bufs<T> &b
                 const T vio = own == 0 ? B.vv[b][0].e[k] : (own == 1 ? B.vv[b][1].e[k] : B.vv[b][2].e[k]);
                 const T val = one - qo * vio;
                 const T g_ = halfc * qo * (val != mn ? mn : sec);                    // :64-70
-                if (TT && own != 0) {  // the clause product from its owner; R is +-0 (see above)
-                    dv[k] += B.mem[b].e[k] * g_;                                      // :80
-                    continue;
-                }
                 const T xs_m = B.mem[b].e[2 * k], xl_m = B.mem[b].e[2 * k + 1];
-                const T t = xl_m * xs_m;
+                // owner-TT: the other incidences hold the owner's product in both words; their tr is
+                // then some finite number and r_ is +-0 on in-range states, so tr r_ is a signed zero,
+                // which the sum below and a dv that is never -0 absorb (see above)
+                const T t = (TT && own != 0) ? xs_m : xl_m * xs_m;
                 const T tr = (one + a.zeta * xl_m) * (one - xs_m);
                 const T r_ = (C[k] == one - qo * vio) ? halfc * (qo - vio) : (T)0.0;  // :73-77
                 dv[k] += t * g_ + tr * r_;                                            // :80
@@ -508,7 +509,7 @@ __device__ __forceinline__ void stream_rows3(const KArgs<T> &a, const Bufs<T> &b
 #endif
 template <typename T, int LW, int VEC, int MODE, int K, int RB = 4, bool TT = false>
 __global__ __launch_bounds__(256) KSTEP_ATTR void k_step(KArgs<T> a) {
-    static_assert(!TT || (LW == 64 && K == 3 && MODE == M_FIXED), "owner-TT: the 3-SAT incidence stream, fixed steps");
+    static_assert(!TT || (LW == 64 && VEC == 1 && K == 3 && MODE == M_FIXED), "owner-TT: the 3-SAT incidence stream, fixed steps");
     using G_ = Geo<LW, VEC>;
     constexpr int W = G_::W, IPR = G_::IPR;
     static_assert(K == 0 || K == 3, "incidence records are laid out for 3-SAT");

@@ -300,7 +300,7 @@ int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which, bool tt = false) {
     {
         Timed tm(s, which == K_VARIABLE ? 1 : 0);
         if (which == K_STEP) {
-            if constexpr (LW == 64 && MODE == M_FIXED) {
+            if constexpr (LW == 64 && VEC == 1 && MODE == M_FIXED) {
                 if (tt) {  // owner-TT (kernels.hpp stream_rows3): the caller checked the conditions
                     if (s->rb == 8)
                         hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 3, 8, true>), grid, block, 0, s->stream, a);

@@ -23,11 +23,21 @@ cp, v_, n_ = wl.formula_arrays(var, neg)
 f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
 with Solver(f, int(os.environ.get("B", "1024")), "f32") as s:
     s.init_state(42)
+    if os.environ.get("PROFILE_WARMUP") == "1":  # the warm-up call already profiled
+        s.profile(True)
     s.simulate(dt=0.01, max_steps=5, stop=ODESAT_STOP_NONE, poll_interval=5)
     walls, kerns = [], []
+    gap = float(os.environ.get("GAP_MS", "0")) / 1e3  # host idle (sleep) or busy (BUSY=1) time between calls
     for i in range(N):
         s.profile(True)
         s.synchronize()
+        if gap:
+            if os.environ.get("BUSY") == "1":
+                t_end = time.perf_counter() + gap
+                while time.perf_counter() < t_end:
+                    pass
+            else:
+                time.sleep(gap)
         t0 = time.perf_counter()
         s.simulate(dt=0.01, max_steps=K, stop=ODESAT_STOP_NONE, poll_interval=K)
         s.synchronize()
