@@ -187,6 +187,10 @@ def dist_setup(args):
             td.init_process_group(backend=backend, device_id=torch.device("cuda", local))
         else:
             td.init_process_group(backend=backend)
+        # the group's first collective sets up the communicator's device resources; run it here, so
+        # the first timed region's barrier is not the first (at world 1 over RCCL the first barrier
+        # left ~115 us on the next call: profiles/r04r_overhead_first_barrier.jsonl)
+        td.barrier()
         dist = td
     elif args.gpus != 1:
         raise SystemExit("bench.py: --gpus N > 1 needs N ranks (run without a launcher to spawn them)")
@@ -230,7 +234,8 @@ def time_gpu(solver, steps, warmup, dist, local, profile, stop, adaptive=False, 
     sync pairs.  steady > 0: afterwards, `steady` more calls of `steps` steps back to back on this rank
     (outside the timed region; see steady_state())."""
     from odesat_amd.system import ODESAT_STOP_NONE
-    kw = dict(adaptive=adaptive, dt=0.01, tol=1e-3, stop=stop)
+    # reuse=True: the solver's own result arrays, no host allocation in the call (Solver.simulate)
+    kw = dict(adaptive=adaptive, dt=0.01, tol=1e-3, stop=stop, reuse=True)
     if warmup:
         solver.simulate(max_steps=warmup, poll_interval=warmup, **kw)
     solver.profile(profile)

@@ -544,7 +544,8 @@ def test_call_sequences_fold_and_mirror_match_fused(monkeypatch, path):
     that mixes every kind -- fresh STOP_NONE (reset + mirror), continued STOP_EACH, fresh STOP_ANY
     (k_begin_call), fresh adaptive STOP_EACH (reset, dt restarts at 0.01), a continued STOP_NONE (no
     mirror) -- returns the same results and states as FUSED (which never folds), call by call, with
-    replicas freezing on easy.cnf."""
+    replicas freezing on easy.cnf.  The persistent path's calls take Solver.simulate's reuse=True
+    path (the solver's own result arrays and params, rebuilt per call field by field)."""
     from odesat_amd import _lib
     f = product_formula("easy")
     env = {"onchip": ("0", "0", "0"), "wave": ("1", "0", "0"), "resident": ("0", "1", "0"),
@@ -566,9 +567,13 @@ def test_call_sequences_fold_and_mirror_match_fused(monkeypatch, path):
                             (_lib.ODESAT_ALG_ONCHIP if path == "onchip" else _lib.ODESAT_ALG_RESIDENT))
             kern = s.step_kernel(False)
             s.init_state(4)
+            owned = None
             for kw in seq:
-                r = s.simulate(dt=0.1, tol=1e-3, poll_interval=64, **kw)
-                runs.append((r, s.get_state()))
+                r = s.simulate(dt=0.1, tol=1e-3, poll_interval=64, reuse=alg is None, **kw)
+                if alg is None:  # reuse: the same arrays every call
+                    assert owned is None or r["first_sat_step"] is owned
+                    owned = r["first_sat_step"]
+                runs.append(({k: np.copy(x) for k, x in r.items()}, s.get_state()))
         out.append((kern, runs))
     (k1, a), (k2, b) = out
     assert k2 == "k_step" and k1 == {"onchip": "k_onchip", "wave": "k_wave", "resident": "k_resident",
