@@ -645,6 +645,20 @@ constexpr int SOLO_DPAD = 8;
 #ifndef SOLO_FOLD_EARLY
 #define SOLO_FOLD_EARLY 1
 #endif
+// SOLO_DT_LATE=1: an adaptive step's dt update (an f64 divide and square root, system.rs:133-135)
+// runs in the next step's first clause pass, between its gathers and its arithmetic (select form, no
+// branch, so the two chains share a basic block), instead of after the closing barrier: nothing in
+// that pass reads dt.  The last step's update runs after the loop.
+#ifndef SOLO_DT_LATE
+#define SOLO_DT_LATE 1
+#endif
+// SOLO_ERR_LATE=1 (with SOLO_DT_LATE): the step's max_error reduction moves there too -- each lane
+// stores its own error term, and the next pass's `mid` reads the words of its lane slot in every wave
+// (zeros where a wave is absent), folds them and reduces across the wave, so no wave reduction and no
+// atomic sit before the closing barrier
+#ifndef SOLO_ERR_LATE
+#define SOLO_ERR_LATE 0
+#endif
 
 // LDS elements of k_solo_fast: v (rounded up to 16 bytes), the padded term blocks, the overflow area
 inline size_t solo_fast_elems(int64_t n, int64_t L, size_t tsize) {
@@ -662,6 +676,11 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
         TV t[VPL][SOLO_DPAD / PER16];
     };
     __shared__ U errM[2];  // per step parity: the max_error bits of the step (the waves' LDS atomic max)
+#if SOLO_ERR_LATE
+    constexpr int NW16 = SOLO_MAX_NL / 64;
+    __shared__ __attribute__((aligned(16))) U eL[64 * NW16];  // [lane slot][wave]: each lane's error bits
+    for (int i = (int)threadIdx.x; i < 64 * NW16; i += (int)blockDim.x) eL[i] = 0;
+#endif
     __shared__ __attribute__((aligned(16))) int voteW[2][SOLO_MAX_NL / 64];
     const int NL = (int)blockDim.x, l = (int)threadIdx.x;
     const int g = blockIdx.x;
@@ -732,13 +751,15 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
         for (int j = 0; j < SOLO_MAX_NL / 256; ++j) r |= r4[j].x | r4[j].y | r4[j].z | r4[j].w;
         return r != 0;
     };
-    // the clause pass: gathers of every slot first, then each slot's terms; mn into mn_o; unsat
-    auto clauses = [&](const T (&txs)[CPL], const T (&txl)[CPL], T (&mn_o)[CPL]) -> bool {
+    // the clause pass: gathers of every slot first, then `mid` (work that overlaps them), then each
+    // slot's terms; mn into mn_o; unsat
+    auto clauses = [&](const T (&txs)[CPL], const T (&txl)[CPL], T (&mn_o)[CPL], auto &&mid) -> bool {
         T vv[CPL][3];
 #pragma unroll
         for (int k = 0; k < CPL; ++k)
 #pragma unroll
             for (int j = 0; j < 3; ++j) vv[k][j] = vL[va[k][j]];
+        mid();
         bool uns = false;
 #pragma unroll
         for (int k = 0; k < CPL; ++k)
@@ -780,13 +801,37 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
     uint64_t st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = solo_memtime();
 #endif
+    auto nop = [] {};
+    // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3), err = the step's max_error (errM)
+#if SOLO_ERR_LATE
+    auto err_bits = [&](int) -> U {
+        constexpr int PER = 16 / (int)sizeof(U);
+        typedef U UV __attribute__((ext_vector_type(PER)));
+        const UV *p = reinterpret_cast<const UV *>(eL + (l & 63) * NW16);
+        UV r[NW16 / PER];
+#pragma unroll
+        for (int q = 0; q < NW16 / PER; ++q) r[q] = p[q];
+        U m = 0;
+#pragma unroll
+        for (int q = 0; q < NW16 / PER; ++q)
+#pragma unroll
+            for (int u = 0; u < PER; ++u) m = max(m, (U)r[q][u]);
+        return wave_max_bits(m);
+    };
+#else
+    auto err_bits = [&](int k) -> U { return errM[k & 1]; };
+#endif
+    auto dt_next = [&](int k) { return dmax(dmin(dtr * dsqrt((T)a.tol / frombits(err_bits(k))), (T)1e3), (T)0.0078125); };
+    bool pend = false;  // SOLO_DT_LATE: the previous step was taken and its dt update is still due
+    int klast = 0;
     for (int k = 0; k < a.nsteps; ++k) {
         const int step = a.step0 + k;
-        const T h = dtr, hh = (T)0.5 * h, hq = (T)0.25 * h;
+        klast = k;
+        T h = dtr, hh = (T)0.5 * h, hq = (T)0.25 * h;
         T e = (T)0.0;
         bool uns, go = false;
         if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
-            vote(clauses(xs, xl, mk), k);
+            vote(clauses(xs, xl, mk, nop), k);
             __syncthreads();  // the terms (and the votes) before the fold
             const Terms t = fold();
 #pragma unroll
@@ -802,7 +847,20 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
                     vL[l + j * NL] = vr[j];
                 }
         } else {  // euler_step (:111-139)
-            vote(clauses(xs, xl, mk), k);  // the RHS at y, y's memories
+#if SOLO_DT_LATE
+            // the previous step's dt update under this pass's gathers (errM[k - 1] is final: the
+            // previous step's closing barrier ordered every wave's atomic max)
+            auto late = [&] {
+                const T nd = dt_next(k - 1);
+                dtr = pend ? nd : dtr;
+            };
+            vote(clauses(xs, xl, mk, late), k);  // the RHS at y, y's memories
+            h = dtr;
+            hh = (T)0.5 * h;
+            hq = (T)0.25 * h;
+#else
+            vote(clauses(xs, xl, mk, nop), k);  // the RHS at y, y's memories
+#endif
             SOLO_STAMP(0);
             __syncthreads();
             SOLO_STAMP(1);
@@ -837,7 +895,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
             SOLO_STAMP(2);
             __syncthreads();  // the half step's voltages before the second pass; the terms read
             SOLO_STAMP(3);
-            if (go) clauses(xsh, xlh, mn2);
+            if (go) clauses(xsh, xlh, mn2, nop);
             SOLO_STAMP(4);
             __syncthreads();  // the second pass's terms before its fold
             SOLO_STAMP(5);
@@ -862,9 +920,13 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
                         vr[j] = vn;
                         vL[l + j * NL] = vn;
                     }
+#if SOLO_ERR_LATE
+                eL[(l & 63) * NW16 + (l >> 6)] = tobits(e);  // non-negative floats order as their bits
+#else
                 // (an LDS atomic max from every lane instead: 38 ms per criterion call against 12.6)
                 const U eb = wave_max_bits(tobits(e));  // non-negative floats order as their bits
                 if ((l & 63) == 0) atomicMax(&errM[k & 1], eb);
+#endif
             }
             if (l == 0) errM[(k + 1) & 1] = 0;  // read at the start of step k, before this step's first barrier
         }
@@ -876,12 +938,15 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
         }
         if (ADAPTIVE) SOLO_STAMP(6);
         __syncthreads();  // the voltages before the next step's gathers (and the error words)
-        if (ADAPTIVE && go) {  // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3)
-            dtr = dmax(dmin(dtr * dsqrt((T)a.tol / frombits(errM[k & 1])), (T)1e3), (T)0.0078125);
-        }
+#if SOLO_DT_LATE
+        pend = go;
+#else
+        if (ADAPTIVE && go) dtr = dt_next(k);
+#endif
         if (ADAPTIVE) SOLO_STAMP(7);
         if (!act) break;  // uniform
     }
+    if (ADAPTIVE && SOLO_DT_LATE && pend) dtr = dt_next(klast);  // the last step's update
 #ifdef SOLO_STAMPS
     if ((l & 63) == 0 && g == 0)
         for (int i = 0; i < 8; ++i) g_solo_stamps[(l >> 6) * 8 + i] = st_[i];
