@@ -652,13 +652,6 @@ constexpr int SOLO_DPAD = 8;
 #ifndef SOLO_DT_LATE
 #define SOLO_DT_LATE 1
 #endif
-// SOLO_ERR_LATE=1 (with SOLO_DT_LATE): the step's max_error reduction moves there too -- each lane
-// stores its own error term, and the next pass's `mid` reads the words of its lane slot in every wave
-// (zeros where a wave is absent), folds them and reduces across the wave, so no wave reduction and no
-// atomic sit before the closing barrier
-#ifndef SOLO_ERR_LATE
-#define SOLO_ERR_LATE 0
-#endif
 
 // LDS elements of k_solo_fast: v (rounded up to 16 bytes), the padded term blocks, the overflow area
 inline size_t solo_fast_elems(int64_t n, int64_t L, size_t tsize) {
@@ -676,11 +669,6 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
         TV t[VPL][SOLO_DPAD / PER16];
     };
     __shared__ U errM[2];  // per step parity: the max_error bits of the step (the waves' LDS atomic max)
-#if SOLO_ERR_LATE
-    constexpr int NW16 = SOLO_MAX_NL / 64;
-    __shared__ __attribute__((aligned(16))) U eL[64 * NW16];  // [lane slot][wave]: each lane's error bits
-    for (int i = (int)threadIdx.x; i < 64 * NW16; i += (int)blockDim.x) eL[i] = 0;
-#endif
     __shared__ __attribute__((aligned(16))) int voteW[2][SOLO_MAX_NL / 64];
     const int NL = (int)blockDim.x, l = (int)threadIdx.x;
     const int g = blockIdx.x;
@@ -803,25 +791,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
 #endif
     auto nop = [] {};
     // :133-135 dt <- clamp(dt * sqrt(tol / err), 2^-7, 1e3), err = the step's max_error (errM)
-#if SOLO_ERR_LATE
-    auto err_bits = [&](int) -> U {
-        constexpr int PER = 16 / (int)sizeof(U);
-        typedef U UV __attribute__((ext_vector_type(PER)));
-        const UV *p = reinterpret_cast<const UV *>(eL + (l & 63) * NW16);
-        UV r[NW16 / PER];
-#pragma unroll
-        for (int q = 0; q < NW16 / PER; ++q) r[q] = p[q];
-        U m = 0;
-#pragma unroll
-        for (int q = 0; q < NW16 / PER; ++q)
-#pragma unroll
-            for (int u = 0; u < PER; ++u) m = max(m, (U)r[q][u]);
-        return wave_max_bits(m);
-    };
-#else
-    auto err_bits = [&](int k) -> U { return errM[k & 1]; };
-#endif
-    auto dt_next = [&](int k) { return dmax(dmin(dtr * dsqrt((T)a.tol / frombits(err_bits(k))), (T)1e3), (T)0.0078125); };
+    auto dt_next = [&](int k) { return dmax(dmin(dtr * dsqrt((T)a.tol / frombits(errM[k & 1])), (T)1e3), (T)0.0078125); };
     bool pend = false;  // SOLO_DT_LATE: the previous step was taken and its dt update is still due
     int klast = 0;
     for (int k = 0; k < a.nsteps; ++k) {
@@ -920,13 +890,9 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
                         vr[j] = vn;
                         vL[l + j * NL] = vn;
                     }
-#if SOLO_ERR_LATE
-                eL[(l & 63) * NW16 + (l >> 6)] = tobits(e);  // non-negative floats order as their bits
-#else
                 // (an LDS atomic max from every lane instead: 38 ms per criterion call against 12.6)
                 const U eb = wave_max_bits(tobits(e));  // non-negative floats order as their bits
                 if ((l & 63) == 0) atomicMax(&errM[k & 1], eb);
-#endif
             }
             if (l == 0) errM[(k + 1) & 1] = 0;  // read at the start of step k, before this step's first barrier
         }
