@@ -78,6 +78,7 @@ struct odesat_solver {
     bool solo_fast = true;      // k_solo's short arithmetic on in-range states (ODESAT_SOLO_FAST=0: the general form)
     bool wave_fast = true;      // k_wave's likewise (ODESAT_WAVE_FAST=0)
     bool res_fast = true;       // k_resident's likewise, 3-SAT only (ODESAT_RES_FAST=0)
+    bool res_rc = true;         // f64 fixed steps: register-cached tiles (resident.hpp; ODESAT_RES_RC=0)
     int wv_tw = 1;              // k_wave: waves per replica, fixed steps
     int wv_tw_ada = 1;          // ... adaptive steps (four barriers per step instead of two: at most 4)
     bool res_ada = false; // adaptive steps run k_resident (else FUSED on the same layout)
@@ -802,14 +803,15 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
     return ODESAT_OK;
 }
 
-template <typename T, int R, bool ADA, bool K3, int NTHR = ResShape<R>::NTH, bool VFG = false, bool FAST = false>
+template <typename T, int R, bool ADA, bool K3, int NTHR = ResShape<R>::NTH, bool VFG = false, bool FAST = false,
+          int RC = 0>
 int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     const size_t lds = res_lds_bytes(s->n, R, sizeof(T), ADA && !VFG);
-    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR, VFG, FAST>),
+    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR, VFG, FAST, RC>),
                                    (int)RES_LDS_MAX));
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR, VFG, FAST>), dim3(s->G), dim3(NTHR), lds, s->stream, a);
+        hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR, VFG, FAST, RC>), dim3(s->G), dim3(NTHR), lds, s->stream, a);
     }
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
@@ -917,6 +919,9 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     }
 }
 
+#ifndef RES_RC
+#define RES_RC 28  // register-cached tiles of the f64 fixed-step k_resident (4 VGPRs each)
+#endif
 template <typename T>
 int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
                     int stop_mode, bool oop, bool fast) {
@@ -979,6 +984,11 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
             return f3   ? launch_resident_k<T, R, true, true, NT, false, true>(s, a)
                    : k3 ? launch_resident_k<T, R, true, true>(s, a)
                         : launch_resident_k<T, R, true, false>(s, a);
+        if constexpr (std::is_same<T, double>::value && R == 1) {
+            // f64 fixed steps: the first RES_RC tiles' memories in VGPRs for the launch (resident.hpp)
+            if (f3 && s->res_rc && s->res_ntiles >= RES_RC + 16)
+                return launch_resident_k<T, 1, false, true, NT, false, true, RES_RC>(s, a);
+        }
         return f3   ? launch_resident_k<T, R, false, true, NT, false, true>(s, a)
                : k3 ? launch_resident_k<T, R, false, true>(s, a)
                     : launch_resident_k<T, R, false, false>(s, a);
@@ -1474,6 +1484,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         s->res_R = res_r;
         s->res_ada = res_fits(n, res_r, s->tsize, true);
         if (const char *ev = std::getenv("ODESAT_RES_FAST")) s->res_fast = std::atoi(ev) != 0;
+        if (const char *ev = std::getenv("ODESAT_RES_RC")) s->res_rc = std::atoi(ev) != 0;
         // adaptive steps whose clone of v does not fit beside v and dv (f64 at n > 6.7 k, the CLI's
         // default precision and mode on config 2): k_resident with the clone in HBM instead of FUSED
         // on the one-replica layout.  ODESAT_RES_VFG=0 keeps FUSED.

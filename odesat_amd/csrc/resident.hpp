@@ -38,6 +38,9 @@ constexpr int RES_DEPTH = RES_DEPTH_F32;  // tiles in flight per lane (3-SAT reg
 #define RES_DEPTH_F64 8
 #endif
 template <typename T> constexpr int res_depth() { return sizeof(T) == 8 ? RES_DEPTH_F64 : RES_DEPTH; }
+#ifndef RES_RC_DEPTH
+#define RES_RC_DEPTH 4
+#endif
 
 template <typename T> struct RArgs {
     const int4 *__restrict__ cl4;      // [m] 3-SAT: the clause's literals (var << 1 | neg), internal order
@@ -119,7 +122,7 @@ template <typename T> __device__ __forceinline__ void res_stm(T *p, const Vec<T,
 // ring's loads stay in flight across iterations (no control flow for the wait counters to merge).
 template <typename T, int R, int PK>
 __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CM, int t,
-                                          TileLoad<T> &ld) {
+                                          TileLoad<T> &ld, bool mem = true) {
     const int tt = min(t, a.ntiles - 1);
     const int c0 = ldc(a.tc, tt), c1 = ldc(a.tc, tt + 1);
     const int c = c0 + x.lc;
@@ -129,7 +132,7 @@ __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> 
     // ring's back-edge but measured 4% slower)
     ld.lit = *at(a.cl4, (uint32_t)cc);
     const uint32_t ci = (uint32_t)(cc * R + x.r) * 2u;  // 32-bit offsets from the group's base
-    ld.mem = res_ldm<T>(at(CM, ci));  // (adaptive: y's memories, untouched until the second pass stores)
+    if (mem) ld.mem = res_ldm<T>(at(CM, ci));  // (adaptive: y's memories, untouched until the second pass stores)
     if (PK == P_ADA2) ld.full.e[0] = *at((const T *)x.cf, ci / 2u);  // the first pass's C
 }
 
@@ -329,16 +332,68 @@ __device__ __forceinline__ void res_clause_any(const RArgs<T> &a, const ResCtx<T
     e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, ci, C, mem, full, on, h, CMr != CM));
 }
 
+// Register-cached tiles (RC > 0; f64 fixed steps on in-range 3-SAT states, R = 1): the memories of
+// the first RC tiles stay in the lane's VGPRs for the whole launch -- read from HBM once at its start
+// and written once at its end -- and only the remaining tiles stream through HBM every step, as
+// k_onchip keeps every tile (f32) in VGPRs.  A fixed step of a register tile: res_clause3's FAST
+// P_FIXED forms with the memories in and out of `rmt`.
+template <typename T, int R>
+__device__ __forceinline__ void res_clause3_reg(const RArgs<T> &a, const ResCtx<T, R> &x, const TileLoad<T> &ld,
+                                                Pend<T> &P, bool on, T h, bool &uns, Vec<T, 2> &rmt) {
+    // branch-free: an empty slot (!ld.ok: its literals are a valid clause's) computes too, but its
+    // terms are never applied, its vote is masked and its memories are never stored
+    P.ok = ld.ok;
+    const int lit[3] = {ld.lit.x, ld.lit.y, ld.lit.z};
+    T v[3];
+    uint32_t sg[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        P.idx[j] = (lit[j] >> 1) * R + x.r;
+        sg[j] = (uint32_t)lit[j] << 31;
+        v[j] = x.vL[P.idx[j]];
+    }
+    const T xs = rmt.e[0], xl = rmt.e[1];
+    const T mn = solo_terms<T>(v, sg, xl * xs, P.d);
+    uns = uns || (on && ld.ok && !(mn < (T)0.5));  // :88
+    T xs_n, xl_n;
+    solo_mem<T>(xs, xl, mn, (T)0.5 * h, h, a.xl_max, xs_n, xl_n);
+    rmt.e[0] = on ? xs_n : xs;
+    rmt.e[1] = on ? xl_n : xl;
+}
+
+// Iteration TT of the pipeline below with a static tile index: tile TT+1's clause from the registers
+// (TT+1 < RC) or from its slot, tile TT's terms applied, the slot refilled with tile TT+1+D (its
+// memories only if that tile streams).
+template <typename T, int R, bool FAST, int RC, int D, int TT>
+__device__ __forceinline__ void res_iter3_rc(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM,
+                                             TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h, bool &uns, T &e,
+                                             Vec<T, 2> (&rm)[RC]) {
+    Pend<T> Q;
+    TileLoad<T> &S = b[(TT + 1) % D];
+    if constexpr (TT + 1 < RC) res_clause3_reg<T, R>(a, x, S, Q, on, h, uns, rm[TT + 1]);
+    else res_clause3<T, R, P_FIXED, FAST>(a, x, CM, TT + 1, S, Q, on, h, uns, e, CMr != CM);
+    res_apply3<T, R>(x, P);
+    res_load3<T, R, P_FIXED>(a, x, CMr, TT + 1 + D, S, TT + 1 + D >= RC);
+    __syncthreads();
+    P = Q;
+}
+template <typename T, int R, bool FAST, int RC, int D, int... Ts>
+__device__ __forceinline__ void res_prefix(std::integer_sequence<int, Ts...>, const RArgs<T> &a, const ResCtx<T, R> &x,
+                                           const T *CMr, T *CM, TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h,
+                                           bool &uns, T &e, Vec<T, 2> (&rm)[RC]) {
+    (res_iter3_rc<T, R, FAST, RC, D, Ts>(a, x, CMr, CM, b, P, on, h, uns, e, rm), ...);
+}
+
 // One step of the 3-SAT tile pipeline: the terms of tile t+1 are computed from slot S (which is
 // then refilled with tile t+1+RES_DEPTH), tile t's terms P are applied to dv, barrier (tile t+1
 // may touch the same dv entries).
-template <typename T, int R, int PK, bool FAST = false>
+template <typename T, int R, int PK, bool FAST = false, int D = res_depth<T>()>
 __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, int t,
                                           TileLoad<T> &S, Pend<T> &P, bool on, T h, bool &uns, T &e) {
     Pend<T> Q;
     res_clause3<T, R, PK, FAST>(a, x, CM, t + 1, S, Q, on, h, uns, e, CMr != CM);  // Q.ok = false past the last tile
     res_apply3<T, R>(x, P);
-    res_load3<T, R, PK>(a, x, CMr, t + 1 + res_depth<T>(), S);
+    res_load3<T, R, PK>(a, x, CMr, t + 1 + D, S);
 #ifdef RES_TIMING_PAIRS  // timing-only diagnostic build (results race): a barrier after odd tiles only
     if (t & 1)
 #endif
@@ -348,13 +403,16 @@ __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> 
 
 // One RHS pass over all tiles: dv (LDS) accumulates; memories are read from CMr (or the adaptive
 // scratch) and written by kind (P_FIXED: to CM).  Ends with a barrier (dv complete).
-template <typename T, int R, int PK, bool K3, bool FAST = false>
+template <typename T, int R, int PK, bool K3, bool FAST = false, int RC = 0>
 __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, bool on, T h,
-                                         bool &uns, T &e) {
+                                         bool &uns, T &e, Vec<T, 2> (&rm)[RC > 0 ? RC : 1]) {
     const int NT_ = a.ntiles;
     if constexpr (K3) {
-        constexpr int D = res_depth<T>();
+        // (register tiles: a ring of RES_RC_DEPTH, whose VGPRs the register tiles need more)
+        constexpr int D = RC > 0 ? RES_RC_DEPTH : res_depth<T>();
         static_assert(D == 4 || D == 8, "the pipeline below is unrolled for 4 or 8 slots");
+        static_assert(RC == 0 || (PK == P_FIXED && FAST && RC % D == 0 && RC >= D),
+                      "register tiles: fixed short-form steps, whole ring blocks (the host needs ntiles > RC + D)");
         // the host pads 3-SAT tilings to a multiple of 4 tiles (empty tiles), so the unrolled loop
         // below runs whole (D = 8: blocks of 8, then at most one static block of 4)
         if (NT_ == 0) {
@@ -364,18 +422,25 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
         TileLoad<T> b[D];
         Pend<T> P;
 #pragma unroll
-        for (int i = 0; i < D; ++i) res_load3<T, R, PK>(a, x, CMr, i, b[i]);
-        res_clause3<T, R, PK, FAST>(a, x, CM, 0, b[0], P, on, h, uns, e, CMr != CM);
-        res_load3<T, R, PK>(a, x, CMr, D, b[0]);
+        for (int i = 0; i < D; ++i) res_load3<T, R, PK>(a, x, CMr, i, b[i], i >= RC);
         int t0 = 0;
+        if constexpr (RC > 0) {
+            res_clause3_reg<T, R>(a, x, b[0], P, on, h, uns, rm[0]);
+            res_load3<T, R, PK>(a, x, CMr, D, b[0], D >= RC);
+            res_prefix<T, R, FAST, RC, D>(std::make_integer_sequence<int, RC>{}, a, x, CMr, CM, b, P, on, h, uns, e, rm);
+            t0 = RC;
+        } else {
+            res_clause3<T, R, PK, FAST>(a, x, CM, 0, b[0], P, on, h, uns, e, CMr != CM);
+            res_load3<T, R, PK>(a, x, CMr, D, b[0]);
+        }
         for (; t0 + D <= NT_; t0 += D) {  // iteration t computes tile t+1 from slot (t+1) % D
 #pragma unroll
-            for (int i = 0; i < D; ++i) res_iter3<T, R, PK, FAST>(a, x, CMr, CM, t0 + i, b[(i + 1) % D], P, on, h, uns, e);
+            for (int i = 0; i < D; ++i) res_iter3<T, R, PK, FAST, D>(a, x, CMr, CM, t0 + i, b[(i + 1) % D], P, on, h, uns, e);
         }
         if constexpr (D == 8) {
             if (t0 < NT_) {  // four tiles left: slots 1 .. 4
 #pragma unroll
-                for (int i = 0; i < 4; ++i) res_iter3<T, R, PK, FAST>(a, x, CMr, CM, t0 + i, b[i + 1], P, on, h, uns, e);
+                for (int i = 0; i < 4; ++i) res_iter3<T, R, PK, FAST, D>(a, x, CMr, CM, t0 + i, b[i + 1], P, on, h, uns, e);
             }
         }
     } else {
@@ -414,9 +479,10 @@ __device__ unsigned long long g_res_clk[4096 * 64];
 #else
 #define RES_STAMP(i) do {} while (0)
 #endif
-template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR, bool VFG = false, bool FAST = false>
+template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR, bool VFG = false, bool FAST = false, int RC = 0>
 __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     static_assert(!FAST || K3, "the short forms are 3-SAT only (res_clause_any has none)");
+    static_assert(RC == 0 || (!ADAPTIVE && FAST && R == 1), "register tiles: fixed short-form steps, R = 1");
     extern __shared__ __attribute__((aligned(16))) unsigned char res_smem[];
     using U = typename Bits<T>::U;
     constexpr int NTH = NTHR, NL = NTHR / R;
@@ -465,6 +531,18 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
 #pragma unroll
     for (int j = 0; j < R; ++j) any = any || actL[j] != 0;
     if (skipL || !any) return;  // uniform
+    // the register tiles' memories (RC > 0): read once here, written once after the last step
+    Vec<T, 2> rm[RC > 0 ? RC : 1];
+    auto rm_slot = [&](int t, bool &ok) {  // tile t's slot of this lane (a valid clause when empty)
+        const int c0 = ldc(a.tc, t), c = c0 + x.lc;
+        ok = c < ldc(a.tc, t + 1);
+        return (uint32_t)((ok ? c : c0) * R + x.r) * 2u;
+    };
+#pragma unroll
+    for (int t = 0; t < RC; ++t) {
+        bool ok;
+        rm[t] = res_ldm<T>(at((const T *)CM, rm_slot(t, ok)));
+    }
     copy_to_lds<8>(x.vL, V, tid, (int)nR, NTH);
     for (size_t i = tid; i < nR; i += NTH) x.dvL[i] = (T)0.0;  // :33
     __syncthreads();
@@ -475,8 +553,8 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
         const T h = dtL[x.r];
         bool uns = false;
         T e = (T)0.0;
-        if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154)
-            res_pass<T, R, P_FIXED, K3, FAST>(a, x, CMr, CMo, on, h, uns, e);
+        if constexpr (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154)
+            res_pass<T, R, P_FIXED, K3, FAST, RC>(a, x, CMr, CMo, on, h, uns, e, rm);
             CMr = CMo;
             if (uns) unsL[x.r] = 1u;
             const T hv = FAST ? (T)0.5 * h : h;
@@ -496,7 +574,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
                 }
             }
         } else {  // euler_step (system.rs:111-139), per-replica dt
-            res_pass<T, R, P_ADA1, K3, FAST>(a, x, CM, CM, on, h, uns, e);
+            res_pass<T, R, P_ADA1, K3, FAST>(a, x, CM, CM, on, h, uns, e, rm);
             if (uns) unsL[x.r] = 1u;
             __syncthreads();
             const bool st = on && unsL[x.r] != 0u;  // allsat replicas take no step (:122)
@@ -517,7 +595,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
             for (int j = 0; j < R; ++j) any_st = any_st || (actL[j] != 0 && unsL[j] != 0u);
             if (any_st) {  // uniform
                 bool u2 = false;
-                res_pass<T, R, P_ADA2, K3, FAST>(a, x, CM, CM, st, h, u2, e);
+                res_pass<T, R, P_ADA2, K3, FAST>(a, x, CM, CM, st, h, u2, e, rm);
                 for (int i = x.lc; i < a.n; i += NL) {
                     const int idx = i * R + x.r;
                     const T d = x.dvL[idx];
@@ -561,6 +639,12 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
         for (size_t i = tid; i < (size_t)a.m * R * 2; i += NTH) CMo[i] = CM[i];
     }
     for (size_t i = tid; i < nR; i += NTH) Vo[i] = x.vL[i];
+#pragma unroll
+    for (int t = 0; t < RC; ++t) {
+        bool ok;
+        const uint32_t ci = rm_slot(t, ok);
+        if (ok) res_stm<T>(at(CMo, ci), rm[t]);
+    }
     if (oop && tid == 0) a.par[g] = (uint8_t)!p;
     if (tid < R) {
         const int rg = g * R + tid;

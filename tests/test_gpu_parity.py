@@ -645,6 +645,39 @@ def test_onchip_adaptive_matches_resident_and_oracle(stop, monkeypatch):
     assert same(s1[0][0], ov) and same(s1[1][0], oxs) and same(s1[2][0], oxl)
 
 
+@pytest.mark.parametrize("stop", ["each", "any", "none"])
+def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, monkeypatch):
+    """f64 fixed steps keep the first RES_RC tiles' memories in VGPRs for a launch (resident.hpp,
+    round 4): == every tile streamed (ODESAT_RES_RC=0) bit for bit on every stop policy -- STOP_ANY
+    launches write out of place and replay -- over a fresh call and a continued one, and replica 0 ==
+    the oracle's f64 fixed steps (system.rs:141-154).  The instance's tiling is deep enough (85 tiles,
+    tests/test_tiling.py's hook) for the register prefix (the host needs RES_RC + 16)."""
+    from odesat_amd import _lib
+    f, (cp, v_, n_) = _instance(3000, 12600, 5)
+    pol = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[stop]
+    B = 6
+    out = []
+    for rc in ("1", "0"):
+        monkeypatch.setenv("ODESAT_RES_RC", rc)
+        with Solver(f, B, "f64") as s:
+            assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.step_kernel(False) == "k_resident"
+            s.init_state(9)
+            r1 = s.simulate(dt=0.05, zeta=0.001, max_steps=13, stop=pol, poll_interval=13)
+            r2 = s.simulate(dt=0.05, zeta=0.001, max_steps=9, stop=pol, poll_interval=4, resume=True)
+            out.append((r1, r2, s.get_state()))
+    (a1, a2, sa), (b1, b2, sb) = out
+    for x, y in ((a1, b1), (a2, b2)):
+        assert x["steps_run"] == y["steps_run"]
+        assert np.array_equal(x["first_sat_step"], y["first_sat_step"]) and np.array_equal(x["steps_done"], y["steps_done"])
+    for x, y in zip(sa, sb):
+        assert same(x, y)
+    o = Oracle(cp, v_, n_, 3000, "f64")
+    ov = init_voltages(9, 0, 1, 3000)[0]
+    oxs, oxl = o.init_short_term_memory(), np.ones(12600)
+    o.simulate(ov, oxs, oxl, dt=0.05, steps=int(a2["steps_done"][0]), zeta=0.001)
+    assert same(sa[0][0], ov) and same(sa[1][0], oxs) and same(sa[2][0], oxl)
+
+
 @pytest.mark.parametrize("prec", ["f32", "f64"])
 @pytest.mark.parametrize("stop", ["each", "any", "none"])
 def test_fused_owner_tt_matches_general_and_oracle(stop, prec, monkeypatch):
