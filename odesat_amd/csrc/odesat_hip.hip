@@ -922,6 +922,9 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
 #ifndef RES_RC
 #define RES_RC 28  // register-cached tiles of the f64 fixed-step k_resident (4 VGPRs each)
 #endif
+#ifndef RES_RC_ADA
+#define RES_RC_ADA 12  // the same for the f64 adaptive k_resident (VFG; + the first pass's mn)
+#endif
 template <typename T>
 int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
                     int stop_mode, bool oop, bool fast) {
@@ -965,6 +968,11 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
             return f3   ? launch_resident_k<T, 1, true, true, RES_NARROW, true, true>(s, a)
                    : k3 ? launch_resident_k<T, 1, true, true, RES_NARROW, true>(s, a)
                         : launch_resident_k<T, 1, true, false, RES_NARROW, true>(s, a);
+        if constexpr (std::is_same<T, double>::value) {
+            // the first RES_RC_ADA tiles' memories and first-pass mn in VGPRs for the launch (resident.hpp)
+            if (f3 && s->res_rc && s->res_ntiles >= RES_RC_ADA + 16)
+                return launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA>(s, a);
+        }
         return f3   ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true>(s, a)
                : k3 ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true>(s, a)
                     : launch_resident_k<T, 1, true, false, ResShape<1>::NTH, true>(s, a);

@@ -133,7 +133,7 @@ __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> 
     ld.lit = *at(a.cl4, (uint32_t)cc);
     const uint32_t ci = (uint32_t)(cc * R + x.r) * 2u;  // 32-bit offsets from the group's base
     if (mem) ld.mem = res_ldm<T>(at(CM, ci));  // (adaptive: y's memories, untouched until the second pass stores)
-    if (PK == P_ADA2) ld.full.e[0] = *at((const T *)x.cf, ci / 2u);  // the first pass's C
+    if (PK == P_ADA2 && mem) ld.full.e[0] = *at((const T *)x.cf, ci / 2u);  // the first pass's C
 }
 
 // The adaptive step's candidates for one clause's memories from y's memories and the first pass's
@@ -332,16 +332,17 @@ __device__ __forceinline__ void res_clause_any(const RArgs<T> &a, const ResCtx<T
     e = dmax(e, res_mem_update<T, R, PK>(a, x, CM, ci, C, mem, full, on, h, CMr != CM));
 }
 
-// Register-cached tiles (RC > 0; f64 fixed steps on in-range 3-SAT states, R = 1): the memories of
-// the first RC tiles stay in the lane's VGPRs for the whole launch -- read from HBM once at its start
-// and written once at its end -- and only the remaining tiles stream through HBM every step, as
-// k_onchip keeps every tile (f32) in VGPRs.  A fixed step of a register tile: res_clause3's FAST
-// P_FIXED forms with the memories in and out of `rmt`.
-template <typename T, int R>
+// Register-cached tiles (RC > 0; f64 on in-range 3-SAT states, R = 1): the memories of the first RC
+// tiles stay in the lane's VGPRs for the whole launch -- read from HBM once at its start and written
+// once at its end -- and only the remaining tiles stream through HBM every step, as k_onchip keeps
+// every tile (f32) in VGPRs.  Adaptive launches also keep each register tile's first-pass mn there
+// (`rmn`, instead of the C scratch).  A register tile's clause: res_clause3's FAST forms with the
+// memories in and out of `rmt`, branch-free -- an empty slot (!ld.ok: its literals are a valid
+// clause's) computes too, but its terms are never applied, its vote and error are masked and its
+// memories are never stored.
+template <typename T, int R, int PK>
 __device__ __forceinline__ void res_clause3_reg(const RArgs<T> &a, const ResCtx<T, R> &x, const TileLoad<T> &ld,
-                                                Pend<T> &P, bool on, T h, bool &uns, Vec<T, 2> &rmt) {
-    // branch-free: an empty slot (!ld.ok: its literals are a valid clause's) computes too, but its
-    // terms are never applied, its vote is masked and its memories are never stored
+                                                Pend<T> &P, bool on, T h, bool &uns, T &e, Vec<T, 2> &rmt, T &rmn) {
     P.ok = ld.ok;
     const int lit[3] = {ld.lit.x, ld.lit.y, ld.lit.z};
     T v[3];
@@ -352,36 +353,52 @@ __device__ __forceinline__ void res_clause3_reg(const RArgs<T> &a, const ResCtx<
         sg[j] = (uint32_t)lit[j] << 31;
         v[j] = x.vL[P.idx[j]];
     }
-    const T xs = rmt.e[0], xl = rmt.e[1];
+    const T hh = (T)0.5 * h, hq = (T)0.25 * h;
+    T xs = rmt.e[0], xl = rmt.e[1], xs_f = xs, xl_f = xl;
+    if constexpr (PK == P_ADA2) {  // y's memories -> the full-step clone and the first half step (:124-128)
+        solo_mem<T>(rmt.e[0], rmt.e[1], rmn, hh, h, a.xl_max, xs_f, xl_f);
+        solo_mem<T>(rmt.e[0], rmt.e[1], rmn, hq, hh, a.xl_max, xs, xl);
+    }
     const T mn = solo_terms<T>(v, sg, xl * xs, P.d);
-    uns = uns || (on && ld.ok && !(mn < (T)0.5));  // :88
-    T xs_n, xl_n;
-    solo_mem<T>(xs, xl, mn, (T)0.5 * h, h, a.xl_max, xs_n, xl_n);
-    rmt.e[0] = on ? xs_n : xs;
-    rmt.e[1] = on ? xl_n : xl;
+    if constexpr (PK != P_ADA2) uns = uns || (on && ld.ok && !(mn < (T)0.5));  // :88
+    if constexpr (PK == P_FIXED) {
+        T xs_n, xl_n;
+        solo_mem<T>(xs, xl, mn, hh, h, a.xl_max, xs_n, xl_n);
+        rmt.e[0] = on ? xs_n : xs;
+        rmt.e[1] = on ? xl_n : xl;
+    } else if constexpr (PK == P_ADA1) {
+        rmn = mn;  // the memories stay y until the second pass
+    } else {
+        T xs_n, xl_n;
+        solo_mem<T>(xs, xl, mn, hq, hh, a.xl_max, xs_n, xl_n);  // second half step (:130)
+        const T ec = dmax(e, dmax(dabs(xs_f - xs_n), dabs(xl_f - xl_n)));  // :132
+        e = on && ld.ok ? ec : e;
+        rmt.e[0] = on ? xs_n : rmt.e[0];
+        rmt.e[1] = on ? xl_n : rmt.e[1];
+    }
 }
 
 // Iteration TT of the pipeline below with a static tile index: tile TT+1's clause from the registers
 // (TT+1 < RC) or from its slot, tile TT's terms applied, the slot refilled with tile TT+1+D (its
 // memories only if that tile streams).
-template <typename T, int R, bool FAST, int RC, int D, int TT>
+template <typename T, int R, int PK, bool FAST, int RC, int D, int TT>
 __device__ __forceinline__ void res_iter3_rc(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM,
                                              TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h, bool &uns, T &e,
-                                             Vec<T, 2> (&rm)[RC]) {
+                                             Vec<T, 2> (&rm)[RC], T (&rmn)[RC]) {
     Pend<T> Q;
     TileLoad<T> &S = b[(TT + 1) % D];
-    if constexpr (TT + 1 < RC) res_clause3_reg<T, R>(a, x, S, Q, on, h, uns, rm[TT + 1]);
-    else res_clause3<T, R, P_FIXED, FAST>(a, x, CM, TT + 1, S, Q, on, h, uns, e, CMr != CM);
+    if constexpr (TT + 1 < RC) res_clause3_reg<T, R, PK>(a, x, S, Q, on, h, uns, e, rm[TT + 1], rmn[TT + 1]);
+    else res_clause3<T, R, PK, FAST>(a, x, CM, TT + 1, S, Q, on, h, uns, e, CMr != CM);
     res_apply3<T, R>(x, P);
-    res_load3<T, R, P_FIXED>(a, x, CMr, TT + 1 + D, S, TT + 1 + D >= RC);
+    res_load3<T, R, PK>(a, x, CMr, TT + 1 + D, S, TT + 1 + D >= RC);
     __syncthreads();
     P = Q;
 }
-template <typename T, int R, bool FAST, int RC, int D, int... Ts>
+template <typename T, int R, int PK, bool FAST, int RC, int D, int... Ts>
 __device__ __forceinline__ void res_prefix(std::integer_sequence<int, Ts...>, const RArgs<T> &a, const ResCtx<T, R> &x,
                                            const T *CMr, T *CM, TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h,
-                                           bool &uns, T &e, Vec<T, 2> (&rm)[RC]) {
-    (res_iter3_rc<T, R, FAST, RC, D, Ts>(a, x, CMr, CM, b, P, on, h, uns, e, rm), ...);
+                                           bool &uns, T &e, Vec<T, 2> (&rm)[RC], T (&rmn)[RC]) {
+    (res_iter3_rc<T, R, PK, FAST, RC, D, Ts>(a, x, CMr, CM, b, P, on, h, uns, e, rm, rmn), ...);
 }
 
 // One step of the 3-SAT tile pipeline: the terms of tile t+1 are computed from slot S (which is
@@ -405,14 +422,14 @@ __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> 
 // scratch) and written by kind (P_FIXED: to CM).  Ends with a barrier (dv complete).
 template <typename T, int R, int PK, bool K3, bool FAST = false, int RC = 0>
 __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, bool on, T h,
-                                         bool &uns, T &e, Vec<T, 2> (&rm)[RC > 0 ? RC : 1]) {
+                                         bool &uns, T &e, Vec<T, 2> (&rm)[RC > 0 ? RC : 1], T (&rmn)[RC > 0 ? RC : 1]) {
     const int NT_ = a.ntiles;
     if constexpr (K3) {
         // (register tiles: a ring of RES_RC_DEPTH, whose VGPRs the register tiles need more)
         constexpr int D = RC > 0 ? RES_RC_DEPTH : res_depth<T>();
         static_assert(D == 4 || D == 8, "the pipeline below is unrolled for 4 or 8 slots");
-        static_assert(RC == 0 || (PK == P_FIXED && FAST && RC % D == 0 && RC >= D),
-                      "register tiles: fixed short-form steps, whole ring blocks (the host needs ntiles > RC + D)");
+        static_assert(RC == 0 || (FAST && RC % D == 0 && RC >= D),
+                      "register tiles: short-form steps, whole ring blocks (the host needs ntiles > RC + D)");
         // the host pads 3-SAT tilings to a multiple of 4 tiles (empty tiles), so the unrolled loop
         // below runs whole (D = 8: blocks of 8, then at most one static block of 4)
         if (NT_ == 0) {
@@ -425,9 +442,10 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
         for (int i = 0; i < D; ++i) res_load3<T, R, PK>(a, x, CMr, i, b[i], i >= RC);
         int t0 = 0;
         if constexpr (RC > 0) {
-            res_clause3_reg<T, R>(a, x, b[0], P, on, h, uns, rm[0]);
+            res_clause3_reg<T, R, PK>(a, x, b[0], P, on, h, uns, e, rm[0], rmn[0]);
             res_load3<T, R, PK>(a, x, CMr, D, b[0], D >= RC);
-            res_prefix<T, R, FAST, RC, D>(std::make_integer_sequence<int, RC>{}, a, x, CMr, CM, b, P, on, h, uns, e, rm);
+            res_prefix<T, R, PK, FAST, RC, D>(std::make_integer_sequence<int, RC>{}, a, x, CMr, CM, b, P, on, h, uns, e,
+                                              rm, rmn);
             t0 = RC;
         } else {
             res_clause3<T, R, PK, FAST>(a, x, CM, 0, b[0], P, on, h, uns, e, CMr != CM);
@@ -482,7 +500,7 @@ __device__ unsigned long long g_res_clk[4096 * 64];
 template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR, bool VFG = false, bool FAST = false, int RC = 0>
 __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     static_assert(!FAST || K3, "the short forms are 3-SAT only (res_clause_any has none)");
-    static_assert(RC == 0 || (!ADAPTIVE && FAST && R == 1), "register tiles: fixed short-form steps, R = 1");
+    static_assert(RC == 0 || (FAST && R == 1), "register tiles: short-form steps, R = 1");
     extern __shared__ __attribute__((aligned(16))) unsigned char res_smem[];
     using U = typename Bits<T>::U;
     constexpr int NTH = NTHR, NL = NTHR / R;
@@ -533,6 +551,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     if (skipL || !any) return;  // uniform
     // the register tiles' memories (RC > 0): read once here, written once after the last step
     Vec<T, 2> rm[RC > 0 ? RC : 1];
+    T rmn[RC > 0 ? RC : 1];  // adaptive: each register tile's first-pass mn
     auto rm_slot = [&](int t, bool &ok) {  // tile t's slot of this lane (a valid clause when empty)
         const int c0 = ldc(a.tc, t), c = c0 + x.lc;
         ok = c < ldc(a.tc, t + 1);
@@ -554,7 +573,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
         bool uns = false;
         T e = (T)0.0;
         if constexpr (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154)
-            res_pass<T, R, P_FIXED, K3, FAST, RC>(a, x, CMr, CMo, on, h, uns, e, rm);
+            res_pass<T, R, P_FIXED, K3, FAST, RC>(a, x, CMr, CMo, on, h, uns, e, rm, rmn);
             CMr = CMo;
             if (uns) unsL[x.r] = 1u;
             const T hv = FAST ? (T)0.5 * h : h;
@@ -574,7 +593,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
                 }
             }
         } else {  // euler_step (system.rs:111-139), per-replica dt
-            res_pass<T, R, P_ADA1, K3, FAST>(a, x, CM, CM, on, h, uns, e, rm);
+            res_pass<T, R, P_ADA1, K3, FAST, RC>(a, x, CM, CM, on, h, uns, e, rm, rmn);
             if (uns) unsL[x.r] = 1u;
             __syncthreads();
             const bool st = on && unsL[x.r] != 0u;  // allsat replicas take no step (:122)
@@ -595,7 +614,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
             for (int j = 0; j < R; ++j) any_st = any_st || (actL[j] != 0 && unsL[j] != 0u);
             if (any_st) {  // uniform
                 bool u2 = false;
-                res_pass<T, R, P_ADA2, K3, FAST>(a, x, CM, CM, st, h, u2, e, rm);
+                res_pass<T, R, P_ADA2, K3, FAST, RC>(a, x, CM, CM, st, h, u2, e, rm, rmn);
                 for (int i = x.lc; i < a.n; i += NL) {
                     const int idx = i * R + x.r;
                     const T d = x.dvL[idx];

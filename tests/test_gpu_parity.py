@@ -645,36 +645,46 @@ def test_onchip_adaptive_matches_resident_and_oracle(stop, monkeypatch):
     assert same(s1[0][0], ov) and same(s1[1][0], oxs) and same(s1[2][0], oxl)
 
 
+@pytest.mark.parametrize("adaptive", [False, True])
 @pytest.mark.parametrize("stop", ["each", "any", "none"])
-def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, monkeypatch):
-    """f64 fixed steps keep the first RES_RC tiles' memories in VGPRs for a launch (resident.hpp,
-    round 4): == every tile streamed (ODESAT_RES_RC=0) bit for bit on every stop policy -- STOP_ANY
-    launches write out of place and replay -- over a fresh call and a continued one, and replica 0 ==
-    the oracle's f64 fixed steps (system.rs:141-154).  The instance's tiling is deep enough (85 tiles,
-    tests/test_tiling.py's hook) for the register prefix (the host needs RES_RC + 16)."""
+def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, adaptive, monkeypatch):
+    """f64 steps keep the first RES_RC (fixed) / RES_RC_ADA (adaptive, VFG: with each tile's first-pass
+    mn) tiles' memories in VGPRs for a launch (resident.hpp, round 4): == every tile streamed
+    (ODESAT_RES_RC=0) bit for bit on every stop policy -- fixed STOP_ANY launches write out of place and
+    replay -- over a fresh call and a continued one (per-replica dt included), and replica 0 == the
+    oracle's f64 simulate (system.rs:111-154).  The instances' tilings are deep enough (85+ tiles,
+    tests/test_tiling.py's hook) for the register prefix (the host needs RC + 16); the adaptive one is
+    large enough (n = 7 000) for the clone-in-HBM kernel."""
     from odesat_amd import _lib
-    f, (cp, v_, n_) = _instance(3000, 12600, 5)
+    n, m = (7000, 29400) if adaptive else (3000, 12600)
+    f, (cp, v_, n_) = _instance(n, m, 5)
     pol = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[stop]
-    B = 6
+    B = 4 if adaptive else 6
+    kw = dict(adaptive=True, tol=1e-3) if adaptive else dict(dt=0.05)
     out = []
     for rc in ("1", "0"):
         monkeypatch.setenv("ODESAT_RES_RC", rc)
         with Solver(f, B, "f64") as s:
-            assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.step_kernel(False) == "k_resident"
+            assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.step_kernel(adaptive) == "k_resident"
             s.init_state(9)
-            r1 = s.simulate(dt=0.05, zeta=0.001, max_steps=13, stop=pol, poll_interval=13)
-            r2 = s.simulate(dt=0.05, zeta=0.001, max_steps=9, stop=pol, poll_interval=4, resume=True)
+            r1 = s.simulate(zeta=0.001, max_steps=13, stop=pol, poll_interval=13, **kw)
+            r2 = s.simulate(zeta=0.001, max_steps=9, stop=pol, poll_interval=4, resume=True, **kw)
             out.append((r1, r2, s.get_state()))
     (a1, a2, sa), (b1, b2, sb) = out
     for x, y in ((a1, b1), (a2, b2)):
         assert x["steps_run"] == y["steps_run"]
         assert np.array_equal(x["first_sat_step"], y["first_sat_step"]) and np.array_equal(x["steps_done"], y["steps_done"])
+        assert same(x["dt"], y["dt"])
     for x, y in zip(sa, sb):
         assert same(x, y)
-    o = Oracle(cp, v_, n_, 3000, "f64")
-    ov = init_voltages(9, 0, 1, 3000)[0]
-    oxs, oxl = o.init_short_term_memory(), np.ones(12600)
-    o.simulate(ov, oxs, oxl, dt=0.05, steps=int(a2["steps_done"][0]), zeta=0.001)
+    o = Oracle(cp, v_, n_, n, "f64")
+    ov = init_voltages(9, 0, 1, n)[0]
+    oxs, oxl = o.init_short_term_memory(), np.ones(m)
+    t, _, _, h, _ = o.simulate(ov, oxs, oxl, tol=1e-3 if adaptive else None, dt=None if adaptive else 0.05,
+                               steps=int(a2["steps_done"][0]), zeta=0.001)
+    assert t == a2["steps_done"][0]
+    if adaptive:
+        assert same(h, a2["dt"][0])
     assert same(sa[0][0], ov) and same(sa[1][0], oxs) and same(sa[2][0], oxl)
 
 
