@@ -404,6 +404,11 @@ def roofline(args, short, ms, launches, clause_bytes_step, batch=None, dtype=Non
                               "frac": lds / per_launch_s / 1e9 / LDS_PEAK_GINST, "lds_insts_per_launch": lds}
     else:
         r.update({"bound": "hbm", **hbm})
+        if traffic is not None:  # the bytes the kernel actually moved (PMC) at the same launch time
+            t_gbs = traffic / per_launch_s / 1e9
+            r["hbm_traffic"] = {"achieved": t_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": t_gbs / HBM_PEAK_GBS}
+            if short == "k_resident" and traffic < 0.9 * per_launch_bytes:
+                r["note"] = RES_RC_NOTE
     return r
 
 
@@ -411,6 +416,11 @@ ONCHIP_NOTE = ("k_onchip keeps v, dv and the clause memories on the CU for a who
                "once per launch (traffic), so the HBM-algorithmic rate exceeds the HBM peak and the binding "
                "resource is the CU's VALU issue (plus LDS/barrier latency; DESIGN.md §4.0).  ab_hbm_streaming is "
                "the HBM-bound kernel on the same workload.")
+RES_RC_NOTE = ("the f64 k_resident keeps its first register tiles' clause memories (fixed: 28 tiles; adaptive: 12, "
+               "with the first pass's mn) in VGPRs for a whole launch (DESIGN.md §4.1), so it moves fewer bytes than "
+               "the algorithmic convention counts (traffic) and the algorithmic rate can exceed the HBM peak; "
+               "hbm_traffic is the rate of the bytes actually moved.  At ~1 500 cycles per tile it is bound by its f64 "
+               "arithmetic and per-tile barriers more than by HBM.")
 WAVE_NOTE = ("k_wave keeps a replica's v, memories, terms and topology in LDS for a whole launch (HBM moves the "
              "state once per launch): the CU's VALU and LDS issue bound it (DESIGN.md §4.3b); lds_issue gives "
              "the LDS instruction rate against one LDS instruction per CU per cycle.")
