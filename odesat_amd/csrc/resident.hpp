@@ -391,6 +391,9 @@ __device__ __forceinline__ void res_iter3_rc(const RArgs<T> &a, const ResCtx<T, 
     else res_clause3<T, R, PK, FAST>(a, x, CM, TT + 1, S, Q, on, h, uns, e, CMr != CM);
     res_apply3<T, R>(x, P);
     res_load3<T, R, PK>(a, x, CMr, TT + 1 + D, S, TT + 1 + D >= RC);
+#ifdef RES_TIMING_PAIRS  // timing-only diagnostic build (results race): a barrier after odd tiles only
+    if (TT & 1)
+#endif
     __syncthreads();
     P = Q;
 }
