@@ -1524,12 +1524,13 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             s->res_ada = true;  // wave_lds_bytes(adaptive) fits by selection
             // k_solo (wave.hpp): the latency path when k_wave would run one replica per workgroup
             // anyway (small batches, B = 1 for solve): every lane's clause and variable slots in
-            // registers.  Lanes: one per clause, at least 256 (a wave per SIMD) and at most 512
-            // (measured, profiles/r03_solo_sweep.jsonl: hard.cnf f64 fixed 1.01 / 0.81 / 0.79 us per
-            // step at 128 / 256 / 512 lanes; config 3 at 512 lanes 15-25 % under k_wave's best team,
-            // at 1024 no faster and slower in f64 adaptive steps).
+            // registers.  Lanes: one per clause rounded up to a wave, at least 192 and at most 512
+            // (measured, profiles/r03_solo_sweep.jsonl: config 3 at 512 lanes 15-25 % under k_wave's
+            // best team, at 1024 no faster and slower in f64 adaptive steps; round 4,
+            // profiles/r04ae_solo_lanes.txt: hard.cnf (m = 160) f64 criterion calls 4.64-4.66 / 12.23-12.24
+            // ms fixed / adaptive at 192 lanes against 4.85-4.93 / 12.54-12.57 at 256 and 5.6 / 13.4 at 128).
             // ODESAT_SOLO=0/1 and ODESAT_SOLO_LANES override.
-            int64_t nl = std::min<int64_t>(512, std::max<int64_t>(256, (m + 63) / 64 * 64));
+            int64_t nl = std::min<int64_t>(512, std::max<int64_t>(192, (m + 63) / 64 * 64));
             if (const char *ev = std::getenv("ODESAT_SOLO_LANES")) {
                 const int64_t want = std::atoll(ev);
                 if (want >= 64 && want <= SOLO_MAX_NL && want % 64 == 0) nl = want;
