@@ -184,3 +184,22 @@ def test_time_gpu_excludes_the_closing_barrier():
     assert wall < 0.02
     wall0, _, _, _ = bench.time_gpu(_FakeSolver(), 20, 5, None, 0, False, ODESAT_STOP_NONE)
     assert abs(wall - wall0) < 0.02
+
+
+def test_roofline_reads_the_committed_profiles():
+    """The bench line's roofline from the committed PMC fits (profiles/profile_*.json), at the
+    driver's shape (20 steps, B = 1024, config 2) with made-up launch times: k_onchip names VALU issue
+    and carries its cycle model; the f64 k_resident with register tiles moves fewer bytes than the
+    algorithmic convention counts, so its line also carries the rate of the bytes actually moved
+    (hbm_traffic, below the HBM peak) and says why the algorithmic rate can exceed the peak."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    args = SimpleNamespace(batch=1024, dtype="f32", config="config2", steps=20, profile_dir=os.path.join(ROOT, "profiles"))
+    n, m = 10000, 42000
+    r = bench.roofline(args, "k_onchip", [1.6, 0.0, 0.0], [1, 0, 0], 1024 * (8 * n + 16 * m))
+    assert r["bound"] == "valu" and 0.1 < r["frac"] < 1.0 and r["traffic"] > 0
+    assert 0.0 < r["cycle_model"]["valu_floor_frac"] < 1.0
+    r64 = bench.roofline(args, "k_resident", [4.7, 0.0, 0.0], [1, 0, 0], 1024 * (8 * n + 16 * m) * 2, dtype="f64")
+    assert r64["bound"] == "hbm" and r64["traffic"] < 0.9 * r64["algorithmic_bytes_per_launch"]
+    assert 0.0 < r64["hbm_traffic"]["frac"] < r64["frac"] and "register tiles" in r64["note"]
