@@ -164,8 +164,8 @@ def test_config2_f32_tracks_f64_reference_at_bench_horizon():
 
 @pytest.mark.parametrize("leg,prec,adaptive,kernel", [
     ("adaptive", "f32", True, "k_onchip"),       # k_onchip<90, 1, true>
-    ("f64", "f64", False, "k_resident"),         # short forms, ring of 8 (§4.1)
-    ("f64_adaptive", "f64", True, "k_resident"),  # VFG: the full-step clone in HBM (§4.1)
+    ("f64", "f64", False, "k_resident"),         # short forms, 28 register tiles (§4.1)
+    ("f64_adaptive", "f64", True, "k_resident"),  # VFG: the clone in HBM, 12 register tiles (§4.1)
 ])
 def test_config2_bench_leg_kernels_bitexact(leg, prec, adaptive, kernel):
     """bench.py's `adaptive`, `f64` and `f64_adaptive` legs at the configuration they time: n=10k,
