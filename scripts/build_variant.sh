@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 name=$1; flags=$2; src=${3:-onchip}
 mkdir -p build/vobj/$name expt
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -Wall -Wno-unused-function"
-extra=""; [ "$src" = onchip ] && extra="-fno-slp-vectorize"
+extra=""; [ "$src" = onchip ] && extra="-fno-slp-vectorize -mllvm -amdgpu-sched-strategy=max-ilp"  # (the Makefile's ONCHIP_FLAGS)
 $H $extra $flags -c -o build/vobj/$name/$src.o odesat_amd/csrc/$src.hip
 objs=""
 for o in odesat_hip onchip partition cnf preprocess stoch run_abi; do
