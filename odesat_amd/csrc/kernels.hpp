@@ -1036,6 +1036,9 @@ __global__ void k_gather(double *dst, const T *b0, const T *b1, const uint8_t *p
     dst[tid] = (double)src[(((size_t)g * items + i) * W + (r % W)) * stride + comp];
 }
 
+// (ODK_NO_COMMON_KERNELS: a second translation unit -- wave_k.hip -- includes this header for its
+// device helpers; the three non-template kernels below are defined in odesat_hip.hip's only.)
+#ifndef ODK_NO_COMMON_KERNELS
 // Checkpoint (to_ck) or rollback of one double-buffered state array: group g's words live in buffer
 // par[g]; ck holds them group by group.
 __global__ void k_group_copy(uint32_t *ck, uint32_t *b0, uint32_t *b1, const uint8_t *par, int64_t gwords, int G,
@@ -1048,9 +1051,8 @@ __global__ void k_group_copy(uint32_t *ck, uint32_t *b0, uint32_t *b1, const uin
     }
 }
 
-// Per-call bookkeeping of odesat_simulate, queued on the solver's stream (no host round trip):
-// every real replica active, no sat step, no steps done, the adaptive dt restarted at 0.01
-// (system.rs:205) when reset_dt, and the stop word cleared.
+#endif
+
 // owner-TT prologue: the current buffer's clause products xl xs (k_step's t, :80) for every group
 template <typename T>
 __global__ void k_tt_init(const T *c0, const T *c1, const uint8_t *par, T *tt0, T *tt1, int64_t per_group,
@@ -1062,6 +1064,10 @@ __global__ void k_tt_init(const T *c0, const T *c1, const uint8_t *par, T *tt0, 
     }
 }
 
+#ifndef ODK_NO_COMMON_KERNELS
+// Per-call bookkeeping of odesat_simulate, queued on the solver's stream (no host round trip):
+// every real replica active, no sat step, no steps done, the adaptive dt restarted at 0.01
+// (system.rs:205) when reset_dt, and the stop word cleared.
 __global__ void k_begin_call(uint8_t *act, uint32_t *unsat, int64_t *sat_step, int64_t *steps_done, void *dtr,
                              int dtype, int reset_dt, int64_t B, int64_t Bp, int32_t *stop) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1088,6 +1094,7 @@ __global__ void k_reset_replicas(uint8_t *act, uint32_t *unsat, int64_t *sat_ste
     if (dtype == ODESAT_F64) ((double *)dtr)[r] = 0.01;
     else ((float *)dtr)[r] = 0.01f;
 }
+#endif
 
 // The exact short forms of one 3-SAT clause on in-range states (the FAST launches of k_resident,
 // k_wave, k_solo_fast; onchip.hip's header states the exactness argument).

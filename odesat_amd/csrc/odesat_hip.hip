@@ -821,31 +821,28 @@ template <typename T, bool ADA, int WPW, int TW, bool FAST> int launch_wave_k(od
     a.topo_bytes = (uint32_t)wave_topo_bytes(s->n, s->m);
     a.rep_bytes = (uint32_t)wave_lds_bytes(s->n, s->m, s->L, sizeof(T), ADA);
     const size_t lds = a.topo_bytes + (size_t)WPW * a.rep_bytes;
-    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_wave<T, ADA, WPW, TW, FAST>), (int)RES_LDS_MAX));
+    const unsigned grid = (unsigned)((s->G + WPW - 1) / WPW), block = WAVE_NTH * WPW * TW;
+    HIP_TRY((wave_launch<T, ADA, WPW, TW, FAST>(true, a, grid, block, lds, (int)RES_LDS_MAX, s->stream)));
+    hipError_t e;
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_wave<T, ADA, WPW, TW, FAST>), dim3((unsigned)((s->G + WPW - 1) / WPW)),
-                           dim3(WAVE_NTH * WPW * TW), lds, s->stream, a);
+        e = wave_launch<T, ADA, WPW, TW, FAST>(false, a, grid, block, lds, (int)RES_LDS_MAX, s->stream);
     }
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(e);
     return ODESAT_OK;
 }
 
 template <typename T, bool ADA, int CPL, int VPL, bool FAST> int launch_solo_k(odesat_solver *s, WArgs<T> a) {
-    if constexpr (FAST) {  // k_solo_fast: in-range states
-        const size_t lds = solo_fast_elems(s->n, s->L, sizeof(T)) * sizeof(T);
-        HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_solo_fast<T, ADA, CPL, VPL>), (int)RES_LDS_MAX));
+    // k_solo_fast on in-range states, k_solo otherwise
+    const size_t lds = FAST ? solo_fast_elems(s->n, s->L, sizeof(T)) * sizeof(T) : (size_t)(s->n + s->L) * sizeof(T);
+    const unsigned grid = (unsigned)s->G, block = (unsigned)s->solo_nl;
+    HIP_TRY((solo_launch<T, ADA, CPL, VPL, FAST>(true, a, grid, block, lds, (int)RES_LDS_MAX, s->stream)));
+    hipError_t e;
+    {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_solo_fast<T, ADA, CPL, VPL>), dim3((unsigned)s->G), dim3((unsigned)s->solo_nl), lds,
-                           s->stream, a);
-    } else {
-        const size_t lds = (size_t)(s->n + s->L) * sizeof(T);
-        HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_solo<T, ADA, CPL, VPL>), (int)RES_LDS_MAX));
-        Timed tm(s, 0);
-        hipLaunchKernelGGL((k_solo<T, ADA, CPL, VPL>), dim3((unsigned)s->G), dim3((unsigned)s->solo_nl), lds,
-                           s->stream, a);
+        e = solo_launch<T, ADA, CPL, VPL, FAST>(false, a, grid, block, lds, (int)RES_LDS_MAX, s->stream);
     }
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(e);
     return ODESAT_OK;
 }
 

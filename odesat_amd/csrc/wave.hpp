@@ -941,6 +941,16 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
     }
 }
 
+// The launches of k_wave / k_solo / k_solo_fast live in wave_k.hip, a translation unit of their own
+// built with the max-ILP machine scheduler (Makefile WAVE_FLAGS): prep = true sets the
+// kernel's dynamic-LDS limit (once per device, outside any timed region), prep = false launches.
+template <typename T, bool ADA, int WPW, int TW, bool FAST>
+hipError_t wave_launch(bool prep, const WArgs<T> &a, unsigned grid, unsigned block, size_t lds, int lds_max,
+                       hipStream_t st);
+template <typename T, bool ADA, int CPL, int VPL, bool FAST>
+hipError_t solo_launch(bool prep, const WArgs<T> &a, unsigned grid, unsigned block, size_t lds, int lds_max,
+                       hipStream_t st);
+
 }  // namespace odk
 
 #ifdef SOLO_STAMPS
