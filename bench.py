@@ -89,6 +89,10 @@ def parse():
     p.add_argument("--steady-calls", type=int, default=8,
                    help="after the headline's timed call, repeat it this many times back to back (untimed for "
                         "`value`) and report their medians as steady_state; 0 = off")
+    p.add_argument("--lib", default="", help="A/B tooling: load this libodesat_hip build (scripts/build_variant.sh) "
+                                             "instead of the in-tree product library")
+    p.add_argument("--knob", action="append", default=[], metavar="KEY=VALUE",
+                   help="A/B tooling: an experiment knob (odesat_set_experiment, DESIGN.md §4.6); repeatable")
     p.add_argument("--leg-deadline", type=float, default=900.0,
                    help="seconds after the headline by which every extra leg must be done; past it each rank's "
                         "watchdog ends the job (rank 0 first prints the line with the legs finished so far)")
@@ -376,7 +380,8 @@ def roofline(args, short, ms, launches, clause_bytes_step, batch=None, dtype=Non
         traffic = pj["hbm_bytes_fixed"] + pj["hbm_bytes_per_step"] * steps_per_launch
         if "valu_insts_per_step" in pj:
             valu = pj["valu_insts_fixed"] + pj["valu_insts_per_step"] * steps_per_launch
-    r = {"kernel": kernel, "traffic": traffic, "mean_launch_us": per_launch_s * 1e6, "launches": nlaunch,
+    r = {"kernel": kernel, "traffic": traffic, "traffic_counts": TRAFFIC_COUNTS if traffic is not None else None,
+         "mean_launch_us": per_launch_s * 1e6, "launches": nlaunch,
          "steps_per_launch": steps_per_launch, "algorithmic_bytes_per_launch": per_launch_bytes,
          "profile": pj["file"] if pj else None}
     hbm = {"achieved": hbm_alg, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_alg / HBM_PEAK_GBS}
@@ -406,11 +411,22 @@ def roofline(args, short, ms, launches, clause_bytes_step, batch=None, dtype=Non
         r.update({"bound": "hbm", **hbm})
         if traffic is not None:  # the bytes the kernel actually moved (PMC) at the same launch time
             t_gbs = traffic / per_launch_s / 1e9
-            r["hbm_traffic"] = {"achieved": t_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": t_gbs / HBM_PEAK_GBS}
+            r["fabric_traffic"] = {"achieved": t_gbs, "unit": "GB/s", "copy_rate": HBM_COPY_GBS,
+                                   "note": "L2 <-> fabric bytes per second, Infinity-Cache hits included: above the "
+                                           "HBM copy rate when re-reads hit the Infinity Cache"}
             if short == "k_resident" and traffic < 0.9 * per_launch_bytes:
                 r["note"] = RES_RC_NOTE
     return r
 
+
+# What roofline.traffic counts (round 5, scripts/micro/fetch_calib.hip, profiles/r05_fetch_calibration.json):
+# 2 x FETCH_SIZE + WRITE_SIZE equals the known bytes of every access shape measured -- 4, 8 and 16 B per lane,
+# 256- and 512-B random rows, random 4-B gathers (one 128-B line per miss) -- but a 64 MiB buffer re-read from
+# the Infinity Cache counts the same as one read from HBM: the counters sit between the L2s and the fabric.
+TRAFFIC_COUNTS = ("L2 <-> fabric bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, exact at 128-B request granularity "
+                  "for every access width; Infinity-Cache hits are included, so HBM bytes are at most this: "
+                  "profiles/r05_fetch_calibration.json)")
+HBM_COPY_GBS = 6290.0  # the float4 copy rate measured on this part
 
 ONCHIP_NOTE = ("k_onchip keeps v, dv and the clause memories on the CU for a whole launch: HBM moves the state "
                "once per launch (traffic), so the HBM-algorithmic rate exceeds the HBM peak and the binding "
@@ -419,7 +435,7 @@ ONCHIP_NOTE = ("k_onchip keeps v, dv and the clause memories on the CU for a who
 RES_RC_NOTE = ("the f64 k_resident keeps its first register tiles' clause memories (fixed: 28 tiles; adaptive: 12, "
                "with the first pass's mn) in VGPRs for a whole launch (DESIGN.md §4.1), so it moves fewer bytes than "
                "the algorithmic convention counts (traffic) and the algorithmic rate can exceed the HBM peak; "
-               "hbm_traffic is the rate of the bytes actually moved.  At ~1 500 cycles per tile it is bound by its f64 "
+               "fabric_traffic is the rate of the bytes actually moved.  At ~1 500 cycles per tile it is bound by its f64 "
                "arithmetic and per-tile barriers more than by HBM.")
 WAVE_NOTE = ("k_wave keeps a replica's v, memories, terms and topology in LDS for a whole launch (HBM moves the "
              "state once per launch): the CU's VALU and LDS issue bound it (DESIGN.md §4.3b); lds_issue gives "
@@ -484,6 +500,11 @@ def main():
     legs = [x for x in LEGS if x not in args.skip_legs]
 
     from odesat_amd import _lib
+    if args.lib:  # measurement tooling only; the line records it
+        _lib.use_library(args.lib)
+    for kv in args.knob:
+        k, v = kv.split("=", 1)
+        _lib.set_experiment(k.strip(), int(v))
     from odesat_amd.sharding import max_over_ranks, shard_range
     from odesat_amd.system import ODESAT_STOP_ANY, ODESAT_STOP_NONE, Solver
 
@@ -542,6 +563,7 @@ def main():
                        "global_batch": B * world, "batch_per_gpu": B, "n": n, "m": m,
                        "parallelism": f"replica-sharded x{world} (no collectives)"},
             "roofline": roof,
+            **({"variant": {"lib": args.lib, "knobs": args.knob}} if args.lib or args.knob else {}),
             "steady_state": steady_out[0] if steady_out else None,
             "step_kernels_ms": {"clause": ms[0], "variable": ms[1], "status": ms[2]},
             "step_algorithmic_GBps": step_bytes * args.steps / wall / 1e9,
@@ -812,6 +834,7 @@ def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5")
                          "algorithmic_bytes_per_step": alg_bytes, "gpu_ms_per_step": per_step_s * 1e3,
                          "traffic": traffic, "traffic_profile": "profiles/profile_k_part_config5.json (world 1)"
                          if traffic is not None else None,
+                         "traffic_counts": TRAFFIC_COUNTS if traffic is not None else None,
                          "gather_floor": {"us_per_step": GATHER_FLOOR_US_C5 / world,
                                           "frac": GATHER_FLOOR_US_C5 / world / (per_step_s * 1e6),
                                           "source": "scripts/micro/gather_ceiling.hip, profiles/r02_gather_ceiling.jsonl: "

@@ -293,6 +293,18 @@ int odesat_group_width(const odesat_solver *s);
 /* The step kernel odesat_simulate launches for fixed (adaptive = 0) or adaptive steps: "k_onchip",
  * "k_resident", "k_wave", "k_step" (FUSED) or "k_clause_u" (TWOPASS); NULL for a null solver. */
 const char *odesat_step_kernel(const odesat_solver *s, int adaptive);
+/* Experiment knobs: kernel variants and layouts for A/B measurement and for the
+ * parity tests that drive every path against the oracle.  Production callers never need them: the
+ * defaults are the measured best, and every variant is bit-identical to them.  The library reads no
+ * environment variable; a knob is set here, process-wide, and read when the object it shapes is
+ * created (solver, partition or stoch context; RUN_CHUNK by each odesat_run).  value >= 0 sets the
+ * knob, value < 0 unsets it.  ODESAT_EINVAL for an unknown key.  odesat_get_experiment stores the
+ * knob's value, or -1 when it is unset.  odesat_experiment_knob(i) names the i-th knob
+ * (ODESAT_EINVAL past the last). */
+int odesat_set_experiment(const char *key, int64_t value);
+int odesat_get_experiment(const char *key, int64_t *value);
+void odesat_clear_experiments(void);
+int odesat_experiment_knob(int i, const char **name);
 
 /* --------------------------------------------- one instance across GPUs ------- */
 

@@ -9,7 +9,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("ODESAT_LIB") or os.path.join(_HERE, "lib", "libodesat_hip.so")  # override: A/B builds
+LIB_PATH = os.path.join(_HERE, "lib", "libodesat_hip.so")  # the in-tree product library (use_library: A/B builds)
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "odesat.h")
 
 ODESAT_OK, ODESAT_EINVAL, ODESAT_ENOMEM, ODESAT_EDEVICE, ODESAT_ESTATE = 0, -1, -2, -3, -4
@@ -102,6 +102,10 @@ SIGNATURES = {
     "odesat_get_algorithm": (C.c_int, [_P]),
     "odesat_group_width": (C.c_int, [_P]),
     "odesat_step_kernel": (C.c_char_p, [_P, C.c_int]),
+    "odesat_set_experiment": (C.c_int, [C.c_char_p, _i64]),
+    "odesat_get_experiment": (C.c_int, [C.c_char_p, _i64p]),
+    "odesat_clear_experiments": (None, []),
+    "odesat_experiment_knob": (C.c_int, [C.c_int, C.POINTER(C.c_char_p)]),
     "odesat_part_create": (C.c_int, [C.c_int, C.c_int, _i64, _i64, _i64, _i64p, _i64p, _u8p, _i64, _i64, _i64p,
                                      _i64p, _i64, C.POINTER(_P)]),
     "odesat_part_destroy": (None, [_P]),
@@ -135,6 +139,15 @@ def _adopt_torch_runtime():
         p = os.path.join(d, name)
         if os.path.exists(p):
             C.CDLL(p, mode=C.RTLD_GLOBAL)
+
+
+def use_library(path: str) -> None:
+    """Measurement tooling only (scripts/build_variant.sh builds): load `path` instead of the in-tree
+    library.  Must be called before the first call into the library; the product never calls it."""
+    global LIB_PATH
+    if _lib is not None and os.path.abspath(path) != os.path.abspath(LIB_PATH):
+        raise RuntimeError(f"libodesat_hip already loaded from {LIB_PATH}")
+    LIB_PATH = os.path.abspath(path)
 
 
 def lib():
@@ -171,6 +184,52 @@ def u8ptr(a):
 
 def i64ptr(a):
     return None if a is None else a.ctypes.data_as(_i64p)
+
+
+def set_experiment(key: str, value) -> None:
+    """An experiment knob (include/odesat.h odesat_set_experiment): A/B variants and the
+    parity tests' forced paths.  value None (or < 0) unsets it.  Read when a solver / partition / stoch
+    context is created."""
+    check(lib().odesat_set_experiment(key.encode(), -1 if value is None else int(value)))
+
+
+def get_experiment(key: str):
+    v = C.c_int64(0)
+    check(lib().odesat_get_experiment(key.encode(), C.byref(v)))
+    return None if v.value < 0 else v.value
+
+
+def clear_experiments() -> None:
+    lib().odesat_clear_experiments()
+
+
+def experiment_knobs() -> list:
+    out, i = [], 0
+    name = C.c_char_p()
+    while lib().odesat_experiment_knob(i, C.byref(name)) == ODESAT_OK:
+        out.append(name.value.decode())
+        i += 1
+    return out
+
+
+class experiments:
+    """Context manager: `with experiments(WAVE=1, RES_NARROW=0): ...` sets the knobs and restores their
+    previous values on exit."""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.knobs.items():
+            self.old[k] = get_experiment(k)
+            set_experiment(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            set_experiment(k, v)
+        return False
 
 
 def device_count() -> int:

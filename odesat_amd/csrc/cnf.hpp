@@ -21,3 +21,12 @@ void set_error(const std::string &msg);
 int fail(int code, const std::string &msg);
 
 }  // namespace odesat
+
+namespace odesat {
+
+// Experiment knobs (odesat_set_experiment, experiment.cpp): the value set for `key`, or `dflt` when
+// the knob is unset.  Read by the host code when it shapes a solver, a partition or a stoch context.
+int64_t xp_get(const char *key, int64_t dflt);
+inline bool xp_isset(const char *key) { return xp_get(key, -1) >= 0; }
+
+}  // namespace odesat

@@ -122,7 +122,6 @@ template <typename T> struct KArgs {
     T *w;                              // contributions [chunk groups][L][W] (TWOPASS)
     T *vh, *vf;                        // half / full voltages (adaptive); DERIV: vh = dv
     T *ch, *cf;                        // half / full memories (adaptive); DERIV: ch = (dxs, dxl)
-    T *tt0, *tt1;                      // double-buffered clause products xl xs [G][m][W] (FUSED owner-TT)
     T *dtr;                            // [Bp] per-replica adaptive dt
     typename Bits<T>::U *err;          // [Bp] max_error bits (non-negative floats order as ints)
     uint32_t *unsat;                   // [Bp] 1 = some clause had C >= gamma this step
@@ -180,15 +179,13 @@ template <int LW, int VEC> struct Geo {
 };
 
 template <typename T> struct Bufs {
-    T *vcur, *vnxt, *ccur, *cnxt, *tcur, *tnxt;
+    T *vcur, *vnxt, *ccur, *cnxt;
     __device__ __forceinline__ Bufs(const KArgs<T> &a, int g) {
         const bool p = a.par[g] != 0;
         vcur = p ? a.v1 : a.v0;
         vnxt = p ? a.v0 : a.v1;
         ccur = p ? a.c1 : a.c0;
         cnxt = p ? a.c0 : a.c1;
-        tcur = p ? a.tt1 : a.tt0;
-        tnxt = p ? a.tt0 : a.tt1;
     }
 };
 
@@ -220,7 +217,7 @@ template <typename T, int VEC, int MODE>
 __device__ __forceinline__ void clause_update(const KArgs<T> &a, const Bufs<T> &bf, size_t ci,
                                               const T (&C)[VEC], const Vec<T, 2 * VEC> &mem,
                                               const T (&h)[VEC], const bool (&on)[VEC], bool all_on,
-                                              T (&e)[VEC], T *ttn = nullptr) {
+                                              T (&e)[VEC]) {
     const T one = (T)1.0, eps = (T)0.001, xs_hi = (T)1.0 - (T)0.001;
     Vec<T, 2 * VEC> o1, o2;
 #pragma unroll
@@ -249,12 +246,6 @@ __device__ __forceinline__ void clause_update(const KArgs<T> &a, const Bufs<T> &
         stv<T, 2 * VEC>(a.ch + ci, o1);
     } else if (MODE == M_FIXED) {
         stv_nt<T, 2 * VEC>(bf.cnxt + ci, o1);
-        if (ttn) {  // owner-TT: the next step's clause product xl xs (:80's factor), for the other literals
-            Vec<T, VEC> tp;
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) tp.e[k] = o1.e[2 * k + 1] * o1.e[2 * k];
-            stv<T, VEC>(ttn, tp);
-        }
     } else if (MODE == M_ADA) {
         stv<T, 2 * VEC>(a.cf + ci, o1);
         stv<T, 2 * VEC>(a.ch + ci, o2);
@@ -362,20 +353,14 @@ template <typename T> __device__ __forceinline__ void minsec(T val, T &mn, T &se
 template <typename T, int VEC, int RB> struct Batch {
     Inc rec[RB];
     Vec<T, VEC> vv[RB][3];
-    Vec<T, 2 * VEC> mem[RB];  // owner-TT: the other literals' incidences hold the clause product in mem[b].e[0..VEC)
+    Vec<T, 2 * VEC> mem[RB];
 };
 
-// TT (owner-TT, round 4; fixed steps on in-range states, see k_step): only the clause's owning
-// incidence reads and writes its memory row; it also stores the next step's product xl xs, which the
-// other two incidences read (one T per replica instead of the (xs, xl) pair).  On in-range states the
-// rigidity term is +-0 (onchip.hip's header), which a dv that starts at +0 and is never -0 absorbs, so
-// those incidences need nothing else of the clause: every dv is bit-identical to the general form's.
-template <typename T, int W, int VEC, int MODE, int RB, bool TT = false>
+template <typename T, int W, int VEC, int MODE, int RB>
 __device__ __forceinline__ void stream_rows3(const KArgs<T> &a, const Bufs<T> &bf, const T *__restrict__ V,
                                              const T *CM, size_t vbase, size_t cbase, int i0, int i1,
                                              const T (&h)[VEC], const bool (&on)[VEC], bool all_on,
                                              bool (&uns)[VEC], T (&e)[VEC]) {
-    const size_t tbase = cbase / 2;  // the product buffer's element offset (W values per clause row)
     const T one = (T)1.0, halfc = (T)0.5;
     const int P0 = ldc(a.vptr, i0), P1 = ldc(a.vptr, i1);
     int cur = i0;
@@ -412,17 +397,7 @@ __device__ __forceinline__ void stream_rows3(const KArgs<T> &a, const Bufs<T> &b
             B.vv[b][2] = ldv<T, VEC>(V + vbase + (size_t)(r[b].w >> 1) * W);
         }
 #pragma unroll
-        for (int b = 0; b < RB; ++b) {
-            if constexpr (TT) {  // (VEC == 1) no branch: the owner's (xs, xl), the others' product twice
-                const size_t c = (size_t)(r[b].x >> 2);
-                const bool own0 = (r[b].x & 3) == 0;  // uniform (LW = 64: one incidence per wave)
-                const T *pa = own0 ? CM + cbase + c * W * 2 : bf.tcur + tbase + c * W;
-                B.mem[b].e[0] = __builtin_nontemporal_load(pa);
-                B.mem[b].e[1] = __builtin_nontemporal_load(own0 ? pa + 1 : pa);
-            } else {
-                B.mem[b] = ldv_nt<T, 2 * VEC>(CM + cbase + (size_t)(r[b].x >> 2) * W * 2);
-            }
-        }
+        for (int b = 0; b < RB; ++b) B.mem[b] = ldv_nt<T, 2 * VEC>(CM + cbase + (size_t)(r[b].x >> 2) * W * 2);
     };
     auto compute = [&](const Batch<T, VEC, RB> &B, int q0) {
 #pragma unroll
@@ -449,18 +424,14 @@ __device__ __forceinline__ void stream_rows3(const KArgs<T> &a, const Bufs<T> &b
                 const T val = one - qo * vio;
                 const T g_ = halfc * qo * (val != mn ? mn : sec);                    // :64-70
                 const T xs_m = B.mem[b].e[2 * k], xl_m = B.mem[b].e[2 * k + 1];
-                // owner-TT: the other incidences hold the owner's product in both words; their tr is
-                // then some finite number and r_ is +-0 on in-range states, so tr r_ is a signed zero,
-                // which the sum below and a dv that is never -0 absorb (see above)
-                const T t = (TT && own != 0) ? xs_m : xl_m * xs_m;
+                const T t = xl_m * xs_m;
                 const T tr = (one + a.zeta * xl_m) * (one - xs_m);
                 const T r_ = (C[k] == one - qo * vio) ? halfc * (qo - vio) : (T)0.0;  // :73-77
                 dv[k] += t * g_ + tr * r_;                                            // :80
                 if (MODE != M_ADB && own == 0) uns[k] = uns[k] || (on[k] && !(C[k] < (T)0.25));
             }
             if (own == 0)  // the clause's first literal owns its memories
-                clause_update<T, VEC, MODE>(a, bf, cbase + (size_t)c * W * 2, C, B.mem[b], h, on, all_on, e,
-                                            TT ? bf.tnxt + tbase + (size_t)c * W : nullptr);
+                clause_update<T, VEC, MODE>(a, bf, cbase + (size_t)c * W * 2, C, B.mem[b], h, on, all_on, e);
             }
         }
     };
@@ -507,9 +478,8 @@ __device__ __forceinline__ void stream_rows3(const KArgs<T> &a, const Bufs<T> &b
 #else
 #define KSTEP_ATTR
 #endif
-template <typename T, int LW, int VEC, int MODE, int K, int RB = 4, bool TT = false>
+template <typename T, int LW, int VEC, int MODE, int K, int RB = 4>
 __global__ __launch_bounds__(256) KSTEP_ATTR void k_step(KArgs<T> a) {
-    static_assert(!TT || (LW == 64 && VEC == 1 && K == 3 && MODE == M_FIXED), "owner-TT: the 3-SAT incidence stream, fixed steps");
     using G_ = Geo<LW, VEC>;
     constexpr int W = G_::W, IPR = G_::IPR;
     static_assert(K == 0 || K == 3, "incidence records are laid out for 3-SAT");
@@ -536,7 +506,7 @@ __global__ __launch_bounds__(256) KSTEP_ATTR void k_step(KArgs<T> a) {
     if constexpr (LW == 64 && K == 3) {
         const int i0 = __builtin_amdgcn_readfirstlane(geo.tile * a.rows);
         const int i1 = min(i0 + a.rows, a.n);
-        if (i0 < i1) stream_rows3<T, W, VEC, MODE, RB, TT>(a, bf, V, CM, vbase, cbase, i0, i1, h, on, all_on, uns, e);
+        if (i0 < i1) stream_rows3<T, W, VEC, MODE, RB>(a, bf, V, CM, vbase, cbase, i0, i1, h, on, all_on, uns, e);
         flush_flags<T, VEC, MODE>(a, geo.r0, on, uns, e);
         return;
     }
@@ -1052,17 +1022,6 @@ __global__ void k_group_copy(uint32_t *ck, uint32_t *b0, uint32_t *b1, const uin
 }
 
 #endif
-
-// owner-TT prologue: the current buffer's clause products xl xs (k_step's t, :80) for every group
-template <typename T>
-__global__ void k_tt_init(const T *c0, const T *c1, const uint8_t *par, T *tt0, T *tt1, int64_t per_group,
-                          int64_t total) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-        const bool p = par[i / per_group] != 0;
-        const T *cm = p ? c1 : c0;
-        (p ? tt1 : tt0)[i] = cm[2 * i + 1] * cm[2 * i];
-    }
-}
 
 #ifndef ODK_NO_COMMON_KERNELS
 // Per-call bookkeeping of odesat_simulate, queued on the solver's stream (no host round trip):

@@ -37,12 +37,11 @@ using namespace odk;
 struct odesat_solver {
     int device = 0, dtype = ODESAT_F32;
     int64_t n = 0, m = 0, L = 0, B = 0, Bp = 0;
-    int LW = 64, VEC = 1, W = 64, G = 1;
+    int LW = 64, W = 64, G = 1;  // W = LW: one replica per lane
     int chunk_groups = 1;
     int uniform_k = 0;  // every clause has this many literals (0 = mixed widths)
     int schedule = ODESAT_SCHED_AUTO;
     int alg = ODESAT_ALG_FUSED;
-    int rb = 4;  // 3-SAT incidences per batch in k_step (ODESAT_RB: 4 or 8)
     size_t tsize = 4;
     hipStream_t stream = nullptr;
     int32_t *cptr = nullptr, *lits = nullptr, *wpos = nullptr, *vptr = nullptr, *pc = nullptr, *ps = nullptr;
@@ -55,12 +54,10 @@ struct odesat_solver {
     void *w = nullptr;
     void *vh = nullptr, *vf = nullptr, *ch = nullptr, *cf = nullptr;
     void *dtr = nullptr, *err = nullptr;
-    void *tt[2] = {nullptr, nullptr};  // FUSED owner-TT: clause products xl xs [G][m][W], double-buffered (lazy)
-    bool fused_tt = false;             // ODESAT_FUSED_TT=1: FUSED owner-TT (measured 7 % slower on config 4: off)
     // per-call bookkeeping of the persistent kernels (callio.hpp): io_begin -- the next launch starts the
     // call (no k_begin_call); io_mirror -- launches store the results in the pinned host buffers
     bool io_begin = false, io_mirror = false;
-    bool io_fold = true;               // ODESAT_CALL_FOLD=0: k_begin_call and the result copy (A/B)
+    bool check_fault = false;  // this call ran a kernel that may report a fault in stop[1] (k_onchip split barriers)
     uint32_t *unsat = nullptr;
     uint8_t *act = nullptr;
     int64_t *sat_step = nullptr, *steps_done = nullptr;
@@ -94,6 +91,7 @@ struct odesat_solver {
     int32_t *oc_tcp = nullptr;   // [ntp * 8 + 1] wave starts (t * 8 + w) padded with m (static-index loads in k_onchip)
     int64_t oc_rec_bytes = 0;
     bool oc_ada = false;  // ONCHIP also takes adaptive steps (onchip.hpp ADA_*)
+    uint32_t oc_poll_limit = 1u << 22;  // split-barrier polls before a wait gives up (knob ONCHIP_POLL_LIMIT)
     int oc_off = 0;  // pair offset of the wave-paired tiles (pair_tiles): barrier after tile t iff t + off is odd
     bool in_range = true;        // every replica's state is in ONCHIP's range (onchip.hip header)
     int64_t bytes = 0;
@@ -129,13 +127,9 @@ namespace {
 
 template <int V> using IC = std::integral_constant<int, V>;
 
-// Call f(IC<LW>, IC<VEC>) with the solver's compile-time layout.
+// Call f(IC<LW>, IC<1>) with the solver's compile-time layout (one replica per lane: the kernels'
+// VEC template parameter, contiguous replicas per lane, is 1 -- round 2 measured 2 and 4 slower).
 template <typename T, typename F> int with_layout(const odesat_solver *s, F &&f) {
-    if (s->VEC == 4) {
-        if constexpr (sizeof(T) == 4) return f(IC<64>{}, IC<4>{});
-        else return fail(ODESAT_EINVAL, "VEC=4 is f32-only");
-    }
-    if (s->VEC == 2) return f(IC<64>{}, IC<2>{});
     switch (s->LW) {
         case 1: return f(IC<1>{}, IC<1>{});
         case 2: return f(IC<2>{}, IC<1>{});
@@ -235,8 +229,6 @@ template <typename T> KArgs<T> make_args(odesat_solver *s) {
     a.ch = (T *)s->ch;
     a.cf = (T *)s->cf;
     a.dtr = (T *)s->dtr;
-    a.tt0 = (T *)s->tt[0];
-    a.tt1 = (T *)s->tt[1];
     a.err = (typename Bits<T>::U *)s->err;
     a.unsat = s->unsat;
     a.act = s->act;
@@ -293,7 +285,7 @@ template <typename T> unsigned geometry(const odesat_solver *s, KArgs<T> &a, int
 }
 
 template <typename T, int LW, int VEC, int MODE>
-int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which, bool tt = false) {
+int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which) {
     const int64_t items = which == K_CLAUSE ? s->m : s->n;
     const unsigned blocks = geometry<T>(s, a, items, LW);
     if (blocks == 0) return ODESAT_OK;
@@ -301,18 +293,7 @@ int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which, bool tt = false) {
     {
         Timed tm(s, which == K_VARIABLE ? 1 : 0);
         if (which == K_STEP) {
-            if constexpr (LW == 64 && VEC == 1 && MODE == M_FIXED) {
-                if (tt) {  // owner-TT (kernels.hpp stream_rows3): the caller checked the conditions
-                    if (s->rb == 8)
-                        hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 3, 8, true>), grid, block, 0, s->stream, a);
-                    else
-                        hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 3, 4, true>), grid, block, 0, s->stream, a);
-                    goto launched;
-                }
-            }
-            if (s->uniform_k == 3 && s->rb == 8)
-                hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 3, 8>), grid, block, 0, s->stream, a);
-            else if (s->uniform_k == 3)
+            if (s->uniform_k == 3)
                 hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 3, 4>), grid, block, 0, s->stream, a);
             else
                 hipLaunchKernelGGL((k_step<T, LW, VEC, MODE, 0>), grid, block, 0, s->stream, a);
@@ -324,7 +305,6 @@ int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which, bool tt = false) {
         } else {
             hipLaunchKernelGGL((k_variable<T, LW, VEC, MODE>), grid, block, 0, s->stream, a);
         }
-    launched:;
     }
     HIP_TRY(hipGetLastError());
     if (which == K_STEP && s->n_empty > 0) {  // clauses with no literal (no owning variable)
@@ -337,10 +317,9 @@ int launch_kernel(odesat_solver *s, KArgs<T> a, Kern which, bool tt = false) {
     return ODESAT_OK;
 }
 
-// One RHS(+update) of `MODE` for the groups [gA, gB).  tt: FUSED fixed step with owner-TT (the
-// current products are valid: ensure_tt).
+// One RHS(+update) of `MODE` for the groups [gA, gB).
 template <typename T, int LW, int VEC, int MODE>
-int step_groups(odesat_solver *s, int step, T dt, T zeta, int gA, int gB, bool tt = false) {
+int step_groups(odesat_solver *s, int step, T dt, T zeta, int gA, int gB) {
     KArgs<T> a = make_args<T>(s);
     a.step = step;
     a.dt = dt;
@@ -349,7 +328,7 @@ int step_groups(odesat_solver *s, int step, T dt, T zeta, int gA, int gB, bool t
     if (s->alg != ODESAT_ALG_TWOPASS) {  // FUSED (RESIDENT's single steps too)
         a.g0 = gA;
         a.ng = gB - gA;
-        return launch_kernel<T, LW, VEC, MODE>(s, a, K_STEP, tt);
+        return launch_kernel<T, LW, VEC, MODE>(s, a, K_STEP);
     }
     for (int g0 = gA; g0 < gB; g0 += s->chunk_groups) {  // TWOPASS: one contribution buffer per chunk
         a.g0 = g0;
@@ -393,11 +372,11 @@ int launch_status(odesat_solver *s, int step, int stop_mode, bool adaptive, doub
 // One full euler step (fixed or adaptive) for the replica groups [gA, gB), enqueued on the stream.
 template <typename T>
 int enqueue_step(odesat_solver *s, int step, bool adaptive, double dt, double zeta, double tol, int stop_mode,
-                 int gA, int gB, bool tt = false) {
+                 int gA, int gB) {
     int rc = with_layout<T>(s, [&](auto lw, auto vec) -> int {
         constexpr int LW = decltype(lw)::value, VEC = decltype(vec)::value;
         int r;
-        if (!adaptive) return step_groups<T, LW, VEC, M_FIXED>(s, step, (T)dt, (T)zeta, gA, gB, tt);
+        if (!adaptive) return step_groups<T, LW, VEC, M_FIXED>(s, step, (T)dt, (T)zeta, gA, gB);
         const int span = s->alg == ODESAT_ALG_TWOPASS ? s->chunk_groups : gB - gA;
         for (int g0 = gA; g0 < gB; g0 += span) {  // both half steps of one contribution-buffer chunk
             const int g1 = std::min(gB, g0 + span);
@@ -411,9 +390,9 @@ int enqueue_step(odesat_solver *s, int step, bool adaptive, double dt, double ze
 }
 
 int dispatch_step(odesat_solver *s, int step, bool adaptive, double dt, double zeta, double tol, int stop_mode,
-                  int gA, int gB, bool tt = false) {
-    return s->dtype == ODESAT_F64 ? enqueue_step<double>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB, tt)
-                                  : enqueue_step<float>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB, tt);
+                  int gA, int gB) {
+    return s->dtype == ODESAT_F64 ? enqueue_step<double>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB)
+                                  : enqueue_step<float>(s, step, adaptive, dt, zeta, tol, stop_mode, gA, gB);
 }
 
 // The CallIO of the next persistent launch: `begin` for the first launch of a folded call only.
@@ -428,32 +407,6 @@ CallIO take_io(odesat_solver *s) {
         io.h_dt = s->h_dt;
     }
     return io;
-}
-
-// FUSED owner-TT (kernels.hpp stream_rows3) applies to fixed steps of the 3-SAT incidence stream
-// (64 replicas per group, one per lane) on in-range states with a finite zeta and a finite, normal
-// dt -- where the rigidity term is +-0 (onchip.hip's header).
-bool tt_layout(const odesat_solver *s) {
-    return s->fused_tt && s->alg == ODESAT_ALG_FUSED && s->uniform_k == 3 && s->LW == 64 && s->VEC == 1;
-}
-
-// The clause products of the groups' current buffers (once per call that steps with owner-TT).
-int ensure_tt(odesat_solver *s) {
-    int rc;
-    const size_t elems = state_elems(s, s->m);
-    if (!s->tt[0] && ((rc = dmalloc(s, &s->tt[0], elems * s->tsize)) || (rc = dmalloc(s, &s->tt[1], elems * s->tsize))))
-        return rc;
-    const int64_t per_group = s->m * (int64_t)s->W, total = per_group * s->G;
-    const int threads = 256;
-    const unsigned blocks = (unsigned)std::min<int64_t>((total + threads - 1) / threads, 65536);
-    if (s->dtype == ODESAT_F64)
-        hipLaunchKernelGGL(k_tt_init<double>, dim3(blocks), dim3(threads), 0, s->stream, (const double *)s->c[0],
-                           (const double *)s->c[1], s->par, (double *)s->tt[0], (double *)s->tt[1], per_group, total);
-    else
-        hipLaunchKernelGGL(k_tt_init<float>, dim3(blocks), dim3(threads), 0, s->stream, (const float *)s->c[0],
-                           (const float *)s->c[1], s->par, (float *)s->tt[0], (float *)s->tt[1], per_group, total);
-    HIP_TRY(hipGetLastError());
-    return ODESAT_OK;
 }
 
 // ---- RESIDENT ---------------------------------------------------------------------------------
@@ -581,7 +534,7 @@ int64_t tile_count(const odesat_cnf *f, int64_t n, int cap) {
 // Instances whose tiles are at least half full keep R = 1 (ONCHIP / RESIDENT at one replica).
 int small_instance_width(const odesat_cnf *f, int64_t n, int64_t batch, int device, size_t tsize) {
     const int64_t m = f->nclauses();
-    if (m == 0 || std::getenv("ODESAT_GROUP_WIDTH")) return 1;
+    if (m == 0 || odesat::xp_isset("GROUP_WIDTH")) return 1;
     const int64_t nt = tile_count(f, n, ResShape<1>::NL);
     if (2 * m >= nt * (int64_t)ResShape<1>::NL) return 1;
     int cus = 256;
@@ -672,8 +625,8 @@ bool build_tiles(const odesat_cnf *f, int64_t n, int cap, int R, bool k3, bool p
         pair_tiles(f, n, 0, tile_of, wave_of, fill);
         pair_tiles(f, n, 1, t1, w1, f1);
         pair_off = f1.size() < fill.size() ? 1 : 0;
-        if (const char *ev = std::getenv("ODESAT_PAIR_OFF"))  // tests: force the offset
-            if (std::atoi(ev) == 0 || std::atoi(ev) == 1) pair_off = std::atoi(ev);
+        const int64_t want = odesat::xp_get("PAIR_OFF", -1);  // tests: force the offset
+        if (want == 0 || want == 1) pair_off = (int)want;
         if (pair_off) {
             tile_of.swap(t1);
             wave_of.swap(w1);
@@ -737,8 +690,7 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
                  const std::vector<int32_t> &lits) {
     if (s->res_R != 1 || s->res_narrow || s->res_wave || s->dtype != ODESAT_F32 || s->uniform_k != 3 || s->n > onchip::MAX_N)
         return ODESAT_OK;
-    if (const char *ev = std::getenv("ODESAT_ONCHIP"))
-        if (std::atoi(ev) == 0) return ODESAT_OK;
+    if (odesat::xp_get("ONCHIP", 1) == 0) return ODESAT_OK;
     const int nt = (int)tiles.size() - 1;
     if (nt == 0 || s->m == 0 || wst.empty()) return ODESAT_OK;  // k_onchip runs wave-paired tiles only
     for (int64_t k = 0; k < s->m; ++k) {  // three distinct variables per clause (independent dv updates)
@@ -799,7 +751,8 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
     // adaptive steps on chip: four voltage arrays in LDS, every tile in VGPRs; the first step of a
     // call on a caller-supplied state runs k_resident's adaptive step (res_ada)
     s->oc_ada = s->oc_tl == 0 && s->n <= onchip::ADA_MAX_N && s->res_ada;
-    if (const char *ev = std::getenv("ODESAT_ONCHIP_ADAPTIVE")) s->oc_ada = s->oc_ada && std::atoi(ev) != 0;
+    s->oc_ada = s->oc_ada && odesat::xp_get("ONCHIP_ADAPTIVE", 1) != 0;
+    s->oc_poll_limit = (uint32_t)std::min<int64_t>(odesat::xp_get("ONCHIP_POLL_LIMIT", 1 << 22), 1 << 22);
     return ODESAT_OK;
 }
 
@@ -1040,11 +993,13 @@ int launch_onchip(odesat_solver *s, int step0, int nsteps, double dt, double zet
     a.dt = (float)dt;
     a.xl_max = 1e4f * (float)s->m;  // system.rs:95, as (T)1e4 * (T)m
     a.io = take_io(s);
+    a.poll_limit = s->oc_poll_limit;
     {
         Timed tm(s, 0);
         const size_t lds = adaptive ? onchip::LDS_MAX : onchip::lds_bytes(s->n, s->oc_tl);
         HIP_TRY(onchip::launch(s->oc_tr, s->oc_off, a, s->G, lds, s->stream, adaptive));
     }
+    s->check_fault = s->check_fault || onchip::split_barriers(adaptive);
     return ODESAT_OK;
 }
 
@@ -1249,8 +1204,6 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     void *snaps[] = {s->snap_par, s->snap_sat, s->snap_done, s->snap_dt, s->ck_v, s->ck_c, s->ck_dt, s->ck_par,
                      s->ck_act, s->ck_sat, s->ck_done, s->ck_stop};
     for (void *p : snaps) dfree(p);
-    dfree(s->tt[0]);
-    dfree(s->tt[1]);
     void *pinned[] = {s->h_sat, s->h_dt, s->h_stop, s->h_act};  // (h_done lies inside h_sat's block)
     for (void *p : pinned)
         if (p) (void)hipHostFree(p);
@@ -1304,11 +1257,11 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     // ODESAT_GROUP_WIDTH overrides (tuning; RESIDENT only if that width admits it).
     int lw = 1, res_r = 0;
     // k_wave (wave.hpp) for small 3-SAT instances whose replica -- with the adaptive clones --
-    // fits in 64 KiB of LDS (two or more waves per CU); ODESAT_WAVE=0/1 overrides, an explicit
-    // ODESAT_GROUP_WIDTH selects the tile kernels
+    // fits in 64 KiB of LDS (two or more waves per CU); the WAVE knob (0/1) overrides, a set
+    // GROUP_WIDTH selects the tile kernels (odesat_set_experiment)
     // (its clause records pack a literal and a term position in 16 bits each)
-    if (s->uniform_k == 3 && m > 0 && !std::getenv("ODESAT_GROUP_WIDTH") && 2 * n + 1 < (1 << 16) && L < (1 << 16)) {
-        const char *ev = std::getenv("ODESAT_WAVE");
+    if (s->uniform_k == 3 && m > 0 && !odesat::xp_isset("GROUP_WIDTH") && 2 * n + 1 < (1 << 16) && L < (1 << 16)) {
+        const int64_t ev = odesat::xp_get("WAVE", -1);
         const size_t topo = wave_topo_bytes(n, m), rep = wave_lds_bytes(n, m, L, s->tsize, true);
         s->wv_wpw = topo + 4 * rep <= RES_LDS_MAX ? 4 : (topo + 2 * rep <= RES_LDS_MAX ? 2 : 1);
         // ... and no more than leaves every CU a workgroup: a small batch spreads over the chip one
@@ -1319,7 +1272,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
                 cus = 256;
             while (s->wv_wpw > 1 && (batch + s->wv_wpw - 1) / s->wv_wpw < cus) s->wv_wpw /= 2;
         }
-        s->res_wave = ev ? (std::atoi(ev) != 0 && topo + rep <= RES_LDS_MAX) : topo + 2 * rep <= RES_LDS_MAX;
+        s->res_wave = ev >= 0 ? (ev != 0 && topo + rep <= RES_LDS_MAX) : topo + 2 * rep <= RES_LDS_MAX;
         // waves per replica: LDS holds one workgroup (wv_wpw replicas) per CU, so a replica of one
         // wave leaves a lone wave on each SIMD, which issues a VALU instruction every 4 cycles.  A
         // team of TW waves splits the replica's clauses and variables over 64 TW lanes: the workgroup
@@ -1333,9 +1286,9 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         // twice as many (config 3, B = 256, one replica per workgroup: adaptive 42.4 M replica-steps/s
         // at TW = 4 vs 35.7 M at 16; fixed 80.2 M at 4 vs 91.7 M at 16)
         s->wv_tw_ada = std::min(s->wv_tw, 4);
-        if (const char *et = std::getenv("ODESAT_WAVE_TEAM")) {
-            const int t = std::atoi(et);
-            if ((t == 1 || t == 2 || t == 4 || t == 8 || t == 16) && t * s->wv_wpw <= 16) s->wv_tw = s->wv_tw_ada = t;
+        {
+            const int64_t t = odesat::xp_get("WAVE_TEAM", -1);
+            if ((t == 1 || t == 2 || t == 4 || t == 8 || t == 16) && t * s->wv_wpw <= 16) s->wv_tw = s->wv_tw_ada = (int)t;
         }
     }
     if (s->res_wave) {
@@ -1345,8 +1298,8 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     } else {
         while (lw < batch && lw < 64) lw <<= 1;
     }
-    if (const char *ev = std::getenv("ODESAT_GROUP_WIDTH")) {
-        const int want = std::atoi(ev);
+    if (odesat::xp_isset("GROUP_WIDTH")) {
+        const int want = (int)odesat::xp_get("GROUP_WIDTH", 0);
         if (want == 1 || want == 2 || want == 4 || want == 8 || want == 16 || want == 32 || want == 64) {
             lw = want;
             res_r = (want <= 32 && res_fits(n, want, s->tsize, false)) ? want : 0;
@@ -1355,21 +1308,20 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     // One replica per wave (RES_NARROW) when the tile chain is deep and narrow: 64-clause tiles
     // then need barely more tiles than 512-clause ones, and a replica's step costs one wave instead
     // of eight (hard.cnf at B = 1: a step is a chain of ~20 tiles of ~8 clauses).
-    // ODESAT_RES_NARROW=0/1 overrides.
+    // The RES_NARROW knob (0/1) overrides.
     if (res_r == 1 && m > 0 && !s->res_wave) {
-        const char *ev = std::getenv("ODESAT_RES_NARROW");
-        if (ev) s->res_narrow = std::atoi(ev) != 0;
+        const int64_t ev = odesat::xp_get("RES_NARROW", -1);
+        if (ev >= 0) s->res_narrow = ev != 0;
         else s->res_narrow = 4 * tile_count(f, n, RES_NARROW) <= 5 * tile_count(f, n, ResShape<1>::NL);
     }
     // the internal clause order: var-disjoint tiles for RESIDENT, else the file order
     std::vector<int32_t> perm, tiles, wst;
     std::vector<uint8_t> lorder;  // per internal clause: literal order code (kP3), 0 = file order
     // wave-paired tiles where ONCHIP may run (onchip_setup's conditions; k_onchip needs them);
-    // ODESAT_ONCHIP_PAIRS=0: plain tiles (RESIDENT)
+    // the ONCHIP_PAIRS knob = 0: plain tiles (RESIDENT)
     bool pairs = res_r == 1 && !s->res_narrow && !s->res_wave && s->dtype == ODESAT_F32 && s->uniform_k == 3 &&
                  n <= onchip::MAX_N;
-    if (const char *ev = std::getenv("ODESAT_ONCHIP")) pairs = pairs && std::atoi(ev) != 0;
-    if (const char *ev = std::getenv("ODESAT_ONCHIP_PAIRS")) pairs = pairs && std::atoi(ev) != 0;
+    pairs = pairs && odesat::xp_get("ONCHIP", 1) != 0 && odesat::xp_get("ONCHIP_PAIRS", 1) != 0;
     const int cap = s->res_narrow ? RES_NARROW : res_capacity(res_r);
     if (s->res_wave) {  // no tiles: the file order, one pseudo-tile
         perm.resize(m);
@@ -1380,7 +1332,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         res_r = 0;
     }
     if (res_r != 1) s->res_narrow = false;
-    if (res_r == 0 && !std::getenv("ODESAT_GROUP_WIDTH")) {
+    if (res_r == 0 && !odesat::xp_isset("GROUP_WIDTH")) {
         lw = 1;
         while (lw < batch && lw < 64) lw <<= 1;
     }
@@ -1390,15 +1342,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         lorder.assign(m, 0);
     }
     s->LW = lw;
-    s->VEC = 1;
-    // ODESAT_VEC=2/4 (tuning, FUSED / TWOPASS at LW = 64): contiguous replicas per lane, W = 64 VEC
-    if (const char *ev = std::getenv("ODESAT_VEC"))
-        if (res_r == 0 && lw == 64 && (std::atoi(ev) == 2 || (std::atoi(ev) == 4 && s->dtype == ODESAT_F32)))
-            s->VEC = std::atoi(ev);
-    if (const char *ev = std::getenv("ODESAT_RB")) s->rb = std::atoi(ev) == 8 ? 8 : 4;
-    if (const char *ev = std::getenv("ODESAT_FUSED_TT")) s->fused_tt = std::atoi(ev) != 0;
-    if (const char *ev = std::getenv("ODESAT_CALL_FOLD")) s->io_fold = std::atoi(ev) != 0;
-    s->W = s->LW * s->VEC;
+    s->W = s->LW;
     s->Bp = (batch + s->W - 1) / s->W * s->W;
     s->G = (int)(s->Bp / s->W);
     pick_chunk(s, 0);
@@ -1488,14 +1432,13 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
         s->res_R = res_r;
         s->res_ada = res_fits(n, res_r, s->tsize, true);
-        if (const char *ev = std::getenv("ODESAT_RES_FAST")) s->res_fast = std::atoi(ev) != 0;
-        if (const char *ev = std::getenv("ODESAT_RES_RC")) s->res_rc = std::atoi(ev) != 0;
+        s->res_fast = odesat::xp_get("RES_FAST", 1) != 0;
+        s->res_rc = odesat::xp_get("RES_RC", 1) != 0;
         // adaptive steps whose clone of v does not fit beside v and dv (f64 at n > 6.7 k, the CLI's
         // default precision and mode on config 2): k_resident with the clone in HBM instead of FUSED
-        // on the one-replica layout.  ODESAT_RES_VFG=0 keeps FUSED.
+        // on the one-replica layout.  The RES_VFG knob = 0 keeps FUSED.
         if (!s->res_ada && res_r == 1 && !s->res_wave) {
-            s->res_vfg = true;
-            if (const char *ev = std::getenv("ODESAT_RES_VFG")) s->res_vfg = std::atoi(ev) != 0;
+            s->res_vfg = odesat::xp_get("RES_VFG", 1) != 0;
             s->res_ada = s->res_vfg;
         }
         s->res_ntiles = (int)tiles.size() - 1;
@@ -1526,23 +1469,23 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             // best team, at 1024 no faster and slower in f64 adaptive steps; round 4,
             // profiles/r04ae_solo_lanes.txt: hard.cnf (m = 160) f64 criterion calls 4.64-4.66 / 12.23-12.24
             // ms fixed / adaptive at 192 lanes against 4.85-4.93 / 12.54-12.57 at 256 and 5.6 / 13.4 at 128).
-            // ODESAT_SOLO=0/1 and ODESAT_SOLO_LANES override.
+            // The SOLO (0/1) and SOLO_LANES knobs override.
             int64_t nl = std::min<int64_t>(512, std::max<int64_t>(192, (m + 63) / 64 * 64));
-            if (const char *ev = std::getenv("ODESAT_SOLO_LANES")) {
-                const int64_t want = std::atoll(ev);
+            {
+                const int64_t want = odesat::xp_get("SOLO_LANES", -1);
                 if (want >= 64 && want <= SOLO_MAX_NL && want % 64 == 0) nl = want;
             }
             const int64_t cpl = (m + nl - 1) / nl, vpl = (n + nl - 1) / nl;
             const bool fits = cpl <= 4 && vpl <= 2 && (size_t)(n + L) * s->tsize <= RES_LDS_MAX;
             s->solo = fits && s->wv_wpw == 1;
-            if (const char *ev = std::getenv("ODESAT_SOLO")) s->solo = fits && std::atoi(ev) != 0;
+            if (odesat::xp_isset("SOLO")) s->solo = fits && odesat::xp_get("SOLO", 0) != 0;
             s->solo_nl = (int)nl;
             s->solo_cpl = cpl <= 1 ? 1 : (cpl <= 2 ? 2 : 4);
             s->solo_vpl = (int)vpl;
             // k_solo_fast's padded term blocks must fit as well
             s->solo_fast = solo_fast_elems(n, L, s->tsize) * s->tsize <= RES_LDS_MAX;
-            if (const char *ev = std::getenv("ODESAT_SOLO_FAST")) s->solo_fast = s->solo_fast && std::atoi(ev) != 0;
-            if (const char *ev = std::getenv("ODESAT_WAVE_FAST")) s->wave_fast = std::atoi(ev) != 0;
+            s->solo_fast = s->solo_fast && odesat::xp_get("SOLO_FAST", 1) != 0;
+            s->wave_fast = odesat::xp_get("WAVE_FAST", 1) != 0;
         }
         if ((rc = onchip_setup(s, tiles, wst, lits))) return bail(rc);
         if (s->oc_tr > 0) s->alg = ODESAT_ALG_ONCHIP;
@@ -1561,6 +1504,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     if ((rc = dmalloc(s, (void **)&s->sat_step, 2 * s->Bp * 8))) return bail(rc);
     s->steps_done = s->sat_step + s->Bp;
     if ((rc = dmalloc(s, (void **)&s->stop, 16))) return bail(rc);
+    if (hipMemset(s->stop, 0, 16) != hipSuccess) return bail(fail(ODESAT_EDEVICE, "memset failed"));  // stop[1]: fault word
     if (hipHostMalloc((void **)&s->h_sat, 2 * s->Bp * 8) != hipSuccess ||
         hipHostMalloc((void **)&s->h_dt, s->Bp * 8) != hipSuccess ||
         hipHostMalloc((void **)&s->h_stop, 16) != hipSuccess || hipHostMalloc((void **)&s->h_act, s->Bp) != hipSuccess)
@@ -1781,8 +1725,18 @@ static int finish_simulate(odesat_solver *s, const odesat_params *p, bool adapti
         if (dt_out && adaptive)
             HIP_TRY(hipMemcpyAsync(s->h_dt, s->dtr, s->B * s->tsize, hipMemcpyDeviceToHost, s->stream));
     }
-    if (p->stop == ODESAT_STOP_ANY) HIP_TRY(hipMemcpyAsync(s->h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream));
+    // the stop word (STOP_ANY) and the fault word beside it (a k_onchip split-barrier wait that gave up)
+    const bool fault_check = s->check_fault;
+    s->check_fault = false;
+    if (p->stop == ODESAT_STOP_ANY || fault_check)
+        HIP_TRY(hipMemcpyAsync(s->h_stop, s->stop, 8, hipMemcpyDeviceToHost, s->stream));
     HIP_TRY(hipStreamSynchronize(s->stream));
+    if (fault_check && s->h_stop[1] != 0) {
+        HIP_TRY(hipMemsetAsync(s->stop + 1, 0, 4, s->stream));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        return fail(ODESAT_EDEVICE, "k_onchip: a split-barrier wait timed out; the launch's dv updates may have "
+                                    "raced, so its results are not returned (re-run the call)");
+    }
     // simulate_inter runs T + 1 steps when step T is the first allsat one (system.rs:291): launches
     // after it were no-ops
     if (p->stop == ODESAT_STOP_ANY && *s->h_stop != INT_MAX)
@@ -1926,7 +1880,7 @@ static int simulate_impl(odesat_solver *s, const odesat_params *p, bool cont, in
     const bool persistent = (s->alg == ODESAT_ALG_ONCHIP && (!adaptive || s->oc_ada)) ||
                             ((s->alg == ODESAT_ALG_RESIDENT || s->alg == ODESAT_ALG_ONCHIP) && (!adaptive || s->res_ada));
     s->io_begin = s->io_mirror = false;
-    if (!cont && persistent && s->io_fold && p->stop != ODESAT_STOP_ANY) {
+    if (!cont && persistent && p->stop != ODESAT_STOP_ANY) {
         s->t_base = 0;
         s->io_begin = true;
         s->io_mirror = p->stop == ODESAT_STOP_NONE;
@@ -1961,21 +1915,12 @@ static int simulate_impl(odesat_solver *s, const odesat_params *p, bool cont, in
     const int span = chunk_major ? chunk : s->G;
     const int64_t base = s->t_base;
     int64_t t_run = 0;
-    const double adt = std::fabs(p->dt);
-    const bool use_tt = !adaptive && tt_layout(s) && std::fabs(zeta) <= 1e6 && adt >= 1e-30 && adt <= 1e30;
     for (int gA = 0; gA < s->G; gA += span) {
         const int gB = std::min(s->G, gA + span);
         const int64_t r0 = (int64_t)gA * s->W, r1 = std::min<int64_t>((int64_t)gB * s->W, s->B);
         int64_t t = 0;
-        bool tt_ready = false;
         for (; t < p->max_steps; ++t) {
-            // owner-TT from the first step whose state is in range (after one clamped step at the latest)
-            const bool tt = use_tt && (t > 0 || s->in_range);
-            if (tt && !tt_ready) {
-                if ((rc = ensure_tt(s))) return rc;
-                tt_ready = true;
-            }
-            if ((rc = dispatch_step(s, (int)(base + t), adaptive, p->dt, zeta, tol, p->stop, gA, gB, tt))) return rc;
+            if ((rc = dispatch_step(s, (int)(base + t), adaptive, p->dt, zeta, tol, p->stop, gA, gB))) return rc;
             if (p->stop != ODESAT_STOP_NONE && (t + 1) % poll == 0 && t + 1 < p->max_steps) {
                 // poll the stop condition (results are exact regardless: later launches are no-ops)
                 HIP_TRY(hipMemcpyAsync(s->h_stop, s->stop, 4, hipMemcpyDeviceToHost, s->stream));

@@ -260,9 +260,12 @@ __device__ __forceinline__ void pair_signal(uint32_t cnt, uint32_t ep) {
 }
 // The poll is one inline-assembly loop, invisible to the compiler's control flow: a loop in the
 // unrolled tile sequence cost it 40-65 spilled VGPRs.  (All 64 lanes are active here.)  It gives up
-// after 2^22 polls (~0.1 s), so a broken count can never hang the GPU (the results would then be
-// wrong, which the parity tests see).
-__device__ __forceinline__ void pair_wait(uint32_t cnt, uint32_t target) {
+// after `limit` polls (2^22, ~0.1 s; the experiment knob ONCHIP_POLL_LIMIT lowers it for the test of
+// this path), so a broken count can never hang the GPU.  Giving up stores a nonzero word in the fault
+// slots after the counters (the lane's counter address + 32: no register beyond the loop's own),
+// which the kernel reports to the host at its end: the call then fails instead of returning results
+// that raced.
+__device__ __forceinline__ void pair_wait(uint32_t cnt, uint32_t target, uint32_t limit) {
     __builtin_amdgcn_sched_barrier(0);
     const uint32_t addr = cnt + 4u * (threadIdx.x & 7);
     uint32_t tmp, it;
@@ -276,15 +279,22 @@ __device__ __forceinline__ void pair_wait(uint32_t cnt, uint32_t target) {
         "s_cmp_eq_u64 %1, exec\n\t"
         "s_cbranch_scc1 L_pd%=\n\t"
         "s_add_u32 %2, %2, 1\n\t"
-        "s_cmp_gt_u32 %2, 0x400000\n\t"
-        "s_cbranch_scc1 L_pd%=\n\t"
+        "s_cmp_gt_u32 %2, %5\n\t"
+        "s_cbranch_scc1 L_pt%=\n\t"
 #if ONCHIP_POLL_SLEEP > 0
         "s_sleep " POLL_STR(ONCHIP_POLL_SLEEP) "\n\t"
 #endif
         "s_branch L_pw%=\n"
+        "L_pt%=:\n\t"
+        "v_mov_b32 %0, 1\n\t"
+        "ds_write_b32 %3, %0 offset:32\n"
         "L_pd%=:"
         : "=&v"(tmp), "=&s"(msk), "=&s"(it)
-        : "v"(addr), "s"(target)
+#ifdef ONCHIP_POLL_CONST  // A/B: the limit as an immediate (one SGPR less in the adaptive kernel)
+        : "v"(addr), "s"(target), "i"(0x400000)
+#else
+        : "v"(addr), "s"(target), "s"(limit)
+#endif
         : "memory", "scc");
     __builtin_amdgcn_sched_barrier(0);
 }
@@ -301,7 +311,7 @@ template <bool SPL = false>
 __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, SlotF &slot3, float2 &mem1, Pend &P, Front &Fn,
                                           Gath &Gn, int t, float h, float hh, uint32_t &cmax, Stamps &S, bool bar,
                                           bool first = false, uint32_t cnt = 0, uint32_t *ep = nullptr) {
-    if (SPL && first) pair_wait(cnt, *ep);  // every wave's dv writes of the previous pair are performed
+    if (SPL && first) pair_wait(cnt, *ep, a.poll_limit);  // every wave's dv writes of the previous pair are performed
     const float o0 = lds_f(P.a0 + DVC), o1 = lds_f(P.a1 + DVC), o2 = lds_f(P.a2 + DVC);
     lds_st(P.a0 + DVC, o0 + P.d0);
     lds_st(P.a1 + DVC, o1 + P.d1);
@@ -521,7 +531,7 @@ __device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &s
                                            bool p2, uint32_t &cmax, float &e, bool bar, bool first, uint32_t cnt,
                                            uint32_t &ep) {
     constexpr bool SPL = (ONCHIP_SPLITBAR & 2) != 0;
-    if (SPL && first) pair_wait(cnt, ep);  // (split barriers: see tile_step)
+    if (SPL && first) pair_wait(cnt, ep, a.poll_limit);  // (split barriers: see tile_step)
     const float o0 = lds_f(P.a0 + ADA_D), o1 = lds_f(P.a1 + ADA_D), o2 = lds_f(P.a2 + ADA_D);
     lds_st(P.a0 + ADA_D, o0 + P.d0);
     lds_st(P.a1 + ADA_D, o1 + P.d1);
@@ -765,7 +775,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     // the waves' pair counts (split barriers): after the unsat flags (adaptive: and the error words)
     const uint32_t CNT = UNS + 8u + (ADA ? 4u * WAVES : 0u);
     if (lane < 2) lds_st(UNS + 4u * lane, 0.0f);
-    if ((ONCHIP_SPLITBAR & (ADA ? 2 : 1)) && lane < WAVES) lds_st(CNT + 4u * lane, 0.0f);
+    if ((ONCHIP_SPLITBAR & (ADA ? 2 : 1)) && lane < 2 * WAVES) lds_st(CNT + 4u * lane, 0.0f);  // + the fault slots
     __syncthreads();
     ONCHIP_PHASE(1);
     uint32_t ep = 0u;  // the pairs every wave has signalled so far
@@ -932,6 +942,11 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     }
 #endif
     ONCHIP_PHASE(3);
+    // a split-barrier wait that gave up (EP_TIMEOUT): the dv updates may have raced, so the call must
+    // fail -- the fault word beside the stop word, read by the host after the call (ODESAT_EDEVICE)
+    // (the fault slots after the pair counts; every wave's store to them precedes the steps' last barrier)
+    if ((ONCHIP_SPLITBAR & (ADA ? 2 : 1)) && lane < WAVES && lds_f(CNT + 4u * (WAVES + lane)) != 0.0f)
+        atomicOr(reinterpret_cast<unsigned *>(a.stop + 1), 1u);
     if (lane == 0) {
         if (a.oop) a.par[g] = (uint8_t)q;
         a.act[g] = (uint8_t)act;
@@ -941,6 +956,12 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
         io_mirror<float>(a.io, g, sat, done, dtr, ADA);
     }
 }
+
+}  // namespace
+
+bool split_barriers(bool adaptive) { return (ONCHIP_SPLITBAR & (adaptive ? 2 : 1)) != 0; }
+
+namespace {
 
 template <int TR, int OFF, bool ADA> hipError_t launch_t(const Args &a, int G, size_t lds, hipStream_t stream) {
     hipError_t e = odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_onchip<TR, OFF, ADA>), (int)LDS_MAX);

@@ -37,7 +37,7 @@ inline Lds lds_map(int64_t n) {
     const uint32_t vend = (uint32_t)(4 * (n + SINKS));
     L.gap_base = (vend + 7u) & ~7u;
     L.gap_tiles = L.gap_base < DVC ? (DVC - L.gap_base) / TILE_LDS : 0;
-    L.after_base = ((DVC + vend + 8u + 4u * WAVES) + 7u) & ~7u;  // after dv: two unsat flags, the waves' pair counts
+    L.after_base = ((DVC + vend + 8u + 8u * WAVES) + 7u) & ~7u;  // after dv: two unsat flags, the waves' pair counts, the fault slots
     L.after_tiles = L.after_base < LDS_MAX ? (uint32_t)((LDS_MAX - L.after_base) / TILE_LDS) : 0;
     return L;
 }
@@ -56,7 +56,7 @@ inline int tl_max(int64_t n) {
 // the ds instructions' 16-bit immediate of A, as DVC), H = the half step, F = the full-step clone,
 // n + SINKS floats each; A's region also holds the unsat flags and the waves' error words.
 constexpr uint32_t ADA_D = 40960, ADA_H = 81920, ADA_F = 122880;
-constexpr int ADA_FLAGS = 2 + 2 * WAVES;  // two unsat flags, the waves' error words, their pair counts
+constexpr int ADA_FLAGS = 2 + 3 * WAVES;  // two unsat flags, the waves' error words, their pair counts, the fault slots
 constexpr int ADA_MAX_N = (int)(ADA_D / 4) - SINKS - ADA_FLAGS;
 
 struct Args {
@@ -81,6 +81,7 @@ struct Args {
     float *dtr;          // [B] per-replica adaptive dt (adaptive launches)
     float tol;           // adaptive tolerance, as the solver's f32
     CallIO io;           // per-call bookkeeping (callio.hpp)
+    uint32_t poll_limit; // split-barrier polls before a wait gives up and reports the fault (onchip.hip)
 };
 
 // Register-tile counts compiled (template instantiations; VGPRs ~ 50 + 2 TR, ~245 at TR = 96).
@@ -119,5 +120,8 @@ inline void make_rec12(uint32_t a0, uint32_t a1, uint32_t a2, bool n0, bool n1, 
 // of the wave-paired tiles (a barrier after tile t iff t + off is odd).  adaptive: euler_step with
 // per-replica dt (a.dtr, a.tol); needs a.tl == 0 and n <= ADA_MAX_N, and LDS_MAX bytes of LDS.
 hipError_t launch(int tr, int off, const Args &a, int G, size_t lds, hipStream_t stream, bool adaptive = false);
+// The launch's kernel may wait on split barriers (ONCHIP_SPLITBAR, onchip.hip), whose bounded wait
+// reports a timeout in the fault word stop[1]: the host then checks that word after the call.
+bool split_barriers(bool adaptive);
 
 }  // namespace onchip

@@ -404,14 +404,13 @@ extern "C" int odesat_part_create(int device, int world, int64_t n, int64_t m, i
     for (int64_t k = 0; k < nv; ++k)
         for (int64_t j = 0; j < deg[k]; ++j) ell[cstart[k / 64] + 64 * j + (k % 64)] = inc_slot[var_ptr[k] + j];
     p->voff = block > 0 && v1 - v0 <= block ? v0 / block : 0;
-    // term layout: REGION (default), ELL or SLOT (ODESAT_PART_TERMS=region|ell|slot)
-    p->terms = TERMS_REGION;
-    if (const char *tl = std::getenv("ODESAT_PART_TERMS")) {
-        const std::string t(tl);
-        p->terms = t == "slot" ? TERMS_SLOT : (t == "ell" ? TERMS_ELL : TERMS_REGION);
+    // term layout: REGION (default), ELL or SLOT (experiment knob PART_TERMS = 0 / 1 / 2)
+    {
+        const int64_t t = odesat::xp_get("PART_TERMS", 0);
+        p->terms = t == 2 ? TERMS_SLOT : (t == 1 ? TERMS_ELL : TERMS_REGION);
     }
     p->regions = 16;
-    if (const char *rg = std::getenv("ODESAT_PART_REGIONS")) p->regions = std::max(8, std::atoi(rg) / 8 * 8);
+    if (odesat::xp_isset("PART_REGIONS")) p->regions = std::max(8, (int)odesat::xp_get("PART_REGIONS", 16) / 8 * 8);
     const int64_t ell_words = cstart[nchunk];
     // w's size: SLOT L words, ELL the padded sliced-ELL, REGION the in-range incidences; + 64 sink words
     const int64_t ninc_all = nv ? var_ptr[nv] : 0;
@@ -454,14 +453,12 @@ extern "C" int odesat_part_create(int device, int world, int64_t n, int64_t m, i
     }
     bool k3 = mloc > 0 && L == 3 * mloc;
     for (int64_t c = 0; c < mloc && k3; ++c) k3 = cp[c] == 3 * c;
-    if (const char *ev = std::getenv("ODESAT_PART_K3"))
-        if (std::atoi(ev) == 0) k3 = false;
-    if (const char *ev = std::getenv("ODESAT_PART_XCD")) p->xcd_ranges = std::atoi(ev) != 0 ? 8 : 0;
+    if (odesat::xp_get("PART_K3", 1) == 0) k3 = false;
+    if (odesat::xp_isset("PART_XCD")) p->xcd_ranges = odesat::xp_get("PART_XCD", 0) != 0 ? 8 : 0;
     if (k3) {  // 3-SAT slice: one literal record per clause, term positions in 3 planes
         bool pack = true;
         for (int64_t q = 0; q < L && pack; ++q) pack = lits[q] < (1 << 21);
-        if (const char *ev = std::getenv("ODESAT_PART_PACK"))
-            if (std::atoi(ev) == 0) pack = false;
+        if (odesat::xp_get("PART_PACK", 1) == 0) pack = false;
         p->lit_packed = pack;
         const size_t rb = pack ? 8 : 16;
         std::vector<uint64_t> l8(pack ? (size_t)mloc : 0);

@@ -40,13 +40,10 @@ void to_replica_major(const float *src, int64_t items, int64_t B, std::vector<do
         for (int64_t b = 0; b < B; ++b) dst[(size_t)(b * items + i)] = (double)src[i * B + b];
 }
 
-// steps per bounded call of an unbounded run (ODESAT_RUN_CHUNK overrides: tests force several calls)
+// steps per bounded call of an unbounded run (the RUN_CHUNK knob overrides: tests force several calls)
 int64_t chunk_steps() {
-    if (const char *ev = std::getenv("ODESAT_RUN_CHUNK")) {
-        const long long c = std::atoll(ev);
-        if (c > 0) return (int64_t)c;
-    }
-    return (int64_t)1 << 16;
+    const int64_t c = odesat::xp_get("RUN_CHUNK", 0);
+    return c > 0 ? c : (int64_t)1 << 16;
 }
 
 void to_replica_inner(const std::vector<double> &src, int64_t items, int64_t B, float *dst) {

@@ -378,16 +378,15 @@ size_t round16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // The wave kernel's width: the widest WPW in {8, 4, 2, 1} whose LDS fits and that still gives
 // every CU of the device (`cus`) a workgroup; 0 (3-kernel path) when one replica's state and the
-// topology do not fit.  ODESAT_STOCH_WAVE=0 forces the 3-kernel path, ODESAT_STOCH_WPW=w forces a
-// width that fits.
+// topology do not fit.  The experiment knob STOCH_WAVE = 0 forces the 3-kernel path, STOCH_WPW = w
+// forces a width that fits.
 int stoch_wave_width(int64_t B, size_t topo, size_t rep, int cus) {
-    const char *e = std::getenv("ODESAT_STOCH_WAVE");
-    if (e && e[0] == '0') return 0;
+    if (odesat::xp_get("STOCH_WAVE", 1) == 0) return 0;
     auto fits = [&](int w) { return topo + (size_t)w * rep <= STOCH_LDS_MAX; };
     if (!fits(1)) return 0;
-    if (const char *f = std::getenv("ODESAT_STOCH_WPW")) {
-        const int w = std::atoi(f);
-        if ((w == 1 || w == 2 || w == 4 || w == 8) && fits(w)) return w;
+    {
+        const int64_t w = odesat::xp_get("STOCH_WPW", -1);
+        if ((w == 1 || w == 2 || w == 4 || w == 8) && fits((int)w)) return (int)w;
     }
     for (int w : {8, 4, 2}) {
         if (fits(w) && (B + w - 1) / w >= cus) return w;

@@ -19,6 +19,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import tooling  # noqa: E402  (XP_LIB / XP_KNOBS: a variant build and experiment knobs)
+tooling.apply()
 
 SPEC = {
     "config3": dict(adaptive=True, batch=1024, cpu_replicas=8, cpu_steps=400),
@@ -77,7 +79,7 @@ def main():
         out = {"config": cfg, "workload": f"random 3-SAT n={n} m={m} seed={c['seed']}, "
                                           f"{'adaptive tol 1e-3' if spec['adaptive'] else 'fixed dt 0.01'}",
                "batch": B, "steps": args.steps, "algorithm": alg, "chunk": args.chunk, "schedule": args.schedule,
-               "env": {k: v for k, v in os.environ.items() if k.startswith("ODESAT_")},
+               "experiment": tooling.knobs(),
                "steps_per_s": args.steps / wall, "replica_steps_per_s": B * args.steps / wall,
                "ms_per_step": wall * 1e3 / args.steps,
                "algorithmic_bytes_per_replica_step": per_rs,

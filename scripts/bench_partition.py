@@ -17,6 +17,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import tooling  # noqa: E402  (XP_LIB / XP_KNOBS: a variant build and experiment knobs)
+tooling.apply()
 
 
 def main():
@@ -38,7 +40,7 @@ def main():
     import numpy as np
     import torch
 
-    from odesat_amd import cnf, device_count
+    from odesat_amd import _lib, cnf, device_count
     from odesat_amd import workloads as wl
     from odesat_amd.partition import MODES, LocalComm, PartitionedSolver, TorchComm, default_zeta
 
@@ -121,7 +123,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True,
             "scaling": "strong", "dtype": "fp32", "data": "synthetic: seeded random 3-SAT + counter-RNG voltages",
             "config": {"workload": workload, "mode": args.mode, "order": args.order,
-                       "terms": os.environ.get("ODESAT_PART_TERMS", "ell"),
+                       "terms": ["region", "ell", "slot"][_lib.get_experiment("PART_TERMS") or 0],
                        "graph_steps": args.graph if graph is not None else 0,
                        "collective": {"variables": "all_gather", "clauses": "all_reduce",
                                       "clauses_rs": "reduce_scatter + all_gather"}[args.mode],

@@ -4,6 +4,8 @@ import os, sys, time
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import tooling  # noqa: E402  (XP_LIB / XP_KNOBS: a variant build and experiment knobs)
+tooling.apply()
 from odesat_amd import cnf, workloads as wl
 from odesat_amd.system import ODESAT_STOP_NONE, Solver
 

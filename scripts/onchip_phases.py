@@ -1,5 +1,5 @@
 """Diagnostic: where a k_onchip launch's per-launch cost goes (needs a -DONCHIP_PHASES build via
-ODESAT_LIB).  Config 2, B replicas, one launch of K steps; per workgroup s_memrealtime (100 MHz) at
+XP_LIB).  Config 2, B replicas, one launch of K steps; per workgroup s_memrealtime (100 MHz) at
 start / after the state load / after the steps / end.  Prints per-round medians in microseconds."""
 import ctypes
 import json
@@ -9,6 +9,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import tooling  # noqa: E402  (XP_LIB / XP_KNOBS: a variant build and experiment knobs)
+tooling.apply()
 from odesat_amd import _lib, cnf  # noqa: E402
 from odesat_amd import workloads as wl  # noqa: E402
 from odesat_amd.system import ODESAT_STOP_NONE, Solver  # noqa: E402

@@ -1,5 +1,5 @@
 """Read the k_onchip stamp sums of a diagnostic build (scripts/build_variant.sh NAME -DONCHIP_STAMPS=1|2;
-run with ODESAT_LIB=expt/libNAME.so): per tile and wave, cycles waiting at the barrier vs working
+run with XP_LIB=expt/libNAME.so): per tile and wave, cycles waiting at the barrier vs working
 before it (and, build 2, the dv read-modify-write at the tile's start).  Config 2, B = 256 (one round
 of workgroups), one launch of STEPS steps.  Shares only: the stamps drain LDS operations."""
 import ctypes as C
@@ -10,6 +10,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import tooling  # noqa: E402  (XP_LIB / XP_KNOBS: a variant build and experiment knobs)
+tooling.apply()
 from odesat_amd import _lib, cnf, workloads as wl
 from odesat_amd.system import ODESAT_STOP_NONE, Solver
 

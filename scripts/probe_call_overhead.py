@@ -20,6 +20,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import tooling  # noqa: E402  (XP_LIB / XP_KNOBS: a variant build and experiment knobs)
+tooling.apply()
 from odesat_amd import cnf  # noqa: E402
 from odesat_amd import workloads as wl  # noqa: E402
 from odesat_amd.system import ODESAT_STOP_NONE, Solver  # noqa: E402

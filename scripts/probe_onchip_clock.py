@@ -1,6 +1,6 @@
 """Diagnostic (round 4): the effective shader clock of the headline kernel across the bench's call
 shape.  Needs the -DONCHIP_PHASES build (scripts/build_variant.sh ocphases "-DONCHIP_PHASES
--DONCHIP_ONLY_TR=90"; run with ODESAT_LIB=expt/libocphases.so).  Config 2, B = 1024, f32: a fresh
+-DONCHIP_ONLY_TR=90"; run with XP_LIB=expt/libocphases.so).  Config 2, B = 1024, f32: a fresh
 solver, the bench's 5-step warm-up call, then 12 calls of 20 steps back to back, 1.5 s idle, 4 more.
 Per call: HIP-event kernel time and, per round of 256 workgroups, the median effective shader clock
 over the steps (s_memtime ticks per s_memrealtime tick x 100 MHz) and the median step-loop time."""
@@ -13,6 +13,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import tooling  # noqa: E402  (XP_LIB / XP_KNOBS: a variant build and experiment knobs)
+tooling.apply()
 from odesat_amd import _lib, cnf  # noqa: E402
 from odesat_amd import workloads as wl  # noqa: E402
 from odesat_amd.system import ODESAT_STOP_NONE, Solver  # noqa: E402

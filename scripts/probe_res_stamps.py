@@ -1,5 +1,5 @@
 """Diagnostic: inside the f64 leg's k_resident launches.  Needs the -DRES_STAMPS build
-(scripts/build_variant.sh resstamps "-DRES_STAMPS" odesat_hip; run with ODESAT_LIB=expt/libresstamps.so).
+(scripts/build_variant.sh resstamps "-DRES_STAMPS" odesat_hip; run with XP_LIB=expt/libresstamps.so).
 Config 2, B = 1024, f64 fixed steps: the bench's shape (fresh solver, one 5-step launch), then 20-step
 launches back to back, 1.5 s idle, more 20-step launches, then a 60-step launch.  Per launch: the
 workgroups' start times split them into rounds (two workgroups per CU: 512 at a time); per round
@@ -15,6 +15,8 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import tooling  # noqa: E402  (XP_LIB / XP_KNOBS: a variant build and experiment knobs)
+tooling.apply()
 from odesat_amd import _lib, cnf  # noqa: E402
 from odesat_amd import workloads as wl  # noqa: E402
 from odesat_amd.system import ODESAT_STOP_NONE, Solver  # noqa: E402

@@ -1,4 +1,4 @@
-"""Diagnostic: stamp breakdown of a k_solo_fast fixed / adaptive step (needs a -DSOLO_STAMPS build, ODESAT_LIB=...).
+"""Diagnostic: stamp breakdown of a k_solo_fast fixed / adaptive step (needs a -DSOLO_STAMPS build, XP_LIB=...).
 hard.cnf, B = 1, f64, 2000 fixed steps; prints cycles per step per segment for each wave."""
 import ctypes
 import json
@@ -7,6 +7,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import tooling  # noqa: E402  (XP_LIB / XP_KNOBS: a variant build and experiment knobs)
+tooling.apply()
 
 
 def main():
@@ -28,7 +30,7 @@ def main():
                 row = [buf[w * 8 + i] / steps for i in range(len(names))]
                 if sum(row) == 0:
                     continue
-                print(json.dumps({"prec": prec, "adaptive": adaptive, "wave": w, "lanes": os.environ.get("ODESAT_SOLO_LANES"),
+                print(json.dumps({"prec": prec, "adaptive": adaptive, "wave": w, "knobs": tooling.knobs()["knobs"],
                                   **{n: round(x, 1) for n, x in zip(names, row)}, "total": round(sum(row), 1)}))
 
 

@@ -1,5 +1,5 @@
 """A/B helper: the sha256 of a run's final state (v, xs, xl of every replica) and its bookkeeping, for
-comparing two builds bit for bit (run once per build, e.g. with ODESAT_LIB=expt/libX.so).
+comparing two builds bit for bit (run once per build, e.g. with XP_LIB=expt/libX.so).
 
   python scripts/state_digest.py [--config config2] [--batch 256] [--steps 200] [--seeds 1,2,3] [--calls 4]
 """
@@ -11,6 +11,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+import tooling  # noqa: E402  (XP_LIB / XP_KNOBS: a variant build and experiment knobs)
+tooling.apply()
 
 
 def main():

@@ -191,7 +191,8 @@ def test_roofline_reads_the_committed_profiles():
     driver's shape (20 steps, B = 1024, config 2) with made-up launch times: k_onchip names VALU issue
     and carries its cycle model; the f64 k_resident with register tiles moves fewer bytes than the
     algorithmic convention counts, so its line also carries the rate of the bytes actually moved
-    (hbm_traffic, below the HBM peak) and says why the algorithmic rate can exceed the peak."""
+    (fabric_traffic, below the algorithmic one) and says why the algorithmic rate can exceed the peak;
+    every traffic figure says what the counters count (L2 <-> fabric bytes, Infinity-Cache hits included)."""
     import sys
     sys.path.insert(0, ROOT)
     import bench
@@ -202,4 +203,5 @@ def test_roofline_reads_the_committed_profiles():
     assert 0.0 < r["cycle_model"]["valu_floor_frac"] < 1.0
     r64 = bench.roofline(args, "k_resident", [4.7, 0.0, 0.0], [1, 0, 0], 1024 * (8 * n + 16 * m) * 2, dtype="f64")
     assert r64["bound"] == "hbm" and r64["traffic"] < 0.9 * r64["algorithmic_bytes_per_launch"]
-    assert 0.0 < r64["hbm_traffic"]["frac"] < r64["frac"] and "register tiles" in r64["note"]
+    assert 0.0 < r64["fabric_traffic"]["achieved"] < r64["achieved"] and "register tiles" in r64["note"]
+    assert "Infinity-Cache hits are included" in r64["traffic_counts"] and "fabric" in r["traffic_counts"]

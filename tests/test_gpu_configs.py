@@ -8,8 +8,9 @@
   config 3  uf250-style n=250 m=1065 seed 2, adaptive, B=1024 (k_wave): replicas bit-exact vs oc32;
   config 4  n=50k m=210k seed 3, B=1024 f32: replicas bit-exact vs oc32, every replica by property;
             inter (STOP_ANY) on the planted variant: the winner and the stop step;
-  config 5  n=1M m=4.2M seed 4, one replica partitioned (VARIABLES world 2 bit-exact; CLAUSES world 1
-            bit-exact, world 2 within a stated tolerance) vs oc32's fixed steps.
+  config 5  n=1M m=4.2M seed 4, one replica partitioned over 1, 2, 4 and 8 ranks (VARIABLES bit-exact;
+            CLAUSES / CLAUSES_RS bit-exact at world 1, within a stated tolerance beyond) vs oc32's fixed
+            steps; and the stop step of simulate on a planted instance of the same size at every world.
 Subsets of replicas are checked bit for bit; the rest through size-independent properties (the
 clamp ranges of system.rs:94-96, finiteness)."""
 import os
@@ -249,42 +250,107 @@ def test_config1_cli_solve_easy_adaptive_matches_oracle(tmp_path):
 
 # ----------------------------------------------------------------------------------- config 5 ---
 CLAUSES_TOL = 1e-5  # CLAUSES at world > 1 sums per-rank partial dv (reordered fold), max |dv| after 5 steps
+# BASELINE configs[4] names an 8-way partition; every world up to it runs as ranks held by one process on
+# the box's GPU (LocalComm + step_in_process: the collectives' sums and copies done in process)
+PART_CASES = [("VARIABLES", 2), ("VARIABLES", 4), ("VARIABLES", 8), ("CLAUSES", 1), ("CLAUSES", 2),
+              ("CLAUSES", 4), ("CLAUSES", 8), ("CLAUSES_RS", 1), ("CLAUSES_RS", 2), ("CLAUSES_RS", 4),
+              ("CLAUSES_RS", 8)]
 
 
-def test_config5_partitioned_full_size_vs_oracle():
-    """One replica of n = 1M, m = 4.2M over 2 ranks on the box's GPU (the exchange done in-process):
-    VARIABLES bit-exact, CLAUSES and CLAUSES_RS (reduce-scatter + all-gather) bit-exact at world 1 and
-    within CLAUSES_TOL at world 2, against oc32's fixed steps (system.rs:141-154), 5 steps of dt 0.01."""
-    from odesat_amd.partition import (CLAUSES, CLAUSES_RS, VARIABLES, LocalComm, PartitionedSolver, default_zeta,
-                                      step_in_process)
+@pytest.fixture(scope="module")
+def config5_random():
+    """Config 5 (n = 1M, m = 4.2M, seed 4) and the oracle's 5 fixed steps of dt 0.01 from replica 0."""
+    from odesat_amd.partition import default_zeta
     c = wl.CONFIGS["config5"]
     n, m = c["n"], c["m"]
     var, neg = wl.random_ksat(n, m, 3, c["seed"])
     cp, v_, n_ = wl.formula_arrays(var, neg)
     del var, neg
     o = Oracle(cp, v_, n_, n, "f32")
-    K, dt = 5, 0.01
-    zeta = default_zeta(n, m)
+    K, dt, zeta = 5, 0.01, default_zeta(n, m)
     v0 = init_voltages(42, 0, 1, n)[0].astype(np.float32)
     xs0 = o.init_short_term_memory()
     v, xs, xl = v0.copy(), xs0.copy(), np.ones(m, np.float32)
     for _ in range(K):
         o.euler_step_fixed(v, xs, xl, np.float32(dt), np.float32(zeta))
-    for mode, world in ((VARIABLES, 2), (CLAUSES, 1), (CLAUSES, 2), (CLAUSES_RS, 1), (CLAUSES_RS, 2)):
-        parts = [PartitionedSolver(cp, v_, n_, n, mode, comm=LocalComm(r, world)) for r in range(world)]
+    return dict(cp=cp, var=v_, neg=n_, n=n, m=m, K=K, dt=dt, zeta=zeta, init=(v0, xs0, np.ones(m)), ref=(v, xs, xl))
+
+
+def _run_partition(cfg, mode, world, steps, stop):
+    from odesat_amd.partition import LocalComm, PartitionedSolver, step_in_process
+    parts = [PartitionedSolver(cfg["cp"], cfg["var"], cfg["neg"], cfg["n"], mode, comm=LocalComm(r, world))
+             for r in range(world)]
+    try:
         for p in parts:
-            p.set_state(v0, xs0, np.ones(m))
-        for _ in range(K):
-            step_in_process(parts, dt, zeta, False)
+            p.set_state(*cfg["init"])
+        for _ in range(steps):
+            step_in_process(parts, cfg["dt"], cfg["zeta"], stop)
+        return [(p.status(stop), p.get_state()) for p in parts]
+    finally:
         for p in parts:
-            st = p.status(False)
-            assert st["steps_done"] == K
-            gv, gxs, gxl, loc = p.get_state()
-            if mode == VARIABLES or world == 1:
-                assert np.array_equal(gv.astype(np.float32), v)
-                assert np.array_equal(gxs.astype(np.float32), xs[loc]) and np.array_equal(gxl.astype(np.float32), xl[loc])
-            else:
-                assert np.max(np.abs(gv - v)) <= CLAUSES_TOL
-                assert np.max(np.abs(gxs - xs[loc])) <= CLAUSES_TOL
-                assert np.max(np.abs(gxl - xl[loc]) / xl[loc]) <= CLAUSES_TOL
             p.close()
+
+
+def _check_partition(cfg, mode, world, out, v, xs, xl):
+    from odesat_amd.partition import VARIABLES
+    for st, (gv, gxs, gxl, loc) in out:
+        if mode == VARIABLES or world == 1:  # the reference's fold order on every rank: bit-exact
+            assert np.array_equal(gv.astype(np.float32), v)
+            assert np.array_equal(gxs.astype(np.float32), xs[loc]) and np.array_equal(gxl.astype(np.float32), xl[loc])
+        else:  # CLAUSES / CLAUSES_RS: the ranks' partial sums reorder each dv fold
+            assert np.max(np.abs(gv - v)) <= CLAUSES_TOL
+            assert np.max(np.abs(gxs - xs[loc])) <= CLAUSES_TOL
+            assert np.max(np.abs(gxl - xl[loc]) / xl[loc]) <= CLAUSES_TOL
+
+
+@pytest.mark.parametrize("mode_name,world", PART_CASES)
+def test_config5_partitioned_full_size_vs_oracle(config5_random, mode_name, world):
+    """One replica of n = 1M, m = 4.2M split over `world` ranks (up to the 8 BASELINE names): VARIABLES
+    bit-exact at every world (its spanning clauses duplicated: 33 % of the clauses per rank at world
+    8), CLAUSES and CLAUSES_RS (reduce-scatter + all-gather) bit-exact at world 1 and within
+    CLAUSES_TOL beyond, against oc32's fixed steps (system.rs:141-154), 5 steps of dt 0.01."""
+    from odesat_amd import partition
+    mode = getattr(partition, mode_name)
+    cfg = config5_random
+    out = _run_partition(cfg, mode, world, cfg["K"], stop=False)
+    for st, _ in out:
+        assert st["steps_done"] == cfg["K"] and st["first_sat_step"] == -1
+    _check_partition(cfg, mode, world, out, *cfg["ref"])
+
+
+@pytest.fixture(scope="module")
+def config5_planted():
+    """Config 5's size with a planted assignment x*: v0 = 0.6 x* except three variables flipped to
+    -0.6 x*_i, xs0 per system.rs:361-372, fixed dt 0.1.  The oracle's simulate (system.rs:190-203)
+    reaches its first allsat step T, takes that step's update and stops (T + 1 steps)."""
+    c = wl.CONFIGS["config5"]
+    n, m = c["n"], c["m"]
+    var, neg, star = wl.planted_ksat(n, m, 3, c["seed"])
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    del var, neg
+    o = Oracle(cp, v_, n_, n, "f32")
+    v0 = (np.float32(0.6) * np.where(star, 1.0, -1.0)).astype(np.float32)
+    v0[[10, 500000, 999990]] *= -1
+    xs0 = o.init_short_term_memory()
+    v, xs, xl = v0.copy(), xs0.copy(), np.ones(m, np.float32)
+    dt, zeta, cap = 0.1, 0.001, 200
+    t, sat, _, _, _ = o.simulate(v, xs, xl, dt=np.float32(dt), steps=cap, zeta=np.float32(zeta))
+    assert sat and 1 < t < cap  # (measured: T = 78, so t = 79 steps)
+    return dict(cp=cp, var=v_, neg=n_, n=n, m=m, dt=dt, zeta=zeta, init=(v0, xs0, np.ones(m)), ref=(v, xs, xl),
+                steps_run=t, cap=t + 10)
+
+
+@pytest.mark.parametrize("mode_name,world", PART_CASES)
+def test_config5_partitioned_stop_step_vs_oracle_simulate(config5_planted, mode_name, world):
+    """The stop of simulate (system.rs:190-203: the first allsat step T, its update taken, nothing after)
+    at config 5's size over `world` ranks: the device bookkeeping folds the previous step's collective
+    result (CLAUSES: the all-reduced unsat count; VARIABLES / CLAUSES_RS: every block's flag slot), so
+    every rank reports first_sat_step T and T + 1 steps done while the driver keeps stepping past it;
+    the final state as in test_config5_partitioned_full_size_vs_oracle."""
+    from odesat_amd import partition
+    mode = getattr(partition, mode_name)
+    cfg = config5_planted
+    out = _run_partition(cfg, mode, world, cfg["cap"], stop=True)
+    for st, _ in out:
+        assert st["first_sat_step"] == cfg["steps_run"] - 1 and st["steps_done"] == cfg["steps_run"] and st["frozen"]
+    _check_partition(cfg, mode, world, out, *cfg["ref"])

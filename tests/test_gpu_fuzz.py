@@ -71,44 +71,58 @@ def variants(prec, uniform3, distinct):
     v = [("default", {}, None),
          ("fused", {}, _lib.ODESAT_ALG_FUSED),
          ("twopass", {}, _lib.ODESAT_ALG_TWOPASS),
-         ("fused-w8", {"ODESAT_GROUP_WIDTH": "8"}, _lib.ODESAT_ALG_FUSED),
-         ("resident-r1", {"ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "0"}, _lib.ODESAT_ALG_RESIDENT),
-         ("resident-narrow", {"ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "1"}, _lib.ODESAT_ALG_RESIDENT),
-         ("resident-r4", {"ODESAT_GROUP_WIDTH": "4"}, _lib.ODESAT_ALG_RESIDENT)]
+         ("fused-w8", {"GROUP_WIDTH": "8"}, _lib.ODESAT_ALG_FUSED),
+         ("resident-r1", {"GROUP_WIDTH": "1", "RES_NARROW": "0"}, _lib.ODESAT_ALG_RESIDENT),
+         ("resident-narrow", {"GROUP_WIDTH": "1", "RES_NARROW": "1"}, _lib.ODESAT_ALG_RESIDENT),
+         ("resident-r4", {"GROUP_WIDTH": "4"}, _lib.ODESAT_ALG_RESIDENT)]
     if uniform3:
         for team in ("1", "2", "4"):
-            v.append((f"wave-t{team}", {"ODESAT_WAVE": "1", "ODESAT_SOLO": "0", "ODESAT_WAVE_TEAM": team},
+            v.append((f"wave-t{team}", {"WAVE": "1", "SOLO": "0", "WAVE_TEAM": team},
                       _lib.ODESAT_ALG_RESIDENT))
         for lanes in ("64", "128", "0"):  # k_solo: one wave, two waves, the default team
-            env = {"ODESAT_WAVE": "1", "ODESAT_SOLO": "1"}
+            env = {"WAVE": "1", "SOLO": "1"}
             if lanes != "0":
-                env["ODESAT_SOLO_LANES"] = lanes
+                env["SOLO_LANES"] = lanes
             v.append((f"solo-l{lanes}", env, _lib.ODESAT_ALG_RESIDENT))
         # k_wave's general arithmetic (its short forms are the default on in-range states)
-        v.append(("wave-general", {"ODESAT_WAVE": "1", "ODESAT_SOLO": "0", "ODESAT_WAVE_TEAM": "2",
-                                   "ODESAT_WAVE_FAST": "0"}, _lib.ODESAT_ALG_RESIDENT))
+        v.append(("wave-general", {"WAVE": "1", "SOLO": "0", "WAVE_TEAM": "2",
+                                   "WAVE_FAST": "0"}, _lib.ODESAT_ALG_RESIDENT))
         # k_solo's general arithmetic (the fast kernel, k_solo_fast, is the default on in-range states)
-        v.append(("solo-general", {"ODESAT_WAVE": "1", "ODESAT_SOLO": "1", "ODESAT_SOLO_FAST": "0"},
+        v.append(("solo-general", {"WAVE": "1", "SOLO": "1", "SOLO_FAST": "0"},
                   _lib.ODESAT_ALG_RESIDENT))
-        # k_resident on 3-SAT (ODESAT_WAVE=0: its short forms on in-range states, and the general
-        # arithmetic with ODESAT_RES_FAST=0)
-        for lab, extra in (("r1", {"ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "0"}),
-                           ("narrow", {"ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "1"}),
-                           ("r4", {"ODESAT_GROUP_WIDTH": "4"}),
-                           ("general", {"ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "0", "ODESAT_RES_FAST": "0"})):
-            v.append((f"resident-k3-{lab}", {"ODESAT_WAVE": "0", **extra}, _lib.ODESAT_ALG_RESIDENT))
+        # k_resident on 3-SAT (knob WAVE = 0: its short forms on in-range states, and the general
+        # arithmetic with knob RES_FAST = 0)
+        for lab, extra in (("r1", {"GROUP_WIDTH": "1", "RES_NARROW": "0"}),
+                           ("narrow", {"GROUP_WIDTH": "1", "RES_NARROW": "1"}),
+                           ("r4", {"GROUP_WIDTH": "4"}),
+                           ("general", {"GROUP_WIDTH": "1", "RES_NARROW": "0", "RES_FAST": "0"})):
+            v.append((f"resident-k3-{lab}", {"WAVE": "0", **extra}, _lib.ODESAT_ALG_RESIDENT))
         if prec == "f32" and distinct:
-            v.append(("onchip", {"ODESAT_WAVE": "0", "ODESAT_GROUP_WIDTH": "1", "ODESAT_RES_NARROW": "0"},
+            v.append(("onchip", {"WAVE": "0", "GROUP_WIDTH": "1", "RES_NARROW": "0"},
                       _lib.ODESAT_ALG_ONCHIP))
     return v
 
 
 COVERED = {}  # (variant label, algorithm that ran) -> cases checked
 
+TERMS = {"region": 0, "ell": 1, "slot": 2}
+
+
+def push_knobs(env):
+    """Set the library's experiment knobs (odesat_set_experiment) of `env`; returns their old values."""
+    old = {k: _lib.get_experiment(k) for k in env}
+    for k, x in env.items():
+        _lib.set_experiment(k, TERMS[x] if k == "PART_TERMS" else int(x))
+    return old
+
+
+def pop_knobs(old):
+    for k, x in old.items():
+        _lib.set_experiment(k, x)
+
 
 def run_variant(f, B, prec, env, alg, adaptive, K, poll):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
+    old = push_knobs(env)
     try:
         with Solver(f, B, prec) as s:
             if alg is not None:
@@ -116,7 +130,7 @@ def run_variant(f, B, prec, env, alg, adaptive, K, poll):
                     s.set_algorithm(alg)
                 except _lib.OdesatError:
                     return None  # not available for this formula / layout
-            if "ODESAT_SOLO" in env and (s.step_kernel(adaptive) == "k_solo") != (env["ODESAT_SOLO"] == "1"):
+            if "SOLO" in env and (s.step_kernel(adaptive) == "k_solo") != (env["SOLO"] == "1"):
                 return None  # the forced path is not available for this formula (k_solo: slots per lane)
             s.init_state(9)
             # fixed: dt 0.05; adaptive: the reference's initial dt 0.01 (system.rs:182)
@@ -124,11 +138,7 @@ def run_variant(f, B, prec, env, alg, adaptive, K, poll):
                            stop=ODESAT_STOP_EACH, poll_interval=poll)
             return s.algorithm, r, s.get_state()
     finally:
-        for k, x in old.items():
-            if x is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = x
+        pop_knobs(old)
 
 
 @pytest.mark.parametrize("seed", PATH_SEEDS)
@@ -193,8 +203,8 @@ def test_fuzz_covered_every_path():
 
 
 # ------------------------------------------------------------- one instance across ranks -------
-PART_ENVS = [{}, {"ODESAT_PART_TERMS": "slot"}, {"ODESAT_PART_TERMS": "ell"}, {"ODESAT_PART_PACK": "0"},
-             {"ODESAT_PART_K3": "0"}, {"ODESAT_PART_XCD": "1"}]
+PART_ENVS = [{}, {"PART_TERMS": "slot"}, {"PART_TERMS": "ell"}, {"PART_PACK": "0"},
+             {"PART_K3": "0"}, {"PART_XCD": "1"}]
 
 
 @pytest.mark.parametrize("seed", PART_SEEDS)
@@ -219,8 +229,7 @@ def test_fuzz_partition_matches_oracle(seed):
     exp_sat = next((k for k, s in enumerate(sats) if s), -1)
     cases = [(VARIABLES, w) for w in (1, 2, 3, 4) if w <= n] + [(CLAUSES, 1)]
     for env in PART_ENVS[seed // 2 % len(PART_ENVS):][:2]:
-        old = {k: os.environ.get(k) for k in env}
-        os.environ.update(env)
+        old = push_knobs(env)
         try:
             for mode, world in cases:
                 parts = [PartitionedSolver(cp, var, neg, n, mode, comm=LocalComm(r, world)) for r in range(world)]
@@ -244,11 +253,7 @@ def test_fuzz_partition_matches_oracle(seed):
                     assert same(gxs.astype(T), xs[loc]) and same(gxl.astype(T), xl[loc]), ctx
                     p.close()
         finally:
-            for k, x in old.items():
-                if x is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = x
+            pop_knobs(old)
 
 
 # --------------------------------------------------------------------- the discrete search -----
@@ -271,18 +276,13 @@ def test_fuzz_stoch_matches_oracle(seed):
     f = cnf.CNFFormula.from_arrays(cp, var, neg, n)
     B, steps, rs = [1, 7, 70][seed % 3], 120, 3 + seed
     for path in ("wave", "hbm"):
-        old = os.environ.get("ODESAT_STOCH_WAVE")
-        if path == "hbm":
-            os.environ["ODESAT_STOCH_WAVE"] = "0"
+        old = push_knobs({"STOCH_WAVE": "0"} if path == "hbm" else {})
         try:
             with StochSearch(f, B) as s:
                 r = s.search(rs, steps, replica0=11)
                 gv, gxl = s.get_state()
         finally:
-            if old is None:
-                os.environ.pop("ODESAT_STOCH_WAVE", None)
-            else:
-                os.environ["ODESAT_STOCH_WAVE"] = old
+            pop_knobs(old)
         for b in range(B):
             v = np.zeros(n, np.uint8)
             xl = np.ones(len(cp) - 1, np.uint64)
@@ -315,8 +315,7 @@ def test_fuzz_stop_policies_agree(seed, prec):
     for stop in (ODESAT_STOP_ANY, ODESAT_STOP_NONE):
         for adaptive in (False, True):
             def run(env, alg):
-                old = {k: os.environ.get(k) for k in env}
-                os.environ.update(env)
+                old = push_knobs(env)
                 try:
                     with Solver(f, B, prec) as s:
                         if alg is not None:
@@ -329,11 +328,7 @@ def test_fuzz_stop_policies_agree(seed, prec):
                                        max_steps=K, stop=stop, poll_interval=poll)
                         return s.algorithm, r, s.get_state()
                 finally:
-                    for k, x in old.items():
-                        if x is None:
-                            os.environ.pop(k, None)
-                        else:
-                            os.environ[k] = x
+                    pop_knobs(old)
 
             base = run({}, _lib.ODESAT_ALG_FUSED)
             _, rb, sb = base
@@ -398,8 +393,7 @@ def test_fuzz_caller_states_match_oracle(seed, prec):
                 t, sat, _, _, _ = o.simulate(ov, oxs, oxl, dt=T(0.05), steps=K, zeta=T(0.01))
             ref.append((t, sat, ov, oxs, oxl))
         for label, env, alg in variants(prec, uniform3, distinct):
-            old = {k: os.environ.get(k) for k in env}
-            os.environ.update(env)
+            old = push_knobs(env)
             try:
                 with Solver(f, B, prec) as s:
                     if alg is not None:
@@ -413,11 +407,7 @@ def test_fuzz_caller_states_match_oracle(seed, prec):
                     galg = s.algorithm
                     gv, gxs, gxl = s.get_state()
             finally:
-                for k, x in old.items():
-                    if x is None:
-                        os.environ.pop(k, None)
-                    else:
-                        os.environ[k] = x
+                pop_knobs(old)
             for b in range(B):
                 t, sat, ov, oxs, oxl = ref[b]
                 ctx = f"{name} {prec} {'adaptive' if adaptive else 'fixed'} {label} (alg {galg}) replica {b}"

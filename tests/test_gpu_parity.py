@@ -309,12 +309,12 @@ def test_f32_tracks_f64_on_short_horizon():
 
 # ---------------------------------------------------------------- full size (BASELINE config 2) ---
 @pytest.mark.parametrize("pair_off", [None, "0"])
-def test_config2_full_size_subset_bitexact_and_properties(monkeypatch, pair_off):
+def test_config2_full_size_subset_bitexact_and_properties(xp, pair_off):
     """n=10k, m=42k, B=1024 f32 for 12 steps: replicas {0, 517, 1023} bit-exact vs the oracle's f32
     restatement; every replica: v in [-1,1], xs in [eps, 1-eps], xl in [1, 1e4 m], finite.  The
     solver's wave-paired tiles (k_onchip<90, 1>) and the other pair offset (91 tiles: k_onchip<92, 0>)."""
     if pair_off is not None:
-        monkeypatch.setenv("ODESAT_PAIR_OFF", pair_off)
+        xp.set("PAIR_OFF", pair_off)
     c = wl.CONFIGS["config2"]
     var, neg = wl.random_ksat(c["n"], c["m"], 3, c["seed"])
     cp, v_, n_ = wl.formula_arrays(var, neg)
@@ -367,7 +367,7 @@ def test_schedules_identical():
 @pytest.mark.parametrize("name", ["rand200", "small"])
 @pytest.mark.parametrize("prec", ["f64", "f32"])
 @pytest.mark.parametrize("B", [3, 64, 130])
-def test_algorithms_identical(name, prec, B):
+def test_algorithms_identical(name, prec, B, xp):
     """FUSED (variable-major recompute) and TWOPASS (contribution buffer) give bit-identical
     trajectories, including replicas frozen at different steps (STOP_EACH) and adaptive steps."""
     from odesat_amd import _lib
@@ -376,24 +376,22 @@ def test_algorithms_identical(name, prec, B):
         default = s.algorithm
     # these formulas are small: RESIDENT as k_wave (one wave per replica, variable fold)
     assert default == _lib.ODESAT_ALG_RESIDENT
-    # k_wave, the tile kernels (ODESAT_WAVE=0: RESIDENT, and ONCHIP for f32 3-SAT), FUSED, TWOPASS
+    # k_wave, the tile kernels (WAVE knob 0: RESIDENT, and ONCHIP for f32 3-SAT), FUSED, TWOPASS
     algs = [(_lib.ODESAT_ALG_RESIDENT, "1"), (_lib.ODESAT_ALG_RESIDENT, "0"), (_lib.ODESAT_ALG_FUSED, "1"),
             (_lib.ODESAT_ALG_TWOPASS, "1")]
     if prec == "f32" and name == "rand200":
         algs.append((_lib.ODESAT_ALG_ONCHIP, "0"))
-    import os
     for adaptive in (False, True):
         out = []
         for alg, wave in algs:
-            os.environ["ODESAT_WAVE"] = wave
-            os.environ["ODESAT_RES_NARROW"] = "0" if alg == _lib.ODESAT_ALG_ONCHIP else "1"  # ONCHIP: 512-lane tiles
+            xp.set("WAVE", wave)
+            xp.set("RES_NARROW", "0" if alg == _lib.ODESAT_ALG_ONCHIP else "1")  # ONCHIP: 512-lane tiles
             with Solver(f, B, prec) as s:
                 s.set_algorithm(alg)
                 s.init_state(21)
                 r = s.simulate(adaptive=adaptive, dt=0.05, max_steps=80, stop=ODESAT_STOP_EACH, poll_interval=3)
                 out.append((r["first_sat_step"], r["steps_done"], r["dt"], s.get_state()))
-        os.environ.pop("ODESAT_WAVE", None)
-        os.environ.pop("ODESAT_RES_NARROW", None)
+        xp.restore()
         for o in out[1:]:
             assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1])
             assert same(out[0][2], o[2])
@@ -401,18 +399,18 @@ def test_algorithms_identical(name, prec, B):
                 assert same(x, y)
 
 
-def _run_layout(monkeypatch, f, B, prec, width, **kw):
+def _run_layout(xp, f, B, prec, width, **kw):
     from odesat_amd import _lib
     if width is None:
-        monkeypatch.delenv("ODESAT_GROUP_WIDTH", raising=False)
+        xp.delete("GROUP_WIDTH")
     else:
-        monkeypatch.setenv("ODESAT_GROUP_WIDTH", str(width))
+        xp.set("GROUP_WIDTH", str(width))
     with Solver(f, B, prec) as s:
         alg, w = s.algorithm, s.group_width
         s.init_state(5)
         r = s.simulate(**kw)
         st = s.get_state()
-    monkeypatch.delenv("ODESAT_GROUP_WIDTH", raising=False)
+    xp.delete("GROUP_WIDTH")
     return alg, w, r, st
 
 
@@ -420,7 +418,7 @@ def _run_layout(monkeypatch, f, B, prec, width, **kw):
 @pytest.mark.parametrize("prec", ["f64", "f32"])
 @pytest.mark.parametrize("width", [1, 2, 4, 8, 16, 32])
 @pytest.mark.parametrize("mode", ["fixed-each", "fixed-any", "fixed-none", "adaptive-each", "adaptive-any"])
-def test_resident_widths_match_fused_w64(monkeypatch, name, prec, width, mode):
+def test_resident_widths_match_fused_w64(xp, name, prec, width, mode):
     """RESIDENT with R = 1 .. 32 replicas per workgroup (LDS-resident voltages, tiled clause pass +
     ordered fold) == FUSED at group width 64: every stop policy, fixed and adaptive steps."""
     from odesat_amd import _lib
@@ -429,8 +427,8 @@ def test_resident_widths_match_fused_w64(monkeypatch, name, prec, width, mode):
     stop = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[mode.split("-")[1]]
     kw = dict(adaptive=adaptive, dt=0.05, tol=1e-3, max_steps=150, stop=stop, poll_interval=4)
     B = 37
-    a1, w1, r1, s1 = _run_layout(monkeypatch, f, B, prec, width, **kw)
-    a2, w2, r2, s2 = _run_layout(monkeypatch, f, B, prec, 64, **kw)
+    a1, w1, r1, s1 = _run_layout(xp, f, B, prec, width, **kw)
+    a2, w2, r2, s2 = _run_layout(xp, f, B, prec, 64, **kw)
     # f32 3-SAT at R = 1: ONCHIP, unless the tile chain is narrow enough for one-wave tiles
     assert w1 == width and a1 in (_lib.ODESAT_ALG_RESIDENT, _lib.ODESAT_ALG_ONCHIP)
     assert (a2, w2) == (_lib.ODESAT_ALG_FUSED, 64)
@@ -441,7 +439,7 @@ def test_resident_widths_match_fused_w64(monkeypatch, name, prec, width, mode):
         assert same(x, y)
 
 
-def test_small_instance_width_config3():
+def test_small_instance_width_config3(xp):
     """Config 3 (n = 250): by default k_wave (one replica per wave); with the tile kernel the solver
     packs R replicas per workgroup (the largest R that still gives every CU a workgroup): B = 1024
     -> R = 4, B = 4096 -> R = 16.  Every trajectory equals FUSED's bit for bit on a replica subset."""
@@ -450,11 +448,10 @@ def test_small_instance_width_config3():
     var, neg = wl.random_ksat(c["n"], c["m"], 3, c["seed"])
     cp, v_, n_ = wl.formula_arrays(var, neg)
     f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
-    import os
     for B, R, wave in ((1024, 1, "1"), (1024, 4, "0"), (4096, 16, "0")):
-        os.environ["ODESAT_WAVE"] = wave  # 1: k_wave (one replica per wave); 0: the tile kernel at width R
+        xp.set("WAVE", wave)  # 1: k_wave (one replica per wave); 0: the tile kernel at width R
         with Solver(f, B, "f32") as s:
-            os.environ.pop("ODESAT_WAVE")
+            xp.delete("WAVE")
             assert (s.algorithm, s.group_width) == (_lib.ODESAT_ALG_RESIDENT, R)
             s.init_state(42)
             r1 = s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=40, stop=ODESAT_STOP_EACH, poll_interval=8)
@@ -508,13 +505,13 @@ def _instance(n, m, seed):
 
 @pytest.mark.parametrize("stop", ["each", "any", "none"])
 @pytest.mark.parametrize("pair_off", [None, "0", "1"])
-def test_onchip_lds_tiles_match_resident_and_oracle(stop, monkeypatch, pair_off):
+def test_onchip_lds_tiles_match_resident_and_oracle(stop, xp, pair_off):
     """n=6000, m=33000 (ratio 5.5): 116 tiles, so ONCHIP keeps 96 tiles' memories in VGPRs and 20
     in LDS.  ONCHIP == RESIDENT (HBM-streamed memories) bit for bit on every stop policy, and
     replica 0 == the oracle's f32 restatement -- with the wave-paired tiles at either pair offset
     (ODESAT_PAIR_OFF; None = the solver's choice)."""
     if pair_off is not None:
-        monkeypatch.setenv("ODESAT_PAIR_OFF", pair_off)
+        xp.set("PAIR_OFF", pair_off)
     from odesat_amd import _lib
     f, (cp, v_, n_) = _instance(6000, 33000, 5)
     pol = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[stop]
@@ -538,7 +535,7 @@ def test_onchip_lds_tiles_match_resident_and_oracle(stop, monkeypatch, pair_off)
 
 
 @pytest.mark.parametrize("path", ["onchip", "wave", "resident", "solo"])
-def test_call_sequences_fold_and_mirror_match_fused(monkeypatch, path):
+def test_call_sequences_fold_and_mirror_match_fused(xp, path):
     """Round 4 (callio.hpp): the persistent kernels reset a call's bookkeeping themselves (STOP_NONE /
     STOP_EACH) and store STOP_NONE results straight into the pinned host buffers.  A sequence of calls
     that mixes every kind -- fresh STOP_NONE (reset + mirror), continued STOP_EACH, fresh STOP_ANY
@@ -550,9 +547,9 @@ def test_call_sequences_fold_and_mirror_match_fused(monkeypatch, path):
     f = product_formula("easy")
     env = {"onchip": ("0", "0", "0"), "wave": ("1", "0", "0"), "resident": ("0", "1", "0"),
            "solo": ("1", "0", "1")}[path]
-    monkeypatch.setenv("ODESAT_WAVE", env[0])
-    monkeypatch.setenv("ODESAT_RES_NARROW", env[1])
-    monkeypatch.setenv("ODESAT_SOLO", env[2])
+    xp.set("WAVE", env[0])
+    xp.set("RES_NARROW", env[1])
+    xp.set("SOLO", env[2])
     seq = [dict(stop=ODESAT_STOP_NONE, max_steps=40, resume=False),
            dict(stop=ODESAT_STOP_EACH, max_steps=900, resume=True),
            dict(stop=ODESAT_STOP_ANY, max_steps=900, resume=False),
@@ -588,15 +585,15 @@ def test_call_sequences_fold_and_mirror_match_fused(monkeypatch, path):
 
 
 @pytest.mark.parametrize("adaptive", [False, True])
-def test_onchip_long_launches_sat_and_freeze(monkeypatch, adaptive):
+def test_onchip_long_launches_sat_and_freeze(xp, adaptive):
     """STOP_EACH over launches of many steps: replicas that satisfy easy.cnf freeze at their own
     step inside a launch (ONCHIP == k_wave == FUSED, states, sat steps and adaptive dt)."""
     from odesat_amd import _lib
     f = product_formula("easy")
     out = []
     for alg, wave in ((_lib.ODESAT_ALG_ONCHIP, "0"), (_lib.ODESAT_ALG_RESIDENT, "1"), (_lib.ODESAT_ALG_FUSED, "1")):
-        monkeypatch.setenv("ODESAT_WAVE", wave)
-        monkeypatch.setenv("ODESAT_RES_NARROW", "0")
+        xp.set("WAVE", wave)
+        xp.set("RES_NARROW", "0")
         with Solver(f, 40, "f32") as s:
             s.set_algorithm(alg)
             if alg == _lib.ODESAT_ALG_ONCHIP:
@@ -612,11 +609,41 @@ def test_onchip_long_launches_sat_and_freeze(monkeypatch, adaptive):
             assert same(x, y)
 
 
+def test_onchip_split_barrier_timeout_fails_the_call(xp):
+    """the adaptive k_onchip's split-barrier wait is bounded; a wait that gives up
+    must fail the call (ODESAT_EDEVICE), not return dv updates that raced.  The experiment knob
+    ONCHIP_POLL_LIMIT = 0 makes every wait not satisfied at its first poll give up (the product
+    waits 2^22 polls).  A solver without the knob then runs the same call cleanly, and its replica 0
+    equals the oracle's simulate (system.rs:111-139): the fault word was reset, no false report."""
+    from odesat_amd import _lib
+    n, m = 3000, 12600
+    f, (cp, v_, n_) = _instance(n, m, 7)
+    B, K = 256, 100
+    xp.set("ONCHIP_POLL_LIMIT", 0)
+    with Solver(f, B, "f32") as s:
+        assert s.step_kernel(True) == "k_onchip"
+        s.init_state(3)
+        with pytest.raises(_lib.OdesatError, match="split-barrier") as ei:
+            s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=K, stop=ODESAT_STOP_NONE, poll_interval=K)
+        assert ei.value.code == _lib.ODESAT_EDEVICE
+    xp.delete("ONCHIP_POLL_LIMIT")
+    with Solver(f, B, "f32") as s:
+        s.init_state(3)
+        r = s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=K, stop=ODESAT_STOP_NONE, poll_interval=K)
+        gv, gxs, gxl = s.get_state(0, 1)
+    o = Oracle(cp, v_, n_, n, "f32")
+    ov = init_voltages(3, 0, 1, n)[0].astype(np.float32)
+    oxs, oxl = o.init_short_term_memory(), np.ones(m, np.float32)
+    t, _, _, h, _ = o.simulate(ov, oxs, oxl, tol=np.float32(1e-3), steps=K, zeta=np.float32(0.001))
+    assert t == K and r["steps_done"][0] == K and same(np.float32(h), np.float32(r["dt"][0]))
+    assert same(gv[0], ov) and same(gxs[0], oxs) and same(gxl[0], oxl)
+
+
 @pytest.mark.parametrize("stop", ["each", "any", "none"])
-def test_onchip_adaptive_matches_resident_and_oracle(stop, monkeypatch):
+def test_onchip_adaptive_matches_resident_and_oracle(stop, xp):
     """Adaptive steps on chip (k_onchip's adaptive variant: four voltage arrays in LDS, the clause
     memories in VGPRs, one code instance for both passes) == k_resident's adaptive step
-    (ODESAT_ONCHIP_ADAPTIVE=0) bit for bit on every stop policy, per-replica dt included, and
+    (knob ONCHIP_ADAPTIVE = 0) bit for bit on every stop policy, per-replica dt included, and
     replica 0 == the oracle's f32 simulate with tol 1e-3 (system.rs:111-139, :204-234)."""
     from odesat_amd import _lib
     f, (cp, v_, n_) = _instance(3000, 12600, 5)
@@ -624,7 +651,7 @@ def test_onchip_adaptive_matches_resident_and_oracle(stop, monkeypatch):
     B, K = 6, 30
     out = []
     for ada in ("1", "0"):
-        monkeypatch.setenv("ODESAT_ONCHIP_ADAPTIVE", ada)
+        xp.set("ONCHIP_ADAPTIVE", ada)
         with Solver(f, B, "f32") as s:
             assert s.algorithm == _lib.ODESAT_ALG_ONCHIP
             assert s.step_kernel(True) == ("k_onchip" if ada == "1" else "k_resident")
@@ -647,10 +674,10 @@ def test_onchip_adaptive_matches_resident_and_oracle(stop, monkeypatch):
 
 @pytest.mark.parametrize("adaptive", [False, True])
 @pytest.mark.parametrize("stop", ["each", "any", "none"])
-def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, adaptive, monkeypatch):
+def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, adaptive, xp):
     """f64 steps keep the first RES_RC (fixed) / RES_RC_ADA (adaptive, VFG: with each tile's first-pass
     mn) tiles' memories in VGPRs for a launch (resident.hpp, round 4): == every tile streamed
-    (ODESAT_RES_RC=0) bit for bit on every stop policy -- fixed STOP_ANY launches write out of place and
+    (knob RES_RC = 0) bit for bit on every stop policy -- fixed STOP_ANY launches write out of place and
     replay -- over a fresh call and a continued one (per-replica dt included), and replica 0 == the
     oracle's f64 simulate (system.rs:111-154).  The instances' tilings are deep enough (85+ tiles,
     tests/test_tiling.py's hook) for the register prefix (the host needs RC + 16); the adaptive one is
@@ -663,7 +690,7 @@ def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, adaptive, 
     kw = dict(adaptive=True, tol=1e-3) if adaptive else dict(dt=0.05)
     out = []
     for rc in ("1", "0"):
-        monkeypatch.setenv("ODESAT_RES_RC", rc)
+        xp.set("RES_RC", rc)
         with Solver(f, B, "f64") as s:
             assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.step_kernel(adaptive) == "k_resident"
             s.init_state(9)
@@ -686,44 +713,6 @@ def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, adaptive, 
     if adaptive:
         assert same(h, a2["dt"][0])
     assert same(sa[0][0], ov) and same(sa[1][0], oxs) and same(sa[2][0], oxl)
-
-
-@pytest.mark.parametrize("prec", ["f32", "f64"])
-@pytest.mark.parametrize("stop", ["each", "any", "none"])
-def test_fused_owner_tt_matches_general_and_oracle(stop, prec, monkeypatch):
-    """FUSED owner-TT (round 4, kernels.hpp stream_rows3): only a clause's owning incidence reads its
-    memories and stores the next step's product xl xs for the other two.  Bit-exact against the
-    general FUSED step (ODESAT_FUSED_TT=0) on every stop policy, from a caller state with voltages
-    out of range (the first step of the call runs the general form, the rest owner-TT), and replica 0
-    against the oracle's fixed-step simulate."""
-    from odesat_amd import _lib
-    n, m = 900, 3780
-    f, (cp, v_, n_) = _instance(n, m, 21)
-    T = T_OF[prec]
-    o = Oracle(cp, v_, n_, n, prec)
-    pol = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[stop]
-    B, K = 70, 40
-    v, xs, xl = init_states(o, B, seed=5, T=T)
-    v[3, :20] *= 1.5  # out of range: the call's first step must take the general form
-    out = []
-    for tt in ("1", "0"):
-        monkeypatch.setenv("ODESAT_FUSED_TT", tt)
-        with Solver(f, B, prec) as s:
-            s.set_algorithm(_lib.ODESAT_ALG_FUSED)
-            s.set_state(v.astype(np.float64), xs.astype(np.float64), xl.astype(np.float64))
-            r1 = s.simulate(dt=0.05, max_steps=K, stop=pol, poll_interval=7)
-            r2 = s.simulate(dt=0.05, max_steps=K, stop=pol, poll_interval=7, resume=True)  # in range from the start
-            out.append((r1, r2, s.get_state()))
-    (a1, a2, sa), (b1, b2, sb) = out
-    for x, y in ((a1, b1), (a2, b2)):
-        assert np.array_equal(x["first_sat_step"], y["first_sat_step"]) and np.array_equal(x["steps_done"], y["steps_done"])
-        assert x["steps_run"] == y["steps_run"]
-    for x, y in zip(sa, sb):
-        assert same(x, y)
-    if stop == "none":  # every replica took both calls' 2K steps
-        ov, oxs, oxl = v[0].copy(), xs[0].copy(), xl[0].copy()
-        o.simulate(ov, oxs, oxl, dt=T(0.05), steps=2 * K, zeta=T(0.001))
-        assert same(sa[0][0], ov) and same(sa[1][0], oxs) and same(sa[2][0], oxl)
 
 
 def test_onchip_adaptive_inter_after_out_of_range_set_state():
@@ -755,19 +744,19 @@ def test_onchip_adaptive_inter_after_out_of_range_set_state():
 
 @pytest.mark.parametrize("narrow", ["0", "1"])
 @pytest.mark.parametrize("stop", ["each", "any", "none"])
-def test_resident_adaptive_clone_in_hbm_matches_fused_and_oracle(stop, narrow, monkeypatch):
+def test_resident_adaptive_clone_in_hbm_matches_fused_and_oracle(stop, narrow, xp):
     """f64 at n = 7000: v and dv fill 112 KB of LDS and the full-step clone (56 KB more) does not
     fit, so adaptive steps run k_resident with the clone in HBM (VFG) instead of FUSED on the same
-    one-replica layout.  VFG == FUSED (ODESAT_RES_VFG=0) bit for bit on every stop policy, with
+    one-replica layout.  VFG == FUSED (knob RES_VFG = 0) bit for bit on every stop policy, with
     full-width and one-wave tiles, per-replica dt included; replica 0 == the oracle's f64 simulate
     (system.rs:111-139)."""
-    monkeypatch.setenv("ODESAT_RES_NARROW", narrow)
+    xp.set("RES_NARROW", narrow)
     f, (cp, v_, n_) = _instance(7000, 29400, 11)
     pol = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[stop]
     B, K = 5, 30
     out = []
     for vfg in ("1", "0"):
-        monkeypatch.setenv("ODESAT_RES_VFG", vfg)
+        xp.set("RES_VFG", vfg)
         with Solver(f, B, "f64") as s:
             assert s.step_kernel(True) == ("k_resident" if vfg == "1" else "k_step")
             s.init_state(3)
@@ -788,22 +777,22 @@ def test_resident_adaptive_clone_in_hbm_matches_fused_and_oracle(stop, narrow, m
 
 @pytest.mark.parametrize("team", [None, "1", "2", "solo"])
 @pytest.mark.parametrize("n,m,prec,wave_env,wpw", [(250, 1065, "f64", None, 2), (600, 2520, "f32", "1", 1)])
-def test_wave_workgroup_widths(monkeypatch, n, m, prec, wave_env, wpw, team):
+def test_wave_workgroup_widths(xp, n, m, prec, wave_env, wpw, team):
     """k_wave with 2 (config 3 in f64) and 1 (a larger instance, forced) replicas per workgroup
     equals FUSED bit for bit, fixed and adaptive -- with the automatic team (8 and 16 waves per
     replica) and with teams of 1 and 2 waves; and k_solo (one replica per workgroup, 4 clause slots
     per lane at m = 2520 with 640 lanes: the default 512 would need 5) on the same formulas."""
-    monkeypatch.setenv("ODESAT_SOLO", "1" if team == "solo" else "0")
+    xp.set("SOLO", "1" if team == "solo" else "0")
     if team == "solo":
-        monkeypatch.setenv("ODESAT_SOLO_LANES", "640")
+        xp.set("SOLO_LANES", "640")
     if team not in (None, "solo"):
-        monkeypatch.setenv("ODESAT_WAVE_TEAM", team)
+        xp.set("WAVE_TEAM", team)
     from odesat_amd import _lib
     var, neg = wl.random_ksat(n, m, 3, 7)
     cp, v_, n_ = wl.formula_arrays(var, neg)
     f = cnf.CNFFormula.from_arrays(cp, v_, n_, n)
     if wave_env is not None:
-        monkeypatch.setenv("ODESAT_WAVE", wave_env)
+        xp.set("WAVE", wave_env)
     topo = m * 16 + (n + 1) * 4
     rep = ((2 * n + 3 * m + 3 * m) * (8 if prec == "f64" else 4) + 15) // 16 * 16
     assert (topo + 4 * rep > 159 * 1024) and (wpw == 1) == (topo + 2 * rep > 159 * 1024)
@@ -826,7 +815,7 @@ def test_wave_workgroup_widths(monkeypatch, n, m, prec, wave_env, wpw, team):
 
 @pytest.mark.parametrize("stop", [ODESAT_STOP_EACH, ODESAT_STOP_ANY, ODESAT_STOP_NONE])
 @pytest.mark.parametrize("adaptive", [False, True])
-def test_wave_teams_equal_fused(monkeypatch, stop, adaptive):
+def test_wave_teams_equal_fused(xp, stop, adaptive):
     """k_wave with one, two and four waves per replica (ODESAT_WAVE_TEAM) and k_solo with one, two
     and three waves (ODESAT_SOLO_LANES) equal FUSED bit for bit on easy.cnf, where replicas satisfy
     and freeze at their own steps inside long launches: a frozen replica's team keeps reaching the
@@ -837,13 +826,13 @@ def test_wave_teams_equal_fused(monkeypatch, stop, adaptive):
     for alg, team in ((_lib.ODESAT_ALG_FUSED, "1"), (_lib.ODESAT_ALG_RESIDENT, "1"), (_lib.ODESAT_ALG_RESIDENT, "2"),
                       (_lib.ODESAT_ALG_RESIDENT, "4"), (_lib.ODESAT_ALG_RESIDENT, "solo64"),
                       (_lib.ODESAT_ALG_RESIDENT, "solo128"), (_lib.ODESAT_ALG_RESIDENT, "solo192")):
-        monkeypatch.setenv("ODESAT_WAVE", "1")
+        xp.set("WAVE", "1")
         solo = team.startswith("solo")
-        monkeypatch.setenv("ODESAT_SOLO", "1" if solo else "0")
+        xp.set("SOLO", "1" if solo else "0")
         if solo:
-            monkeypatch.setenv("ODESAT_SOLO_LANES", team[4:])
+            xp.set("SOLO_LANES", team[4:])
         else:
-            monkeypatch.setenv("ODESAT_WAVE_TEAM", team)
+            xp.set("WAVE_TEAM", team)
         with Solver(f, 37, "f32") as s:
             s.set_algorithm(alg)
             if alg == _lib.ODESAT_ALG_RESIDENT:

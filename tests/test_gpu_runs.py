@@ -77,10 +77,10 @@ def test_continue_equals_one_call(prec, adaptive):
 
 @pytest.mark.parametrize("mode", ["fixed", "adaptive"])
 @pytest.mark.parametrize("stop", [0, 1])
-def test_run_abi_unbounded_in_small_chunks_matches_oracle(monkeypatch, mode, stop):
-    """odesat_run with max_steps = 0 (None) forced into 7-step calls (ODESAT_RUN_CHUNK) equals the
+def test_run_abi_unbounded_in_small_chunks_matches_oracle(xp, mode, stop):
+    """odesat_run with max_steps = 0 (None) forced into 7-step calls (knob RUN_CHUNK) equals the
     oracle's continuous run (oc32_run): adaptive dt is not reset between calls."""
-    monkeypatch.setenv("ODESAT_RUN_CHUNK", "7")
+    xp.set("RUN_CHUNK", "7")
     f = oracle_formula("easy")
     n, cp = f.varnum, np.asarray(f.clause_ptr, np.int32)
     lits = (np.asarray(f.var, np.int32) << 1) | np.asarray(f.neg, np.int32)
@@ -110,7 +110,7 @@ def test_run_abi_unbounded_in_small_chunks_matches_oracle(monkeypatch, mode, sto
 
 
 # ---------------------------------------------------------------------- STOP_ANY replay ---
-# (algorithm, ODESAT_WAVE, ODESAT_RES_NARROW, precision, adaptive)
+# (algorithm, WAVE knob, RES_NARROW knob, precision, adaptive)
 REPLAY = [
     ("onchip", "0", "0", "f32", False),      # k_onchip, out-of-place launches
     ("wave", "1", "1", "f32", False),        # k_wave
@@ -122,15 +122,15 @@ REPLAY = [
 
 
 @pytest.mark.parametrize("alg,wave,narrow,prec,adaptive", REPLAY)
-def test_inter_multistep_launches_equal_lockstep(monkeypatch, alg, wave, narrow, prec, adaptive):
+def test_inter_multistep_launches_equal_lockstep(xp, alg, wave, narrow, prec, adaptive):
     """STOP_ANY with 500-step launches: the first allsat step falls inside a launch, the replicas
     that ran past it are replayed to it.  Same stop step, winner and EVERY replica's state as
     FUSED's one-launch-per-step run (and, fixed step, as the oracle's simulate_inter)."""
     f = product_formula("easy")
     B = 40
     kw = dict(adaptive=adaptive, dt=0.1, tol=1e-3, max_steps=6000, stop=ODESAT_STOP_ANY)
-    monkeypatch.setenv("ODESAT_WAVE", wave)
-    monkeypatch.setenv("ODESAT_RES_NARROW", narrow)
+    xp.set("WAVE", wave)
+    xp.set("RES_NARROW", narrow)
     with Solver(f, B, prec) as s:
         want = {"onchip": _lib.ODESAT_ALG_ONCHIP}.get(alg, _lib.ODESAT_ALG_RESIDENT)
         if s.algorithm != want:
@@ -138,8 +138,8 @@ def test_inter_multistep_launches_equal_lockstep(monkeypatch, alg, wave, narrow,
         s.init_state(4)
         r1 = s.simulate(poll_interval=500, **kw)
         s1 = s.get_state()
-    monkeypatch.delenv("ODESAT_WAVE")
-    monkeypatch.delenv("ODESAT_RES_NARROW")
+    xp.delete("WAVE")
+    xp.delete("RES_NARROW")
     with Solver(f, B, prec) as s:
         s.set_algorithm(_lib.ODESAT_ALG_FUSED)
         s.init_state(4)
@@ -162,7 +162,7 @@ def test_inter_multistep_launches_equal_lockstep(monkeypatch, alg, wave, narrow,
         assert same(s1[0], v) and same(s1[1], xs) and same(s1[2], xl)
 
 
-def test_set_state_ends_a_stopped_inter_run(monkeypatch):
+def test_set_state_ends_a_stopped_inter_run(xp):
     """a STOP_ANY run that stopped, then odesat_set_state with states outside ONCHIP's
     range.  set_state ends the run (and its stop word), so a continue runs its steps (it returned 0
     before) and does not mark the state in range; a fresh simulate then takes its first step on the
@@ -175,8 +175,8 @@ def test_set_state_ends_a_stopped_inter_run(monkeypatch):
     xs = rng.uniform(-0.5, 1.5, (B, o.m)).astype(np.float32)
     xl = rng.uniform(0.5, 3.0, (B, o.m)).astype(np.float32)
     kw = dict(dt=0.1, max_steps=30, stop=ODESAT_STOP_ANY, poll_interval=30)
-    monkeypatch.setenv("ODESAT_WAVE", "0")  # one replica per group, as ONCHIP needs (REPLAY above)
-    monkeypatch.setenv("ODESAT_RES_NARROW", "0")
+    xp.set("WAVE", "0")  # one replica per group, as ONCHIP needs (REPLAY above)
+    xp.set("RES_NARROW", "0")
     with Solver(f, B, "f32") as s:
         s.set_algorithm(_lib.ODESAT_ALG_ONCHIP)
         s.init_state(4)

@@ -260,15 +260,15 @@ def test_partition_kernels_match_oracle(name, mode, world):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [
-    {"ODESAT_PART_TERMS": "slot"}, {"ODESAT_PART_TERMS": "ell"}, {"ODESAT_PART_TERMS": "region"},
-    {"ODESAT_PART_PACK": "0"}, {"ODESAT_PART_K3": "0"}, {"ODESAT_PART_XCD": "1"},
-    {"ODESAT_PART_REGIONS": "24", "ODESAT_PART_PACK": "0"}])
+    {"PART_TERMS": "slot"}, {"PART_TERMS": "ell"}, {"PART_TERMS": "region"},
+    {"PART_PACK": "0"}, {"PART_K3": "0"}, {"PART_XCD": "1"},
+    {"PART_REGIONS": "24", "PART_PACK": "0"}])
 @pytest.mark.parametrize("mode,world", [(VARIABLES, 2), (CLAUSES, 1), (CLAUSES_RS, 1)])
-def test_partition_layouts_match_oracle(monkeypatch, env, mode, world):
+def test_partition_layouts_match_oracle(xp, env, mode, world):
     """Every term layout / clause record / clause kernel / placement choice (read when a slice is
     created) folds the same terms in the same order: the same bits as the oracle."""
     for k, val in env.items():
-        monkeypatch.setenv(k, val)
+        xp.set(k, val)
     steps, dt = 20, 0.05
     _, (v, xs, xl), _, _ = _oracle_run("rand200", steps, dt)
     sts, states = _run_parts("rand200", mode, world, steps, dt, stop=False)

@@ -99,26 +99,26 @@ def product_formula(name):
 
 
 # the two device paths: the one-wave-per-replica LDS kernel (default for formulas that fit) and
-# the three-kernel HBM path (ODESAT_STOCH_WAVE=0, the path large formulas take)
-PATHS = {"wave": {}, "hbm": {"ODESAT_STOCH_WAVE": "0"}}
+# the three-kernel HBM path (knob STOCH_WAVE = 0, the path large formulas take)
+PATHS = {"wave": {}, "hbm": {"STOCH_WAVE": "0"}}
 
 
-def set_path(monkeypatch, path):
-    monkeypatch.delenv("ODESAT_STOCH_WAVE", raising=False)
-    monkeypatch.delenv("ODESAT_STOCH_WPW", raising=False)
+def set_path(xp, path):
+    xp.delete("STOCH_WAVE")
+    xp.delete("STOCH_WPW")
     for k, v in PATHS.get(path, {}).items():
-        monkeypatch.setenv(k, v)
+        xp.set(k, v)
     if path.startswith("wpw"):
-        monkeypatch.setenv("ODESAT_STOCH_WPW", path[3:])
+        xp.set("STOCH_WPW", path[3:])
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", ["wave", "hbm"])
 @pytest.mark.parametrize("name", ["easy", "hard", "rand200"])
 @pytest.mark.parametrize("B", [1, 37, 128])
-def test_search_bitexact(name, B, path, monkeypatch):
+def test_search_bitexact(name, B, path, xp):
     from odesat_amd.stoch import StochSearch
-    set_path(monkeypatch, path)
+    set_path(xp, path)
     _, o = oracle_for(name)
     steps, seed = 300, 5
     with StochSearch(product_formula(name), B) as s:
@@ -136,10 +136,10 @@ def test_search_bitexact(name, B, path, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", ["wave", "hbm"])
-def test_stop_none_and_chunked_calls(path, monkeypatch):
+def test_stop_none_and_chunked_calls(path, xp):
     """STOP_NONE keeps stepping after a satisfying step; two calls continue one RNG stream."""
     from odesat_amd.stoch import ODESAT_STOP_NONE, StochSearch
-    set_path(monkeypatch, path)
+    set_path(xp, path)
     _, o = oracle_for("easy")
     with StochSearch(product_formula("easy"), 4) as s:
         s.search(9, 150, stop=ODESAT_STOP_NONE)
@@ -155,9 +155,9 @@ def test_stop_none_and_chunked_calls(path, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", ["wave", "hbm"])
-def test_set_state_roundtrip_and_errors(path, monkeypatch):
+def test_set_state_roundtrip_and_errors(path, xp):
     from odesat_amd.stoch import StochSearch
-    set_path(monkeypatch, path)
+    set_path(xp, path)
     _, o = oracle_for("rand200")
     rng = np.random.default_rng(0)
     v = rng.integers(0, 2, (3, o.n)).astype(np.uint8)
@@ -181,10 +181,10 @@ def test_set_state_roundtrip_and_errors(path, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", ["wpw1", "wpw2", "wpw4", "wpw8"])
-def test_wave_workgroup_widths(path, monkeypatch):
+def test_wave_workgroup_widths(path, xp):
     """WPW replicas share a workgroup's LDS topology; 37 replicas leave the last workgroup ragged."""
     from odesat_amd.stoch import StochSearch
-    set_path(monkeypatch, path)
+    set_path(xp, path)
     _, o = oracle_for("rand200")
     B, steps, seed = 37, 200, 11
     with StochSearch(product_formula("rand200"), B) as s:
@@ -202,10 +202,10 @@ def test_wave_workgroup_widths(path, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", ["wave", "hbm"])
-def test_saturating_memories(path, monkeypatch):
+def test_saturating_memories(path, xp):
     """xl at the top of u64: +20 saturates (stoch.rs:50) and the u64 sums wrap, on both paths."""
     from odesat_amd.stoch import ODESAT_STOP_NONE, StochSearch
-    set_path(monkeypatch, path)
+    set_path(xp, path)
     _, o = oracle_for("easy")
     rng = np.random.default_rng(3)
     B = 3
@@ -223,9 +223,9 @@ def test_saturating_memories(path, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_large_formula_takes_the_hbm_path(monkeypatch):
+def test_large_formula_takes_the_hbm_path(xp):
     from odesat_amd.stoch import StochSearch
-    set_path(monkeypatch, "wave")
+    set_path(xp, "wave")
     n, m = 10_000, 42_000  # config 2's size: 9m + n bytes of state per replica exceed the LDS
     var = np.arange(3 * m) % n
     f = cnf.CNFFormula.from_arrays(np.arange(0, 3 * m + 1, 3), var, var % 2, varnum=n)
@@ -258,9 +258,9 @@ def mixed_width_formula():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", ["wave", "hbm"])
-def test_mixed_clause_widths(path, monkeypatch):
+def test_mixed_clause_widths(path, xp):
     from odesat_amd.stoch import StochSearch
-    set_path(monkeypatch, path)
+    set_path(xp, path)
     cp, var, neg, n = mixed_width_formula()
     o = Oracle(cp, var, neg, n, "f64")
     B, steps, seed = 9, 250, 21
