@@ -2,9 +2,12 @@
 // k_solo, k_solo_fast) so that a simulate call needs no separate launch before its first kernel and
 // no copy after its last one (odesat_hip.hip simulate_impl):
 //   begin   the launch starts the call: every replica r < B starts active with sat_step -1,
-//           steps_done 0 (and dt 0.01 for adaptive steps, system.rs:205) -- what k_begin_call does --
-//           without reading the bookkeeping; one thread per replica stores those values first, so a
-//           workgroup that returns early (padding replicas) leaves them too;
+//           steps_done 0 (and dt 0.01 for adaptive steps, system.rs:205) -- what k_begin_call does,
+//           except the unsat flags: only the FUSED / TWOPASS step kernels set them and k_status clears
+//           them after every step, so they are zero between calls whichever path ran -- without
+//           reading the bookkeeping; one thread per replica stores those values first, so a workgroup
+//           that returns early (padding replicas) leaves them too (test_call_sequences_fold_and_mirror_match_fused
+//           continues a folded call on FUSED);
 //   h_sat / h_done / h_dt   host-mapped pinned mirrors of sat_step, steps_done and dt: every replica's
 //           epilogue also stores its final values there (used on STOP_NONE calls, where every real
 //           replica runs every launch to its epilogue; finish_simulate then reads them directly).

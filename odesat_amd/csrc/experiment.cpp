@@ -33,6 +33,7 @@ const char *const KNOBS[] = {
     "RES_FAST",         // 0: k_resident's general arithmetic on 3-SAT
     "RES_RC",           // 0: no register-cached tiles in the f64 k_resident
     "RES_VFG",          // 0: f64 adaptive steps whose clone does not fit in LDS on FUSED, not k_resident
+    "RES_PAIRS",        // 0: the f64 k_resident on plain tiles (a barrier after every tile) instead of wave-paired ones
     // partition (odesat_part_create)
     "PART_TERMS",       // term layout: 0 REGION, 1 ELL, 2 SLOT
     "PART_REGIONS",     // REGION: ranges (a multiple of 8, >= 8)

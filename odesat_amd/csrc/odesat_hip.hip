@@ -82,6 +82,10 @@ struct odesat_solver {
     bool res_vfg = false; // ... with the full-step voltage clone in HBM (v and dv fill the LDS)
     int res_ntiles = 0;
     int32_t *res_tc = nullptr, *cmap = nullptr;
+    // f64 k_resident on wave-paired tiles (resident.hpp PAIRS): wave w of tile t holds internal clauses
+    // [res_tcw[8t+w], res_tcw[8t+w+1]), padded with m; a barrier after tile t iff t + oc_off is odd
+    int32_t *res_tcw = nullptr;
+    bool res_pairs = false;
     int4 *res_cl4 = nullptr;  // [m] literals of internal clause k (3-SAT)
     // ONCHIP (onchip.hip): same tiles as RESIDENT (R = 1, f32, 3-SAT); tiles [0, oc_tr) keep their
     // memories in VGPRs, [oc_tr, oc_tr + oc_tl) in LDS.  oc_tr == 0: not available
@@ -757,14 +761,15 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
 }
 
 template <typename T, int R, bool ADA, bool K3, int NTHR = ResShape<R>::NTH, bool VFG = false, bool FAST = false,
-          int RC = 0>
+          int RC = 0, bool PAIRS = false>
 int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     const size_t lds = res_lds_bytes(s->n, R, sizeof(T), ADA && !VFG);
-    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR, VFG, FAST, RC>),
+    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR, VFG, FAST, RC, PAIRS>),
                                    (int)RES_LDS_MAX));
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR, VFG, FAST, RC>), dim3(s->G), dim3(NTHR), lds, s->stream, a);
+        hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR, VFG, FAST, RC, PAIRS>), dim3(s->G), dim3(NTHR), lds, s->stream,
+                           a);
     }
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
@@ -886,6 +891,8 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
     a.cptr = s->cptr;
     a.lits = s->lits;
     a.tc = s->res_tc;
+    a.tcw = s->res_tcw;
+    a.pair_off = s->oc_off;
     a.v0 = (T *)s->v[0];
     a.v1 = (T *)s->v[1];
     a.c0 = (T *)s->c[0];
@@ -921,7 +928,9 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
         if constexpr (std::is_same<T, double>::value) {
             // the first RES_RC_ADA tiles' memories and first-pass mn in VGPRs for the launch (resident.hpp)
             if (f3 && s->res_rc && s->res_ntiles >= RES_RC_ADA + 16)
-                return launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA>(s, a);
+                return s->res_pairs
+                           ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA, true>(s, a)
+                           : launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA>(s, a);
         }
         return f3   ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true>(s, a)
                : k3 ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true>(s, a)
@@ -945,7 +954,8 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
         if constexpr (std::is_same<T, double>::value && R == 1) {
             // f64 fixed steps: the first RES_RC tiles' memories in VGPRs for the launch (resident.hpp)
             if (f3 && s->res_rc && s->res_ntiles >= RES_RC + 16)
-                return launch_resident_k<T, 1, false, true, NT, false, true, RES_RC>(s, a);
+                return s->res_pairs ? launch_resident_k<T, 1, false, true, NT, false, true, RES_RC, true>(s, a)
+                                    : launch_resident_k<T, 1, false, true, NT, false, true, RES_RC>(s, a);
         }
         return f3   ? launch_resident_k<T, R, false, true, NT, false, true>(s, a)
                : k3 ? launch_resident_k<T, R, false, true>(s, a)
@@ -1199,7 +1209,7 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     for (auto e : s->pool) (void)hipEventDestroy(e);
     void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->pc, s->ps, s->empty, s->inc, s->v[0], s->v[1], s->c[0],
                     s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
-                    s->sat_step, s->stop, s->res_tc, s->cmap, s->res_cl4, s->oc_rec, s->oc_rec12, s->oc_tcp, s->wv_rec4, s->wv_vst};
+                    s->sat_step, s->stop, s->res_tc, s->res_tcw, s->cmap, s->res_cl4, s->oc_rec, s->oc_rec12, s->oc_tcp, s->wv_rec4, s->wv_vst};
     for (void *p : ptrs) dfree(p);
     void *snaps[] = {s->snap_par, s->snap_sat, s->snap_done, s->snap_dt, s->ck_v, s->ck_c, s->ck_dt, s->ck_par,
                      s->ck_act, s->ck_sat, s->ck_done, s->ck_stop};
@@ -1319,9 +1329,11 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
     std::vector<uint8_t> lorder;  // per internal clause: literal order code (kP3), 0 = file order
     // wave-paired tiles where ONCHIP may run (onchip_setup's conditions; k_onchip needs them);
     // the ONCHIP_PAIRS knob = 0: plain tiles (RESIDENT)
-    bool pairs = res_r == 1 && !s->res_narrow && !s->res_wave && s->dtype == ODESAT_F32 && s->uniform_k == 3 &&
-                 n <= onchip::MAX_N;
-    pairs = pairs && odesat::xp_get("ONCHIP", 1) != 0 && odesat::xp_get("ONCHIP_PAIRS", 1) != 0;
+    // (f64: k_resident's short-form launches on the same tiles, RES_PAIRS; round 5)
+    bool pairs = res_r == 1 && !s->res_narrow && !s->res_wave && s->uniform_k == 3 &&
+                 (s->dtype == ODESAT_F32 ? n <= onchip::MAX_N && odesat::xp_get("ONCHIP", 1) != 0
+                                         : odesat::xp_get("RES_PAIRS", 1) != 0);
+    pairs = pairs && odesat::xp_get("ONCHIP_PAIRS", 1) != 0;
     const int cap = s->res_narrow ? RES_NARROW : res_capacity(res_r);
     if (s->res_wave) {  // no tiles: the file order, one pseudo-tile
         perm.resize(m);
@@ -1443,6 +1455,14 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         }
         s->res_ntiles = (int)tiles.size() - 1;
         s->alg = ODESAT_ALG_RESIDENT;
+        if (s->dtype == ODESAT_F64 && !wst.empty()) {  // the wave table of the paired tiles (k_resident PAIRS)
+            std::vector<int32_t> ws((size_t)(s->res_ntiles + 16) * PAIR_WAVES + 1, (int32_t)m);
+            std::copy(wst.begin(), wst.end() - 1, ws.begin());
+            if ((rc = dmalloc(s, (void **)&s->res_tcw, ws.size() * 4))) return bail(rc);
+            if (hipMemcpy(s->res_tcw, ws.data(), ws.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
+            s->res_pairs = true;
+        }
         if (s->res_wave) {  // k_wave: variable-major term positions, incidences sorted by (clause, literal)
             std::vector<int32_t> vst((size_t)n + 1, 0), fillc((size_t)n, 0);
             for (int64_t k = 0; k < L; ++k) vst[(lits[k] >> 1) + 1] += 1;

@@ -47,6 +47,9 @@ template <typename T> struct RArgs {
     const int32_t *__restrict__ cptr;  // [m+1] internal clause -> first slot
     const int32_t *__restrict__ lits;  // [L] literals by internal slot
     const int32_t *__restrict__ tc;    // [ntiles+1] first internal clause of each tile
+    const int32_t *__restrict__ tcw;   // wave-paired tiles (PAIRS): wave w of tile t holds internal clauses
+                                       // [tcw[8t+w], tcw[8t+w+1]), padded with m past the last tile
+    int32_t pair_off;                  // PAIRS: a barrier follows tile t iff t + pair_off is odd
     T *v0, *v1, *c0, *c1;              // state buffers, group layout with W == R
     uint8_t *par;                      // flipped by an out-of-place launch
     T *cf, *ch;                        // adaptive scratch memories (full step, first half)
@@ -73,7 +76,29 @@ template <typename T, int R> struct ResCtx {
     T *vL, *dvL, *vfL;  // LDS
     T *cf, *ch;         // this group's adaptive scratch: cf holds each clause's first-pass C
     int r, lc;          // this lane's replica and clause-lane index
+    int w, wl;          // PAIRS: this lane's wave (uniform) and lane in it
 };
+
+// The clause of this lane in tile t, and whether the slot holds one (if not, a valid clause index is
+// still returned, for unconditional loads).  Plain tiles: the tile's clauses [tc[t], tc[t+1]) lane by
+// lane.  Wave-paired tiles (PAIRS, odesat_hip.hip pair_tiles, as k_onchip runs them): wave w's
+// clauses [tcw[8t+w], tcw[8t+w+1]) in its lanes, so a clause that depends on one of the same barrier
+// interval sits in the same wave, whose LDS operations complete in issue order.
+template <typename T, int R, bool PAIRS>
+__device__ __forceinline__ int res_slot(const RArgs<T> &a, const ResCtx<T, R> &x, int t, bool &ok) {
+    if constexpr (PAIRS) {
+        const int c0 = ldc(a.tcw, t * 8 + x.w), c1 = ldc(a.tcw, t * 8 + x.w + 1);
+        const int c = c0 + x.wl;
+        ok = c < c1;
+        return ok ? c : (c1 > 0 ? c1 - 1 : 0);
+    } else {
+        const int tt = min(t, a.ntiles - 1);
+        const int c0 = ldc(a.tc, tt), c1 = ldc(a.tc, tt + 1);
+        const int c = c0 + x.lc;
+        ok = t < a.ntiles && c < c1;
+        return c < c1 ? c : (c1 > 0 ? c1 - 1 : 0);
+    }
+}
 
 // base + element offset with a 32-bit BYTE offset: lets the compiler use the SGPR-base + 32-bit
 // VGPR-offset form of global loads / stores (no 64-bit address arithmetic per lane)
@@ -120,14 +145,10 @@ template <typename T> __device__ __forceinline__ void res_stm(T *p, const Vec<T,
 
 // Loads of tile t (t >= ntiles: nothing to do, a valid address is read).  Unconditional, so the
 // ring's loads stay in flight across iterations (no control flow for the wait counters to merge).
-template <typename T, int R, int PK>
+template <typename T, int R, int PK, bool PAIRS = false>
 __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CM, int t,
                                           TileLoad<T> &ld, bool mem = true) {
-    const int tt = min(t, a.ntiles - 1);
-    const int c0 = ldc(a.tc, tt), c1 = ldc(a.tc, tt + 1);
-    const int c = c0 + x.lc;
-    ld.ok = t < a.ntiles && c < c1;
-    const int cc = c < c1 ? c : (c1 > 0 ? c1 - 1 : 0);  // a valid clause
+    const int cc = res_slot<T, R, PAIRS>(a, x, t, ld.ok);  // a valid clause
     // (one 12-byte load; three separate dword loads from SoA arrays avoid a register copy at the
     // ring's back-edge but measured 4% slower)
     ld.lit = *at(a.cl4, (uint32_t)cc);
@@ -196,7 +217,7 @@ template <typename T> struct Pend {
 // One 3-SAT clause of tile t from its prefetched loads: C, the memories' update and the three dv
 // terms (system.rs:43-88).  Voltages are read-only during a pass, so this runs one tile ahead of
 // the dv updates.
-template <typename T, int R, int PK, bool FAST = false>
+template <typename T, int R, int PK, bool FAST = false, bool PAIRS = false>
 __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t,
                                             const TileLoad<T> &ld, Pend<T> &P, bool on, T h, bool &uns, T &e,
                                             bool copy) {
@@ -207,7 +228,8 @@ __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R
         // (kernels.hpp solo_terms): each term tt min(other two values) with the literal's sign, R omitted,
         // 2 x the reference's terms (the variable phases halve h), the memory update from mn
         // (solo_mem); the first adaptive pass keeps mn (= 2 C) in the C scratch.
-        const int c = ldc(a.tc, t) + x.lc;
+        bool ok_;
+        const int c = res_slot<T, R, PAIRS>(a, x, t, ok_);
         const int lit[3] = {ld.lit.x, ld.lit.y, ld.lit.z};
         T v[3];
         uint32_t sg[3];
@@ -381,49 +403,49 @@ __device__ __forceinline__ void res_clause3_reg(const RArgs<T> &a, const ResCtx<
 // Iteration TT of the pipeline below with a static tile index: tile TT+1's clause from the registers
 // (TT+1 < RC) or from its slot, tile TT's terms applied, the slot refilled with tile TT+1+D (its
 // memories only if that tile streams).
-template <typename T, int R, int PK, bool FAST, int RC, int D, int TT>
+template <typename T, int R, int PK, bool FAST, int RC, int D, bool PAIRS, int TT>
 __device__ __forceinline__ void res_iter3_rc(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM,
                                              TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h, bool &uns, T &e,
                                              Vec<T, 2> (&rm)[RC], T (&rmn)[RC]) {
     Pend<T> Q;
     TileLoad<T> &S = b[(TT + 1) % D];
     if constexpr (TT + 1 < RC) res_clause3_reg<T, R, PK>(a, x, S, Q, on, h, uns, e, rm[TT + 1], rmn[TT + 1]);
-    else res_clause3<T, R, PK, FAST>(a, x, CM, TT + 1, S, Q, on, h, uns, e, CMr != CM);
+    else res_clause3<T, R, PK, FAST, PAIRS>(a, x, CM, TT + 1, S, Q, on, h, uns, e, CMr != CM);
     res_apply3<T, R>(x, P);
-    res_load3<T, R, PK>(a, x, CMr, TT + 1 + D, S, TT + 1 + D >= RC);
+    res_load3<T, R, PK, PAIRS>(a, x, CMr, TT + 1 + D, S, TT + 1 + D >= RC);
 #ifdef RES_TIMING_PAIRS  // timing-only diagnostic build (results race): a barrier after odd tiles only
     if (TT & 1)
 #endif
-    __syncthreads();
+    if (!PAIRS || ((TT + a.pair_off) & 1)) __syncthreads();  // (uniform) PAIRS: after the pair's second tile
     P = Q;
 }
-template <typename T, int R, int PK, bool FAST, int RC, int D, int... Ts>
+template <typename T, int R, int PK, bool FAST, int RC, int D, bool PAIRS, int... Ts>
 __device__ __forceinline__ void res_prefix(std::integer_sequence<int, Ts...>, const RArgs<T> &a, const ResCtx<T, R> &x,
                                            const T *CMr, T *CM, TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h,
                                            bool &uns, T &e, Vec<T, 2> (&rm)[RC], T (&rmn)[RC]) {
-    (res_iter3_rc<T, R, PK, FAST, RC, D, Ts>(a, x, CMr, CM, b, P, on, h, uns, e, rm, rmn), ...);
+    (res_iter3_rc<T, R, PK, FAST, RC, D, PAIRS, Ts>(a, x, CMr, CM, b, P, on, h, uns, e, rm, rmn), ...);
 }
 
 // One step of the 3-SAT tile pipeline: the terms of tile t+1 are computed from slot S (which is
 // then refilled with tile t+1+RES_DEPTH), tile t's terms P are applied to dv, barrier (tile t+1
 // may touch the same dv entries).
-template <typename T, int R, int PK, bool FAST = false, int D = res_depth<T>()>
+template <typename T, int R, int PK, bool FAST = false, int D = res_depth<T>(), bool PAIRS = false>
 __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, int t,
                                           TileLoad<T> &S, Pend<T> &P, bool on, T h, bool &uns, T &e) {
     Pend<T> Q;
-    res_clause3<T, R, PK, FAST>(a, x, CM, t + 1, S, Q, on, h, uns, e, CMr != CM);  // Q.ok = false past the last tile
+    res_clause3<T, R, PK, FAST, PAIRS>(a, x, CM, t + 1, S, Q, on, h, uns, e, CMr != CM);  // Q.ok = false past the last tile
     res_apply3<T, R>(x, P);
-    res_load3<T, R, PK>(a, x, CMr, t + 1 + D, S);
+    res_load3<T, R, PK, PAIRS>(a, x, CMr, t + 1 + D, S);
 #ifdef RES_TIMING_PAIRS  // timing-only diagnostic build (results race): a barrier after odd tiles only
     if (t & 1)
 #endif
-    __syncthreads();
+    if (!PAIRS || ((t + a.pair_off) & 1)) __syncthreads();  // (uniform) PAIRS: after the pair's second tile
     P = Q;
 }
 
 // One RHS pass over all tiles: dv (LDS) accumulates; memories are read from CMr (or the adaptive
 // scratch) and written by kind (P_FIXED: to CM).  Ends with a barrier (dv complete).
-template <typename T, int R, int PK, bool K3, bool FAST = false, int RC = 0>
+template <typename T, int R, int PK, bool K3, bool FAST = false, int RC = 0, bool PAIRS = false>
 __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, bool on, T h,
                                          bool &uns, T &e, Vec<T, 2> (&rm)[RC > 0 ? RC : 1], T (&rmn)[RC > 0 ? RC : 1]) {
     const int NT_ = a.ntiles;
@@ -442,28 +464,31 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
         TileLoad<T> b[D];
         Pend<T> P;
 #pragma unroll
-        for (int i = 0; i < D; ++i) res_load3<T, R, PK>(a, x, CMr, i, b[i], i >= RC);
+        for (int i = 0; i < D; ++i) res_load3<T, R, PK, PAIRS>(a, x, CMr, i, b[i], i >= RC);
         int t0 = 0;
         if constexpr (RC > 0) {
             res_clause3_reg<T, R, PK>(a, x, b[0], P, on, h, uns, e, rm[0], rmn[0]);
-            res_load3<T, R, PK>(a, x, CMr, D, b[0], D >= RC);
-            res_prefix<T, R, PK, FAST, RC, D>(std::make_integer_sequence<int, RC>{}, a, x, CMr, CM, b, P, on, h, uns, e,
-                                              rm, rmn);
+            res_load3<T, R, PK, PAIRS>(a, x, CMr, D, b[0], D >= RC);
+            res_prefix<T, R, PK, FAST, RC, D, PAIRS>(std::make_integer_sequence<int, RC>{}, a, x, CMr, CM, b, P, on, h,
+                                                     uns, e, rm, rmn);
             t0 = RC;
         } else {
-            res_clause3<T, R, PK, FAST>(a, x, CM, 0, b[0], P, on, h, uns, e, CMr != CM);
-            res_load3<T, R, PK>(a, x, CMr, D, b[0]);
+            res_clause3<T, R, PK, FAST, PAIRS>(a, x, CM, 0, b[0], P, on, h, uns, e, CMr != CM);
+            res_load3<T, R, PK, PAIRS>(a, x, CMr, D, b[0]);
         }
         for (; t0 + D <= NT_; t0 += D) {  // iteration t computes tile t+1 from slot (t+1) % D
 #pragma unroll
-            for (int i = 0; i < D; ++i) res_iter3<T, R, PK, FAST, D>(a, x, CMr, CM, t0 + i, b[(i + 1) % D], P, on, h, uns, e);
+            for (int i = 0; i < D; ++i)
+                res_iter3<T, R, PK, FAST, D, PAIRS>(a, x, CMr, CM, t0 + i, b[(i + 1) % D], P, on, h, uns, e);
         }
         if constexpr (D == 8) {
             if (t0 < NT_) {  // four tiles left: slots 1 .. 4
 #pragma unroll
-                for (int i = 0; i < 4; ++i) res_iter3<T, R, PK, FAST, D>(a, x, CMr, CM, t0 + i, b[i + 1], P, on, h, uns, e);
+                for (int i = 0; i < 4; ++i)
+                    res_iter3<T, R, PK, FAST, D, PAIRS>(a, x, CMr, CM, t0 + i, b[i + 1], P, on, h, uns, e);
             }
         }
+        if constexpr (PAIRS) __syncthreads();  // dv complete whatever the last tile's parity
     } else {
         for (int t = 0; t < NT_; ++t) {
             res_clause_any<T, R, PK>(a, x, CMr, CM, t, on, h, uns, e);
@@ -500,10 +525,12 @@ __device__ unsigned long long g_res_clk[4096 * 64];
 #else
 #define RES_STAMP(i) do {} while (0)
 #endif
-template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR, bool VFG = false, bool FAST = false, int RC = 0>
+template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR, bool VFG = false, bool FAST = false, int RC = 0,
+          bool PAIRS = false>
 __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     static_assert(!FAST || K3, "the short forms are 3-SAT only (res_clause_any has none)");
     static_assert(RC == 0 || (FAST && R == 1), "register tiles: short-form steps, R = 1");
+    static_assert(!PAIRS || (FAST && R == 1 && NTHR == 512), "wave-paired tiles: 8 waves, one replica, short forms");
     extern __shared__ __attribute__((aligned(16))) unsigned char res_smem[];
     using U = typename Bits<T>::U;
     constexpr int NTH = NTHR, NL = NTHR / R;
@@ -518,6 +545,8 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     ResCtx<T, R> x;
     x.r = tid % R;
     x.lc = tid / R;
+    x.w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    x.wl = tid & 63;
     const size_t nR = (size_t)a.n * R;
     x.vL = reinterpret_cast<T *>(res_smem);
     x.dvL = x.vL + nR;
@@ -556,9 +585,8 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     Vec<T, 2> rm[RC > 0 ? RC : 1];
     T rmn[RC > 0 ? RC : 1];  // adaptive: each register tile's first-pass mn
     auto rm_slot = [&](int t, bool &ok) {  // tile t's slot of this lane (a valid clause when empty)
-        const int c0 = ldc(a.tc, t), c = c0 + x.lc;
-        ok = c < ldc(a.tc, t + 1);
-        return (uint32_t)((ok ? c : c0) * R + x.r) * 2u;
+        const int c = res_slot<T, R, PAIRS>(a, x, t, ok);
+        return (uint32_t)(c * R + x.r) * 2u;
     };
 #pragma unroll
     for (int t = 0; t < RC; ++t) {
@@ -576,7 +604,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
         bool uns = false;
         T e = (T)0.0;
         if constexpr (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154)
-            res_pass<T, R, P_FIXED, K3, FAST, RC>(a, x, CMr, CMo, on, h, uns, e, rm, rmn);
+            res_pass<T, R, P_FIXED, K3, FAST, RC, PAIRS>(a, x, CMr, CMo, on, h, uns, e, rm, rmn);
             CMr = CMo;
             if (uns) unsL[x.r] = 1u;
             const T hv = FAST ? (T)0.5 * h : h;
@@ -596,7 +624,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
                 }
             }
         } else {  // euler_step (system.rs:111-139), per-replica dt
-            res_pass<T, R, P_ADA1, K3, FAST, RC>(a, x, CM, CM, on, h, uns, e, rm, rmn);
+            res_pass<T, R, P_ADA1, K3, FAST, RC, PAIRS>(a, x, CM, CM, on, h, uns, e, rm, rmn);
             if (uns) unsL[x.r] = 1u;
             __syncthreads();
             const bool st = on && unsL[x.r] != 0u;  // allsat replicas take no step (:122)
@@ -617,7 +645,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
             for (int j = 0; j < R; ++j) any_st = any_st || (actL[j] != 0 && unsL[j] != 0u);
             if (any_st) {  // uniform
                 bool u2 = false;
-                res_pass<T, R, P_ADA2, K3, FAST, RC>(a, x, CM, CM, st, h, u2, e, rm, rmn);
+                res_pass<T, R, P_ADA2, K3, FAST, RC, PAIRS>(a, x, CM, CM, st, h, u2, e, rm, rmn);
                 for (int i = x.lc; i < a.n; i += NL) {
                     const int idx = i * R + x.r;
                     const T d = x.dvL[idx];

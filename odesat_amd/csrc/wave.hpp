@@ -413,7 +413,8 @@ template <typename T> __device__ __forceinline__ T solo_fold(const T *tL, int s,
     return dv;
 }
 
-// Diagnostic build only (-DSOLO_STAMPS, scripts/build_variant.sh ... odesat_hip): per wave, s_memtime
+// Diagnostic build only (-DSOLO_STAMPS, scripts/build_variant.sh NAME -DSOLO_STAMPS wave_k -- k_solo is
+// instantiated in wave_k.hip): per wave, s_memtime
 // stamps split each fixed step into the clause pass, the first barrier, the fold and the closing
 // barrier; sums in g_solo_stamps (read by odesat_solo_stamps).  Each stamp drains the wave's LDS
 // operations: read the SHARES.

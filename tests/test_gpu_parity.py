@@ -542,7 +542,9 @@ def test_call_sequences_fold_and_mirror_match_fused(xp, path):
     (k_begin_call), fresh adaptive STOP_EACH (reset, dt restarts at 0.01), a continued STOP_NONE (no
     mirror) -- returns the same results and states as FUSED (which never folds), call by call, with
     replicas freezing on easy.cnf.  The persistent path's calls take Solver.simulate's reuse=True
-    path (the solver's own result arrays and params, rebuilt per call field by field)."""
+    path (the solver's own result arrays and params, rebuilt per call field by field).  Last, a fresh
+    folded call, then the same solver switched to FUSED continuing it (resume=True, no k_begin_call):
+    the folded begin leaves the bookkeeping FUSED reads as k_begin_call would."""
     from odesat_amd import _lib
     f = product_formula("easy")
     env = {"onchip": ("0", "0", "0"), "wave": ("1", "0", "0"), "resident": ("0", "1", "0"),
@@ -571,6 +573,11 @@ def test_call_sequences_fold_and_mirror_match_fused(xp, path):
                     assert owned is None or r["first_sat_step"] is owned
                     owned = r["first_sat_step"]
                 runs.append(({k: np.copy(x) for k, x in r.items()}, s.get_state()))
+            r = s.simulate(dt=0.1, stop=ODESAT_STOP_NONE, max_steps=25, poll_interval=64)  # folded (persistent)
+            runs.append(({k: np.copy(x) for k, x in r.items()}, s.get_state()))
+            s.set_algorithm(_lib.ODESAT_ALG_FUSED)
+            r = s.simulate(dt=0.1, stop=ODESAT_STOP_EACH, max_steps=400, poll_interval=16, resume=True)
+            runs.append(({k: np.copy(x) for k, x in r.items()}, s.get_state()))
         out.append((kern, runs))
     (k1, a), (k2, b) = out
     assert k2 == "k_step" and k1 == {"onchip": "k_onchip", "wave": "k_wave", "resident": "k_resident",
@@ -681,7 +688,8 @@ def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, adaptive, 
     replay -- over a fresh call and a continued one (per-replica dt included), and replica 0 == the
     oracle's f64 simulate (system.rs:111-154).  The instances' tilings are deep enough (85+ tiles,
     tests/test_tiling.py's hook) for the register prefix (the host needs RC + 16); the adaptive one is
-    large enough (n = 7 000) for the clone-in-HBM kernel."""
+    large enough (n = 7 000) for the clone-in-HBM kernel.  Round 5: the default runs them on wave-paired
+    tiles (resident.hpp PAIRS: a barrier after every second tile); == plain tiles (knob RES_PAIRS = 0)."""
     from odesat_amd import _lib
     n, m = (7000, 29400) if adaptive else (3000, 12600)
     f, (cp, v_, n_) = _instance(n, m, 5)
@@ -689,21 +697,23 @@ def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, adaptive, 
     B = 4 if adaptive else 6
     kw = dict(adaptive=True, tol=1e-3) if adaptive else dict(dt=0.05)
     out = []
-    for rc in ("1", "0"):
+    for rc, pairs in (("1", "1"), ("1", "0"), ("0", "0")):
         xp.set("RES_RC", rc)
+        xp.set("RES_PAIRS", pairs)
         with Solver(f, B, "f64") as s:
             assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.step_kernel(adaptive) == "k_resident"
             s.init_state(9)
             r1 = s.simulate(zeta=0.001, max_steps=13, stop=pol, poll_interval=13, **kw)
             r2 = s.simulate(zeta=0.001, max_steps=9, stop=pol, poll_interval=4, resume=True, **kw)
             out.append((r1, r2, s.get_state()))
-    (a1, a2, sa), (b1, b2, sb) = out
-    for x, y in ((a1, b1), (a2, b2)):
-        assert x["steps_run"] == y["steps_run"]
-        assert np.array_equal(x["first_sat_step"], y["first_sat_step"]) and np.array_equal(x["steps_done"], y["steps_done"])
-        assert same(x["dt"], y["dt"])
-    for x, y in zip(sa, sb):
-        assert same(x, y)
+    (a1, a2, sa) = out[0]
+    for (b1, b2, sb) in out[1:]:
+        for x, y in ((a1, b1), (a2, b2)):
+            assert x["steps_run"] == y["steps_run"]
+            assert np.array_equal(x["first_sat_step"], y["first_sat_step"]) and np.array_equal(x["steps_done"], y["steps_done"])
+            assert same(x["dt"], y["dt"])
+        for x, y in zip(sa, sb):
+            assert same(x, y)
     o = Oracle(cp, v_, n_, n, "f64")
     ov = init_voltages(9, 0, 1, n)[0]
     oxs, oxl = o.init_short_term_memory(), np.ones(m)
