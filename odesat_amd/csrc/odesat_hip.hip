@@ -761,7 +761,7 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
 }
 
 template <typename T, int R, bool ADA, bool K3, int NTHR = ResShape<R>::NTH, bool VFG = false, bool FAST = false,
-          int RC = 0, bool PAIRS = false>
+          int RC = 0, int PAIRS = 0>
 int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     const size_t lds = res_lds_bytes(s->n, R, sizeof(T), ADA && !VFG);
     HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR, VFG, FAST, RC, PAIRS>),
@@ -892,7 +892,6 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
     a.lits = s->lits;
     a.tc = s->res_tc;
     a.tcw = s->res_tcw;
-    a.pair_off = s->oc_off;
     a.v0 = (T *)s->v[0];
     a.v1 = (T *)s->v[1];
     a.c0 = (T *)s->c[0];
@@ -928,9 +927,10 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
         if constexpr (std::is_same<T, double>::value) {
             // the first RES_RC_ADA tiles' memories and first-pass mn in VGPRs for the launch (resident.hpp)
             if (f3 && s->res_rc && s->res_ntiles >= RES_RC_ADA + 16)
-                return s->res_pairs
-                           ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA, true>(s, a)
-                           : launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA>(s, a);
+                return !s->res_pairs ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA>(s, a)
+                       : s->oc_off
+                           ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA, 2>(s, a)
+                           : launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA, 1>(s, a);
         }
         return f3   ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true>(s, a)
                : k3 ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true>(s, a)
@@ -954,8 +954,9 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
         if constexpr (std::is_same<T, double>::value && R == 1) {
             // f64 fixed steps: the first RES_RC tiles' memories in VGPRs for the launch (resident.hpp)
             if (f3 && s->res_rc && s->res_ntiles >= RES_RC + 16)
-                return s->res_pairs ? launch_resident_k<T, 1, false, true, NT, false, true, RES_RC, true>(s, a)
-                                    : launch_resident_k<T, 1, false, true, NT, false, true, RES_RC>(s, a);
+                return !s->res_pairs ? launch_resident_k<T, 1, false, true, NT, false, true, RES_RC>(s, a)
+                       : s->oc_off ? launch_resident_k<T, 1, false, true, NT, false, true, RES_RC, 2>(s, a)
+                                   : launch_resident_k<T, 1, false, true, NT, false, true, RES_RC, 1>(s, a);
         }
         return f3   ? launch_resident_k<T, R, false, true, NT, false, true>(s, a)
                : k3 ? launch_resident_k<T, R, false, true>(s, a)

@@ -49,7 +49,6 @@ template <typename T> struct RArgs {
     const int32_t *__restrict__ tc;    // [ntiles+1] first internal clause of each tile
     const int32_t *__restrict__ tcw;   // wave-paired tiles (PAIRS): wave w of tile t holds internal clauses
                                        // [tcw[8t+w], tcw[8t+w+1]), padded with m past the last tile
-    int32_t pair_off;                  // PAIRS: a barrier follows tile t iff t + pair_off is odd
     T *v0, *v1, *c0, *c1;              // state buffers, group layout with W == R
     uint8_t *par;                      // flipped by an out-of-place launch
     T *cf, *ch;                        // adaptive scratch memories (full step, first half)
@@ -84,9 +83,13 @@ template <typename T, int R> struct ResCtx {
 // lane.  Wave-paired tiles (PAIRS, odesat_hip.hip pair_tiles, as k_onchip runs them): wave w's
 // clauses [tcw[8t+w], tcw[8t+w+1]) in its lanes, so a clause that depends on one of the same barrier
 // interval sits in the same wave, whose LDS operations complete in issue order.
-template <typename T, int R, bool PAIRS>
+// PAIRS: 0 = plain tiles; 1 / 2 = wave-paired tiles with pair offset 0 / 1 (a barrier follows tile t iff
+// t + PAIRS - 1 is odd).  The offset is a template parameter so that every tile's barrier is static.
+template <int PAIRS> __host__ __device__ constexpr bool res_bar_after(int t) { return PAIRS == 0 || ((t + PAIRS - 1) & 1) != 0; }
+
+template <typename T, int R, int PAIRS>
 __device__ __forceinline__ int res_slot(const RArgs<T> &a, const ResCtx<T, R> &x, int t, bool &ok) {
-    if constexpr (PAIRS) {
+    if constexpr (PAIRS != 0) {
         const int c0 = ldc(a.tcw, t * 8 + x.w), c1 = ldc(a.tcw, t * 8 + x.w + 1);
         const int c = c0 + x.wl;
         ok = c < c1;
@@ -145,7 +148,7 @@ template <typename T> __device__ __forceinline__ void res_stm(T *p, const Vec<T,
 
 // Loads of tile t (t >= ntiles: nothing to do, a valid address is read).  Unconditional, so the
 // ring's loads stay in flight across iterations (no control flow for the wait counters to merge).
-template <typename T, int R, int PK, bool PAIRS = false>
+template <typename T, int R, int PK, int PAIRS = 0>
 __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CM, int t,
                                           TileLoad<T> &ld, bool mem = true) {
     const int cc = res_slot<T, R, PAIRS>(a, x, t, ld.ok);  // a valid clause
@@ -217,7 +220,7 @@ template <typename T> struct Pend {
 // One 3-SAT clause of tile t from its prefetched loads: C, the memories' update and the three dv
 // terms (system.rs:43-88).  Voltages are read-only during a pass, so this runs one tile ahead of
 // the dv updates.
-template <typename T, int R, int PK, bool FAST = false, bool PAIRS = false>
+template <typename T, int R, int PK, bool FAST = false, int PAIRS = 0>
 __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t,
                                             const TileLoad<T> &ld, Pend<T> &P, bool on, T h, bool &uns, T &e,
                                             bool copy) {
@@ -403,7 +406,7 @@ __device__ __forceinline__ void res_clause3_reg(const RArgs<T> &a, const ResCtx<
 // Iteration TT of the pipeline below with a static tile index: tile TT+1's clause from the registers
 // (TT+1 < RC) or from its slot, tile TT's terms applied, the slot refilled with tile TT+1+D (its
 // memories only if that tile streams).
-template <typename T, int R, int PK, bool FAST, int RC, int D, bool PAIRS, int TT>
+template <typename T, int R, int PK, bool FAST, int RC, int D, int PAIRS, int TT>
 __device__ __forceinline__ void res_iter3_rc(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM,
                                              TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h, bool &uns, T &e,
                                              Vec<T, 2> (&rm)[RC], T (&rmn)[RC]) {
@@ -416,10 +419,10 @@ __device__ __forceinline__ void res_iter3_rc(const RArgs<T> &a, const ResCtx<T, 
 #ifdef RES_TIMING_PAIRS  // timing-only diagnostic build (results race): a barrier after odd tiles only
     if (TT & 1)
 #endif
-    if (!PAIRS || ((TT + a.pair_off) & 1)) __syncthreads();  // (uniform) PAIRS: after the pair's second tile
+    if constexpr (res_bar_after<PAIRS>(TT)) __syncthreads();  // PAIRS: after the pair's second tile only
     P = Q;
 }
-template <typename T, int R, int PK, bool FAST, int RC, int D, bool PAIRS, int... Ts>
+template <typename T, int R, int PK, bool FAST, int RC, int D, int PAIRS, int... Ts>
 __device__ __forceinline__ void res_prefix(std::integer_sequence<int, Ts...>, const RArgs<T> &a, const ResCtx<T, R> &x,
                                            const T *CMr, T *CM, TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h,
                                            bool &uns, T &e, Vec<T, 2> (&rm)[RC], T (&rmn)[RC]) {
@@ -429,7 +432,7 @@ __device__ __forceinline__ void res_prefix(std::integer_sequence<int, Ts...>, co
 // One step of the 3-SAT tile pipeline: the terms of tile t+1 are computed from slot S (which is
 // then refilled with tile t+1+RES_DEPTH), tile t's terms P are applied to dv, barrier (tile t+1
 // may touch the same dv entries).
-template <typename T, int R, int PK, bool FAST = false, int D = res_depth<T>(), bool PAIRS = false>
+template <typename T, int R, int PK, bool FAST = false, int D = res_depth<T>(), int PAIRS = 0, bool BAR = true>
 __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, int t,
                                           TileLoad<T> &S, Pend<T> &P, bool on, T h, bool &uns, T &e) {
     Pend<T> Q;
@@ -439,13 +442,22 @@ __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> 
 #ifdef RES_TIMING_PAIRS  // timing-only diagnostic build (results race): a barrier after odd tiles only
     if (t & 1)
 #endif
-    if (!PAIRS || ((t + a.pair_off) & 1)) __syncthreads();  // (uniform) PAIRS: after the pair's second tile
+    if constexpr (BAR) __syncthreads();  // PAIRS: after the pair's second tile only (res_block)
     P = Q;
+}
+// Iterations t0 + Is of the pipeline (t0 even), slot (slot0 + Is) % D each, with their static barriers.
+template <typename T, int R, int PK, bool FAST, int D, int PAIRS, int... Is>
+__device__ __forceinline__ void res_block(std::integer_sequence<int, Is...>, const RArgs<T> &a, const ResCtx<T, R> &x,
+                                          const T *CMr, T *CM, int t0, TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h,
+                                          bool &uns, T &e) {
+    (res_iter3<T, R, PK, FAST, D, PAIRS, res_bar_after<PAIRS>(Is)>(a, x, CMr, CM, t0 + Is, b[(Is + 1) % D], P, on, h, uns,
+                                                                   e),
+     ...);
 }
 
 // One RHS pass over all tiles: dv (LDS) accumulates; memories are read from CMr (or the adaptive
 // scratch) and written by kind (P_FIXED: to CM).  Ends with a barrier (dv complete).
-template <typename T, int R, int PK, bool K3, bool FAST = false, int RC = 0, bool PAIRS = false>
+template <typename T, int R, int PK, bool K3, bool FAST = false, int RC = 0, int PAIRS = 0>
 __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, bool on, T h,
                                          bool &uns, T &e, Vec<T, 2> (&rm)[RC > 0 ? RC : 1], T (&rmn)[RC > 0 ? RC : 1]) {
     const int NT_ = a.ntiles;
@@ -476,19 +488,14 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
             res_clause3<T, R, PK, FAST, PAIRS>(a, x, CM, 0, b[0], P, on, h, uns, e, CMr != CM);
             res_load3<T, R, PK, PAIRS>(a, x, CMr, D, b[0]);
         }
-        for (; t0 + D <= NT_; t0 += D) {  // iteration t computes tile t+1 from slot (t+1) % D
-#pragma unroll
-            for (int i = 0; i < D; ++i)
-                res_iter3<T, R, PK, FAST, D, PAIRS>(a, x, CMr, CM, t0 + i, b[(i + 1) % D], P, on, h, uns, e);
-        }
+        // iteration t computes tile t+1 from slot (t+1) % D (t0 stays even: RC and D are multiples of 4)
+        for (; t0 + D <= NT_; t0 += D)
+            res_block<T, R, PK, FAST, D, PAIRS>(std::make_integer_sequence<int, D>{}, a, x, CMr, CM, t0, b, P, on, h, uns, e);
         if constexpr (D == 8) {
-            if (t0 < NT_) {  // four tiles left: slots 1 .. 4
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    res_iter3<T, R, PK, FAST, D, PAIRS>(a, x, CMr, CM, t0 + i, b[i + 1], P, on, h, uns, e);
-            }
+            if (t0 < NT_)  // four tiles left: slots 1 .. 4
+                res_block<T, R, PK, FAST, D, PAIRS>(std::make_integer_sequence<int, 4>{}, a, x, CMr, CM, t0, b, P, on, h, uns, e);
         }
-        if constexpr (PAIRS) __syncthreads();  // dv complete whatever the last tile's parity
+        if constexpr (PAIRS != 0) __syncthreads();  // dv complete whatever the last tile's parity
     } else {
         for (int t = 0; t < NT_; ++t) {
             res_clause_any<T, R, PK>(a, x, CMr, CM, t, on, h, uns, e);
@@ -526,7 +533,7 @@ __device__ unsigned long long g_res_clk[4096 * 64];
 #define RES_STAMP(i) do {} while (0)
 #endif
 template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR, bool VFG = false, bool FAST = false, int RC = 0,
-          bool PAIRS = false>
+          int PAIRS = 0>
 __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     static_assert(!FAST || K3, "the short forms are 3-SAT only (res_clause_any has none)");
     static_assert(RC == 0 || (FAST && R == 1), "register tiles: short-form steps, R = 1");
