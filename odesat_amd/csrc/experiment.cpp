@@ -29,6 +29,7 @@ const char *const KNOBS[] = {
     "SOLO",             // 1 / 0: k_solo instead of / never instead of k_wave
     "SOLO_LANES",       // k_solo lanes per replica (a multiple of 64)
     "SOLO_FAST",        // 0: k_solo's general arithmetic on in-range states
+    "SOLO_CV",          // 0: k_solo_fast instead of k_solo_cv (clause-held voltages) on in-range states
     "RES_NARROW",       // 1 / 0: k_resident with one wave (64-clause tiles) per replica / never
     "RES_FAST",         // 0: k_resident's general arithmetic on 3-SAT
     "RES_RC",           // 0: no register-cached tiles in the f64 k_resident

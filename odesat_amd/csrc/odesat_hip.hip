@@ -73,6 +73,7 @@ struct odesat_solver {
     bool solo = false;          // k_solo (wave.hpp) instead of k_wave: one replica per workgroup, lanes' slots in registers
     int solo_nl = 64, solo_cpl = 1, solo_vpl = 1;  // k_solo: lanes per replica, clause / variable slots per lane
     bool solo_fast = true;      // k_solo's short arithmetic on in-range states (ODESAT_SOLO_FAST=0: the general form)
+    bool solo_cv = true;        // k_solo_cv (clause-held voltages) for the short arithmetic when it fits
     bool wave_fast = true;      // k_wave's likewise (ODESAT_WAVE_FAST=0)
     bool res_fast = true;       // k_resident's likewise, 3-SAT only (ODESAT_RES_FAST=0)
     bool res_rc = true;         // f64 fixed steps: register-cached tiles (resident.hpp; ODESAT_RES_RC=0)
@@ -804,6 +805,20 @@ template <typename T, bool ADA, int CPL, int VPL, bool FAST> int launch_solo_k(o
     return ODESAT_OK;
 }
 
+template <typename T, bool ADA, int CPL, int VPL> int launch_solo_cv_k(odesat_solver *s, WArgs<T> a) {
+    const size_t lds = solo_cv_elems(s->n, sizeof(T)) * sizeof(T);
+    const unsigned grid = (unsigned)s->G, block = (unsigned)s->solo_nl;
+    if (block > (unsigned)SOLO_CV_MAX_NL) return fail(ODESAT_EINVAL, "k_solo_cv: too many lanes");
+    HIP_TRY((solo_cv_launch<T, ADA, CPL, VPL>(true, a, grid, block, lds, (int)RES_LDS_MAX, s->stream)));
+    hipError_t e;
+    {
+        Timed tm(s, 0);
+        e = solo_cv_launch<T, ADA, CPL, VPL>(false, a, grid, block, lds, (int)RES_LDS_MAX, s->stream);
+    }
+    HIP_TRY(e);
+    return ODESAT_OK;
+}
+
 template <typename T>
 int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double dt, double zeta, double tol,
                 int stop_mode, bool oop, bool fast) {
@@ -836,6 +851,9 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     if (s->solo) {
         auto so = [&](auto cc, auto vv) -> int {
             constexpr int CPL = decltype(cc)::value, VPL = decltype(vv)::value;
+            if constexpr (CPL <= 2)
+                if (fast && s->solo_fast && s->solo_cv)
+                    return adaptive ? launch_solo_cv_k<T, true, CPL, VPL>(s, a) : launch_solo_cv_k<T, false, CPL, VPL>(s, a);
             if (fast && s->solo_fast)
                 return adaptive ? launch_solo_k<T, true, CPL, VPL, true>(s, a) : launch_solo_k<T, false, CPL, VPL, true>(s, a);
             return adaptive ? launch_solo_k<T, true, CPL, VPL, false>(s, a) : launch_solo_k<T, false, CPL, VPL, false>(s, a);
@@ -1506,6 +1524,14 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             // k_solo_fast's padded term blocks must fit as well
             s->solo_fast = solo_fast_elems(n, L, s->tsize) * s->tsize <= RES_LDS_MAX;
             s->solo_fast = s->solo_fast && odesat::xp_get("SOLO_FAST", 1) != 0;
+            // k_solo_cv (wave.hpp): the clause slots hold their literals' voltages and fold them
+            // themselves (2 barriers per adaptive step instead of 4); up to 2 clause slots per lane,
+            // 512 lanes, no variable with more terms than a padded block holds, and its two term
+            // areas in LDS.  The SOLO_CV knob (0) turns it off.
+            int64_t dmax = 0;
+            for (int64_t i = 0; i < n; ++i) dmax = std::max<int64_t>(dmax, vst[i + 1] - vst[i]);
+            s->solo_cv = s->solo_cpl <= 2 && nl <= SOLO_CV_MAX_NL && dmax <= SOLO_DPAD &&
+                         solo_cv_elems(n, s->tsize) * s->tsize <= RES_LDS_MAX && odesat::xp_get("SOLO_CV", 1) != 0;
             s->wave_fast = odesat::xp_get("WAVE_FAST", 1) != 0;
         }
         if ((rc = onchip_setup(s, tiles, wst, lits))) return bail(rc);

@@ -942,7 +942,326 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
     }
 }
 
-// The launches of k_wave / k_solo / k_solo_fast live in wave_k.hip, a translation unit of their own
+// ------------------------------------------------------------------------------------------------
+// k_solo_cv -- k_solo_fast with the voltages held by the clauses (round 5, the criterion's latency
+// path).  k_solo_fast crosses lanes four times per adaptive step (terms -> fold -> half-step voltages ->
+// clause gathers -> terms -> fold -> voltages -> gathers), each crossing an LDS store, a barrier and
+// a dependent read.  Here every clause slot keeps the voltages of its own three literals in registers
+// and folds their terms itself: variable i's dv is computed by every clause slot that holds i, from
+// the same terms in the same order with the same expressions, so every copy is bit-identical to the
+// one k_solo_fast's variable slot computes.  A pass is the clause arithmetic, the term stores, ONE
+// barrier and the reads of the slot's three padded blocks (SOLO_DPAD terms each, +0 past the degree;
+// the host picks this kernel only when no variable has more terms than that); no voltage crosses
+// lanes.  Per step: fixed 1 barrier (k_solo_fast 2), adaptive 2 (4).
+//   * LDS banks: a block's 16-byte reads from random variables conflict.  Blocks are SOLO_CV_BS
+//     slots apart (one 16-byte pad: 80 bytes in f64, 48 in f32), so a block's bank set is one of 16
+//     instead of 4; and a read past the variable's degree goes to one shared block of zeros (every
+//     lane on it reads the same address: no conflict) instead of the block's +0 padding.
+//   * The two passes (and consecutive fixed steps) use two term areas, so a pass's stores never meet
+//     the previous pass's reads: a slow lane's reads of area A finish before it reaches the barrier
+//     that the next writer of A must pass first.
+//   * Between barriers the step is one basic block: the adaptive step computes its update whether or
+//     not the replica is allsat and commits it by select (an allsat replica takes no step, :122), a
+//     clause slot past m stores its terms to a sink word of its own lane, and the fold adds every
+//     padded slot.  So the term reads go out right after the barrier, under the dt update's divide
+//     and square root (system.rs:133-135) and the vote, instead of after them.
+//   * The adaptive error's wave max and LDS atomic max run after the second barrier and are read after
+//     the next step's first.
+//   * Variables of degree 0 (no clause holds them) belong to variable slots l, l + NL, ... that apply
+//     the same update with dv = +0 (so a -0 voltage becomes +0 as in k_solo_fast); at the end each
+//     variable is written by the slot holding its first incidence (rank 0).
+// Bit-identical to k_solo_fast, k_solo, k_wave and the oracle (tests/test_gpu_parity.py,
+// tests/test_gpu_fuzz.py).  At most 512 lanes (the three blocks' reads take 48 VGPRs per clause slot
+// in f64).
+// ------------------------------------------------------------------------------------------------
+constexpr int SOLO_CV_MAX_NL = 512;
+
+// LDS elements of one k_solo_cv term area: n padded blocks of SOLO_CV_BS slots, the zero block, then a
+// sink word per lane
+__host__ __device__ constexpr int solo_cv_bs(size_t tsize) { return SOLO_DPAD + 16 / (int)tsize; }
+__host__ __device__ inline size_t solo_cv_area(int64_t n, size_t tsize) {
+    const int64_t per16 = 16 / (int64_t)tsize;
+    return (size_t)(((n + 1) * solo_cv_bs(tsize) + SOLO_CV_MAX_NL + per16 - 1) / per16 * per16);
+}
+__host__ __device__ inline size_t solo_cv_elems(int64_t n, size_t tsize) { return 2 * solo_cv_area(n, tsize); }
+
+template <typename T, bool ADAPTIVE, int CPL, int VPL>
+__global__ __launch_bounds__(SOLO_CV_MAX_NL) void k_solo_cv(WArgs<T> a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char wave_smem[];
+    using U = typename Bits<T>::U;
+    constexpr int PER16 = 16 / (int)sizeof(T);
+    constexpr int NB = SOLO_DPAD / PER16;  // 16-byte reads per padded block
+    constexpr int BS = solo_cv_bs(sizeof(T));  // slots between blocks
+    typedef T TV __attribute__((ext_vector_type(PER16)));
+    __shared__ U errM[2];  // per step parity: the max_error bits of the step (the waves' LDS atomic max)
+    __shared__ __attribute__((aligned(16))) int voteW[2][SOLO_CV_MAX_NL / 64];
+    const int NL = (int)blockDim.x, l = (int)threadIdx.x;
+    const int g = blockIdx.x;
+    if (l == 0 && g < a.G) io_begin_store<T>(a.io, g, a.act, a.sat_step, a.steps_done, a.dtr, ADAPTIVE, a.stop);
+    if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
+    if (g >= a.G || !io_active(a.io, a.act, g)) return;                // uniform per workgroup
+    const int n = a.n, m = a.m;
+    const int area = (int)solo_cv_area(n, sizeof(T));
+    T *P0 = reinterpret_cast<T *>(wave_smem);  // pass 1 / even fixed steps
+    T *P1 = P0 + area;                         // pass 2 / odd fixed steps
+    for (int i = l; i < (n + 1) * BS; i += NL) {
+        P0[i] = (T)0.0;
+        P1[i] = (T)0.0;
+    }
+    const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
+    const T *V = (p ? a.v1 : a.v0) + (size_t)g * n;
+    const T *CM = (p ? a.c1 : a.c0) + (size_t)g * m * 2;
+    const int mlast = m - 1, nlast = n - 1;
+    int vi[CPL][3], tp[CPL][3];  // variable and term slot of each literal
+    int ra[CPL][3][NB];          // the element read by each 16-byte read of its block (the zero block past the degree)
+    uint32_t sg[CPL][3];
+    bool ok[CPL], own[CPL][3];  // a clause slot below m; the literal is its variable's first incidence
+    T vv[CPL][3], xs[CPL], xl[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        ok[k] = l + k * NL < m;
+        const int c = min(l + k * NL, mlast);
+        const int4 r4 = a.rec4[c];
+        const int lit[3] = {r4.x & 0xffff, r4.y & 0xffff, r4.z & 0xffff};
+        const int pos[3] = {(int)((uint32_t)r4.x >> 16), (int)((uint32_t)r4.y >> 16), (int)((uint32_t)r4.z >> 16)};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const int v = lit[j] >> 1, rank = pos[j] - a.vst[v], deg = a.vst[v + 1] - a.vst[v];
+            vi[k][j] = v;
+            tp[k][j] = ok[k] ? v * BS + rank : (n + 1) * BS + l;  // (rank < SOLO_DPAD: host selection)
+#pragma unroll
+            for (int q = 0; q < NB; ++q) ra[k][j][q] = (q * PER16 < deg ? v : n) * BS + q * PER16;
+            sg[k][j] = (lit[j] & 1) ? 0x80000000u : 0u;
+            own[k][j] = ok[k] && rank == 0;
+            vv[k][j] = V[v];
+        }
+        xs[k] = CM[2 * c];
+        xl[k] = CM[2 * c + 1];
+    }
+    bool z0[VPL];  // variable slots of degree 0
+    T vr[VPL];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j) {
+        const int i = l + j * NL, ii = min(i, nlast);
+        z0[j] = i < n && a.vst[ii + 1] == a.vst[ii];
+        vr[j] = V[ii];
+    }
+    if (l < 2 * (SOLO_CV_MAX_NL / 64)) voteW[l >> 3][l & 7] = 0;
+    if (l < 2) errM[l] = 0;
+    __syncthreads();
+    int act = 1;
+    int64_t sat = io_sat(a.io, a.sat_step, g), done = io_done(a.io, a.steps_done, g);
+    T dtr = ADAPTIVE ? io_dt<T>(a.io, a.dtr, g) : a.dt;
+    const int w = l >> 6;
+    auto vote = [&](bool u, int k) {
+        const bool wu = __any(u);
+        if ((l & 63) == 0) voteW[k & 1][w] = wu ? 1 : 0;
+    };
+    auto votes = [&](int k) {
+        const int4 *vw = reinterpret_cast<const int4 *>(voteW[k & 1]);
+        int4 r4[SOLO_CV_MAX_NL / 256];
+#pragma unroll
+        for (int j = 0; j < SOLO_CV_MAX_NL / 256; ++j) r4[j] = vw[j];
+        int r = 0;
+#pragma unroll
+        for (int j = 0; j < SOLO_CV_MAX_NL / 256; ++j) r |= r4[j].x | r4[j].y | r4[j].z | r4[j].w;
+        return r != 0;
+    };
+    // a pass's clause arithmetic at voltages x with memories (txs, txl): terms into area A (a slot past
+    // m into its lane's sink word), mn into mn_o; unsat
+    auto terms = [&](const T (&x)[CPL][3], const T (&txs)[CPL], const T (&txl)[CPL], T *A, T (&mn_o)[CPL]) -> bool {
+        bool uns = false;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            T d[3];
+            mn_o[k] = solo_terms<T>(x[k], sg[k], txl[k] * txs[k], d);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) A[tp[k][j]] = d[j];
+            uns = uns || (ok[k] && !(mn_o[k] < (T)0.5));  // :88
+        }
+        return uns;
+    };
+    struct Blocks {
+        TV t[CPL][3][NB];
+    };
+    auto reads = [&](const T *A) {  // every literal's padded block
+        Blocks r;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int q = 0; q < NB; ++q) r.t[k][j][q] = *reinterpret_cast<const TV *>(A + ra[k][j][q]);
+        return r;
+    };
+    // 2 dv of every literal's variable: the reference's left fold of the 2x terms (:33, :80).  Every
+    // padded slot is added, so the 3 CPL chains interleave: the slots past a degree are +0, which
+    // changes no sum (dv starts at +0 and is never -0)
+    auto fold = [&](const Blocks &r, T (&dv)[CPL][3]) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) dv[k][j] = (T)0.0 + r.t[k][j][0][0];
+#pragma unroll
+        for (int u = 1; u < SOLO_DPAD; ++u)
+#pragma unroll
+            for (int k = 0; k < CPL; ++k)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) dv[k][j] = dv[k][j] + r.t[k][j][u / PER16][u % PER16];
+    };
+    auto clamp1 = [](T x) { return dmin(dmax(x, (T)-1.0), (T)1.0); };
+    const T zero = (T)0.0 + (T)0.0;  // 2 dv of a variable without terms (k_solo_fast's fold of a +0 block)
+    T mn1[CPL], mn2[CPL];
+    auto dt_next = [&](int k) { return dmax(dmin(dtr * dsqrt((T)a.tol / frombits(errM[k & 1])), (T)1e3), (T)0.0078125); };
+    bool pend = false;  // the previous step was taken and its dt update is still due
+    int klast = 0;
+#ifdef SOLO_STAMPS
+    uint64_t st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_last = solo_memtime();
+#endif
+    for (int k = 0; k < a.nsteps; ++k) {
+        const int step = a.step0 + k;
+        klast = k;
+        bool uns;
+        if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
+            const T h = dtr, hh = (T)0.5 * h;
+            T *A = (k & 1) ? P1 : P0;
+            vote(terms(vv, xs, xl, A, mn1), k);
+            SOLO_STAMP(0);
+            __syncthreads();  // the terms (and the votes) before the fold
+            SOLO_STAMP(1);
+            const Blocks r = reads(A);
+            uns = votes(k);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) solo_mem<T>(xs[c], xl[c], mn1[c], hh, h, a.xl_max, xs[c], xl[c]);
+            T dv[CPL][3];
+            fold(r, dv);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) vv[c][j] = clamp1(vv[c][j] + hh * dv[c][j]);  // :96
+#pragma unroll
+            for (int j = 0; j < VPL; ++j) {
+                const T x = clamp1(vr[j] + hh * zero);
+                vr[j] = z0[j] ? x : vr[j];
+            }
+            SOLO_STAMP(2);
+        } else {  // euler_step (:111-139)
+            vote(terms(vv, xs, xl, P0, mn1), k);  // the RHS at y, y's memories
+            SOLO_STAMP(0);
+            __syncthreads();  // B1: the first pass's terms, the votes, the previous step's error
+            SOLO_STAMP(1);
+            const T nd = dt_next(k - 1);  // (its read first: the divide starts under the blocks' reads)
+            const Blocks r1 = reads(P0);
+            uns = votes(k);
+            const bool go = uns;  // an allsat replica takes no step (:122): the update below is discarded
+            dtr = pend ? nd : dtr;
+            const T h = dtr, hh = (T)0.5 * h, hq = (T)0.25 * h;
+            T xsf[CPL], xlf[CPL], xsh[CPL], xlh[CPL], vf[CPL][3], vh[CPL][3], vf0[VPL], vh0[VPL];
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {  // the memories' full-step clone and first half step (:124-128)
+                solo_mem<T>(xs[c], xl[c], mn1[c], hh, h, a.xl_max, xsf[c], xlf[c]);
+                solo_mem<T>(xs[c], xl[c], mn1[c], hq, hh, a.xl_max, xsh[c], xlh[c]);
+            }
+            T dv[CPL][3];
+            fold(r1, dv);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    vf[c][j] = clamp1(vv[c][j] + hh * dv[c][j]);  // full-step clone
+                    vh[c][j] = clamp1(vv[c][j] + hq * dv[c][j]);  // first half step
+                }
+#pragma unroll
+            for (int j = 0; j < VPL; ++j) {
+                vf0[j] = clamp1(vr[j] + hh * zero);
+                vh0[j] = clamp1(vr[j] + hq * zero);
+            }
+            terms(vh, xsh, xlh, P1, mn2);  // the RHS at the half step
+            SOLO_STAMP(2);
+            __syncthreads();  // B2: the second pass's terms
+            SOLO_STAMP(3);
+            const Blocks r2 = reads(P1);
+            T e = (T)0.0;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {  // second half step of the memories (:130), max_error (:132)
+                T xsn, xln;
+                solo_mem<T>(xsh[c], xlh[c], mn2[c], hq, hh, a.xl_max, xsn, xln);
+                const T ec = dmax(e, dmax(dabs(xsf[c] - xsn), dabs(xlf[c] - xln)));
+                e = ok[c] ? ec : e;
+                xs[c] = go ? xsn : xs[c];
+                xl[c] = go ? xln : xl[c];
+            }
+            fold(r2, dv);
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const T vn = clamp1(vh[c][j] + hq * dv[c][j]);  // second half step
+                    const T ev = dmax(e, dabs(vf[c][j] - vn));       // :101-108
+                    e = ok[c] ? ev : e;
+                    vv[c][j] = go ? vn : vv[c][j];
+                }
+#pragma unroll
+            for (int j = 0; j < VPL; ++j) {
+                const T vn = clamp1(vh0[j] + hq * zero);
+                const T ev = dmax(e, dabs(vf0[j] - vn));
+                e = z0[j] ? ev : e;
+                vr[j] = z0[j] && go ? vn : vr[j];
+            }
+            const U eb = wave_max_bits(tobits(e));  // non-negative floats order as their bits
+            if ((l & 63) == 0) atomicMax(&errM[k & 1], eb);  // read after the next step's B1 (when go)
+            if (l == 0) errM[(k + 1) & 1] = 0;              // the previous step's error was read before B2
+            pend = go;
+            SOLO_STAMP(4);
+        }
+        done += 1;
+        if (!uns) {  // allsat: the fixed step was still taken (:148-152); adaptive took none
+            if (sat < 0) sat = step;
+            if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                            // simulate() breaks (:193)
+            if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
+        }
+        SOLO_STAMP(5);
+        if (!act) break;  // uniform
+    }
+    if (ADAPTIVE) {
+        __syncthreads();  // the last step's atomic max
+        if (pend) dtr = dt_next(klast);
+    }
+#ifdef SOLO_STAMPS
+    if ((l & 63) == 0 && g == 0)
+        for (int i = 0; i < 8; ++i) g_solo_stamps[(l >> 6) * 8 + i] = st_[i];
+#endif
+    const bool q = a.oop ? !p : p;
+    T *Vo = (q ? a.v1 : a.v0) + (size_t)g * n;
+    T *CMo = (q ? a.c1 : a.c0) + (size_t)g * m * 2;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            if (own[k][j]) Vo[vi[k][j]] = vv[k][j];
+#pragma unroll
+    for (int j = 0; j < VPL; ++j)
+        if (z0[j]) Vo[l + j * NL] = vr[j];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int c = l + k * NL;
+        if (c < m) {
+            CMo[2 * c] = xs[k];
+            CMo[2 * c + 1] = xl[k];
+        }
+    }
+    if (l == 0) {
+        if (a.oop) a.par[g] = (uint8_t)q;
+        a.act[g] = (uint8_t)act;
+        a.sat_step[g] = sat;
+        a.steps_done[g] = done;
+        if (ADAPTIVE) a.dtr[g] = dtr;
+        io_mirror<T>(a.io, g, sat, done, dtr, ADAPTIVE);
+    }
+}
+
+// The launches of k_wave / k_solo / k_solo_fast / k_solo_cv live in wave_k.hip, a translation unit of their own
 // built with the max-ILP machine scheduler (Makefile WAVE_FLAGS): prep = true sets the
 // kernel's dynamic-LDS limit (once per device, outside any timed region), prep = false launches.
 template <typename T, bool ADA, int WPW, int TW, bool FAST>
@@ -951,6 +1270,9 @@ hipError_t wave_launch(bool prep, const WArgs<T> &a, unsigned grid, unsigned blo
 template <typename T, bool ADA, int CPL, int VPL, bool FAST>
 hipError_t solo_launch(bool prep, const WArgs<T> &a, unsigned grid, unsigned block, size_t lds, int lds_max,
                        hipStream_t st);
+template <typename T, bool ADA, int CPL, int VPL>
+hipError_t solo_cv_launch(bool prep, const WArgs<T> &a, unsigned grid, unsigned block, size_t lds, int lds_max,
+                          hipStream_t st);
 
 }  // namespace odk
 

@@ -32,6 +32,14 @@ hipError_t solo_launch(bool prep, const WArgs<T> &a, unsigned grid, unsigned blo
     return hipGetLastError();
 }
 
+template <typename T, bool ADA, int CPL, int VPL>
+hipError_t solo_cv_launch(bool prep, const WArgs<T> &a, unsigned grid, unsigned block, size_t lds, int lds_max,
+                          hipStream_t st) {
+    if (prep) return odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_solo_cv<T, ADA, CPL, VPL>), lds_max);
+    hipLaunchKernelGGL((k_solo_cv<T, ADA, CPL, VPL>), dim3(grid), dim3(block), lds, st, a);
+    return hipGetLastError();
+}
+
 // the shapes odesat_hip.hip's launch_wave / launch_resident dispatch: (replicas per workgroup, waves per
 // replica) for k_wave, (clause slots, variable slots per lane) for k_solo, each in f32 / f64, fixed /
 // adaptive, general / short forms
@@ -55,5 +63,14 @@ WAVE_SHAPES(double)
     SOLO_TF(T, 4, 2)
 SOLO_SHAPES(float)
 SOLO_SHAPES(double)
+
+#define SOLO_CV_ONE(T, A, C, V)                                                                          \
+    template hipError_t solo_cv_launch<T, A, C, V>(bool, const WArgs<T> &, unsigned, unsigned, size_t, int, \
+                                                   hipStream_t);
+#define SOLO_CV_SHAPES(T) SOLO_CV_ONE(T, false, 1, 1) SOLO_CV_ONE(T, true, 1, 1) SOLO_CV_ONE(T, false, 1, 2) \
+    SOLO_CV_ONE(T, true, 1, 2) SOLO_CV_ONE(T, false, 2, 1) SOLO_CV_ONE(T, true, 2, 1) SOLO_CV_ONE(T, false, 2, 2) \
+    SOLO_CV_ONE(T, true, 2, 2)
+SOLO_CV_SHAPES(float)
+SOLO_CV_SHAPES(double)
 
 }  // namespace odk

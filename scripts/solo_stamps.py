@@ -1,5 +1,6 @@
-"""Diagnostic: stamp breakdown of a k_solo_fast fixed / adaptive step (needs a -DSOLO_STAMPS build, XP_LIB=...).
-hard.cnf, B = 1, f64, 2000 fixed steps; prints cycles per step per segment for each wave."""
+"""Diagnostic: stamp breakdown of a k_solo_fast / k_solo_cv fixed / adaptive step (needs a -DSOLO_STAMPS
+build of wave_k, XP_LIB=...; XP_KNOBS=SOLO_CV=0 for k_solo_fast).  hard.cnf, B = 1, f64, 2000 steps;
+prints cycles per step per segment for each wave."""
 import ctypes
 import json
 import os
@@ -24,14 +25,18 @@ def main():
             s.synchronize()
             buf = (ctypes.c_ulonglong * 128)()
             assert _lib.lib().odesat_solo_stamps(buf) == 0
-            names = (["clauses1", "barrier1", "fold1", "barrier2", "clauses2", "barrier3", "fold2", "barrier4_dt"]
-                     if adaptive else ["clauses", "barrier1", "fold", "book", "barrier2"])
+            if tooling.knobs()["knobs"].get("SOLO_CV", 1):  # k_solo_cv
+                names = (["terms1", "barrier1", "fold1_terms2", "barrier2", "fold2_err", "book"]
+                         if adaptive else ["terms", "barrier", "fold", "", "", "book"])
+            else:
+                names = (["clauses1", "barrier1", "fold1", "barrier2", "clauses2", "barrier3", "fold2", "barrier4_dt"]
+                         if adaptive else ["clauses", "barrier1", "fold", "book", "barrier2"])
             for w in range(16):
                 row = [buf[w * 8 + i] / steps for i in range(len(names))]
                 if sum(row) == 0:
                     continue
                 print(json.dumps({"prec": prec, "adaptive": adaptive, "wave": w, "knobs": tooling.knobs()["knobs"],
-                                  **{n: round(x, 1) for n, x in zip(names, row)}, "total": round(sum(row), 1)}))
+                                  **{n: round(x, 1) for n, x in zip(names, row) if n}, "total": round(sum(row), 1)}))
 
 
 if __name__ == "__main__":

@@ -87,6 +87,9 @@ def variants(prec, uniform3, distinct):
         # k_wave's general arithmetic (its short forms are the default on in-range states)
         v.append(("wave-general", {"WAVE": "1", "SOLO": "0", "WAVE_TEAM": "2",
                                    "WAVE_FAST": "0"}, _lib.ODESAT_ALG_RESIDENT))
+        # k_solo_fast (knob SOLO_CV = 0; the default on in-range states is k_solo_cv where a lane
+        # holds at most 2 clause slots, else k_solo_fast)
+        v.append(("solo-fast", {"WAVE": "1", "SOLO": "1", "SOLO_CV": "0"}, _lib.ODESAT_ALG_RESIDENT))
         # k_solo's general arithmetic (the fast kernel, k_solo_fast, is the default on in-range states)
         v.append(("solo-general", {"WAVE": "1", "SOLO": "1", "SOLO_FAST": "0"},
                   _lib.ODESAT_ALG_RESIDENT))
@@ -184,7 +187,8 @@ def test_fuzz_every_path_matches_oracle(seed, prec):
 def test_fuzz_covered_every_path():
     """The cases above reached every kernel family: FUSED (W = 64 and 8), TWOPASS, the RESIDENT
     tile kernels (512-lane, one-wave and R = 4 tiles; on 3-SAT in their short and general forms), k_wave with teams of 1, 2 and 4 waves, k_solo
-    with teams of 64, 128 and the default lanes (k_solo_fast) and in its general form, and ONCHIP."""
+    with teams of 64, 128 and the default lanes (k_solo_cv where a lane holds at most two clause slots,
+    else k_solo_fast), k_solo_fast forced, k_solo in its general form, and ONCHIP."""
     if not COVERED:
         pytest.skip("run together with test_fuzz_every_path_matches_oracle")
     need = [("fused", _lib.ODESAT_ALG_FUSED), ("twopass", _lib.ODESAT_ALG_TWOPASS),
@@ -194,6 +198,7 @@ def test_fuzz_covered_every_path():
             ("wave-t4", _lib.ODESAT_ALG_RESIDENT), ("onchip", _lib.ODESAT_ALG_ONCHIP),
             ("solo-l64", _lib.ODESAT_ALG_RESIDENT), ("solo-l128", _lib.ODESAT_ALG_RESIDENT),
             ("solo-l0", _lib.ODESAT_ALG_RESIDENT), ("solo-general", _lib.ODESAT_ALG_RESIDENT),
+            ("solo-fast", _lib.ODESAT_ALG_RESIDENT),
             ("wave-general", _lib.ODESAT_ALG_RESIDENT), ("resident-k3-r1", _lib.ODESAT_ALG_RESIDENT),
             ("resident-k3-narrow", _lib.ODESAT_ALG_RESIDENT), ("resident-k3-r4", _lib.ODESAT_ALG_RESIDENT),
             ("resident-k3-general", _lib.ODESAT_ALG_RESIDENT)]

@@ -591,6 +591,83 @@ def test_call_sequences_fold_and_mirror_match_fused(xp, path):
     assert (a[1][0]["first_sat_step"] >= 0).any()  # replicas froze on the way
 
 
+def _deg0_formula():
+    """40 variables: 0-31 in 60 distinct-variable 3-SAT clauses, variable 0 in the first 8 (degree 8,
+    a full padded block: k_solo_cv runs only when no variable has more terms than SOLO_DPAD = 8),
+    32-39 in none (degree 0)."""
+    rng = np.random.default_rng(5)
+    while True:
+        var = np.zeros((60, 3), np.int64)
+        for c in range(60):
+            var[c] = (np.concatenate([[0], rng.choice(np.arange(1, 32), 2, replace=False)]) if c < 8
+                      else rng.choice(np.arange(1, 32), 3, replace=False))
+        if np.bincount(var.reshape(-1)).max() <= 8:
+            break
+    neg = (rng.random(180) < 0.5).astype(np.uint8)
+    return np.arange(0, 181, 3, dtype=np.int64), var.reshape(-1), neg, 40
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+@pytest.mark.parametrize("shape,lanes", [("hard", 192), ("hard", 128), ("deg0", 64), ("deg0", 128)])
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_solo_cv_matches_solo_fast_and_oracle(xp, adaptive, shape, lanes, prec):
+    """k_solo_cv (round 5, wave.hpp: the clause slots hold their literals' voltages and fold them
+    themselves) against k_solo_fast (knob SOLO_CV = 0) and the oracle, B = 1 over three calls of 300
+    steps (continued): on hard.cnf (the criterion's formula) at one clause slot per lane (192 lanes) and
+    at two (128: lanes 32-127 hold a slot past m, whose terms go to their sink words), and on a formula
+    with a variable of degree 8 (a full padded block) and 8 variables of degree 0 starting at -0.0 /
+    +0.0 / -1 / 1 / 0.25 / -0.5 (a taken step turns -0.0 into +0.0, as k_solo_fast's dv = +0 does) at
+    64 and 128 lanes (m = 60: lanes past m)."""
+    from odesat_amd import _lib
+    T = T_OF[prec]
+    if shape == "hard":
+        fo, o = oracle_for("hard", prec)
+        f = product_formula("hard")
+        cp, n = fo.clause_ptr, fo.varnum
+    else:
+        cp, var, neg, n = _deg0_formula()
+        f = cnf.CNFFormula.from_arrays(cp, var, neg, n)
+        o = Oracle(cp, var, neg, n, prec)
+    m = len(cp) - 1
+    v0 = init_voltages(3, 0, 1, n)[0].astype(T)
+    if shape == "deg0":
+        v0[32:40] = np.array([-0.0, 0.0, -1.0, 1.0, -0.0, 0.25, -0.5, -0.0], T)
+    xs0, xl0 = o.init_short_term_memory(), np.ones(m, T)
+    out = []
+    for cv in ("1", "0"):
+        xp.set("WAVE", "1")
+        xp.set("SOLO", "1")
+        xp.set("SOLO_LANES", str(lanes))
+        xp.set("SOLO_CV", cv)
+        with Solver(f, 1, prec) as s:
+            s.set_algorithm(_lib.ODESAT_ALG_RESIDENT)
+            assert s.step_kernel(adaptive) == "k_solo"
+            s.set_state(v0[None].astype(np.float64), xs0[None].astype(np.float64), xl0[None].astype(np.float64))
+            runs = []
+            for call in range(3):
+                r = s.simulate(adaptive=adaptive, dt=0.01 if adaptive else 0.05, tol=1e-3, zeta=0.01,
+                               max_steps=300, stop=ODESAT_STOP_EACH, poll_interval=300,
+                               resume=call > 0)
+                runs.append(({k: np.copy(x) for k, x in r.items()}, s.get_state()))
+            out.append(runs)
+    for (ra, sa), (rb, sb) in zip(*out):
+        assert np.array_equal(ra["first_sat_step"], rb["first_sat_step"])
+        assert np.array_equal(ra["steps_done"], rb["steps_done"]) and same(ra["dt"], rb["dt"])
+        for x, y in zip(sa, sb):
+            assert same(x, y)
+    ov, oxs, oxl = v0.copy(), xs0.copy(), xl0.copy()
+    ra, (gv, gxs, gxl) = out[0][-1]
+    if adaptive:
+        t, sat, _, h, _ = o.simulate(ov, oxs, oxl, tol=T(1e-3), dt=None, steps=900, zeta=T(0.01))
+        assert same(ra["dt"][0], h)
+    else:
+        t, sat, _, h, _ = o.simulate(ov, oxs, oxl, dt=T(0.05), steps=900, zeta=T(0.01))
+    assert ra["steps_done"][0] == t and (ra["first_sat_step"][0] >= 0) == bool(sat)
+    assert same(gv[0], ov) and same(gxs[0], oxs) and same(gxl[0], oxl)
+    if shape == "deg0" and t > 0:
+        assert not np.signbit(gv[0][[32, 36, 39]]).any()  # -0.0 became +0.0
+
+
 @pytest.mark.parametrize("adaptive", [False, True])
 def test_onchip_long_launches_sat_and_freeze(xp, adaptive):
     """STOP_EACH over launches of many steps: replicas that satisfy easy.cnf freeze at their own
