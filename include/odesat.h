@@ -306,6 +306,16 @@ int odesat_get_experiment(const char *key, int64_t *value);
 void odesat_clear_experiments(void);
 int odesat_experiment_knob(int i, const char **name);
 
+/* Test hook (no device needed): k_solo_cv's lane and LDS block placement (odesat_amd/csrc/cv_layout.cpp)
+ * for a 3-SAT formula -- lits[3 m] = var << 1 | neg, vst[n + 1] the variable-major term starts -- on nl
+ * lanes (a multiple of 64) of cpl (1 or 2) clause slots, tsize-byte (4 / 8) terms and term blocks
+ * 0 .. blk_cap - 1, after `iters` search steps: slot_clause[nl cpl] (clause or -1), slot_order[3 nl cpl]
+ * (the clause's literal index 0..2 at each position), blk[n + 1] (blk[n]: the zero block), and the bank model's
+ * LDS cycles of the plain and the chosen layout. */
+int odesat_cv_layout(int64_t n, int64_t m, const int32_t *lits, const int32_t *vst, int nl, int cpl, int tsize,
+                     int blk_cap, int iters, int32_t *slot_clause, int32_t *slot_order, int32_t *blk,
+                     int64_t *cost_plain, int64_t *cost_opt);
+
 /* --------------------------------------------- one instance across GPUs ------- */
 
 /* The fixed Euler step (system.rs:141-154) of ONE replica whose formula is partitioned over `world`

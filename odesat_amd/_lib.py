@@ -38,6 +38,7 @@ _i64 = C.c_int64
 _dp = C.POINTER(C.c_double)
 _u8p = C.POINTER(C.c_uint8)
 _i64p = C.POINTER(C.c_int64)
+_i32p = C.POINTER(C.c_int32)
 _fp = C.POINTER(C.c_float)
 
 # name -> (restype, argtypes); kept in sync with include/odesat.h (tests/test_abi.py checks)
@@ -106,6 +107,8 @@ SIGNATURES = {
     "odesat_get_experiment": (C.c_int, [C.c_char_p, _i64p]),
     "odesat_clear_experiments": (None, []),
     "odesat_experiment_knob": (C.c_int, [C.c_int, C.POINTER(C.c_char_p)]),
+    "odesat_cv_layout": (C.c_int, [_i64, _i64, _i32p, _i32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _i32p,
+                                   _i32p, _i32p, _i64p, _i64p]),
     "odesat_part_create": (C.c_int, [C.c_int, C.c_int, _i64, _i64, _i64, _i64p, _i64p, _u8p, _i64, _i64, _i64p,
                                      _i64p, _i64, C.POINTER(_P)]),
     "odesat_part_destroy": (None, [_P]),
@@ -184,6 +187,27 @@ def u8ptr(a):
 
 def i64ptr(a):
     return None if a is None else a.ctypes.data_as(_i64p)
+
+
+def i32ptr(a):
+    return None if a is None else a.ctypes.data_as(_i32p)
+
+
+def cv_layout(lits, vst, nl, cpl, tsize, blk_cap, iters):
+    """k_solo_cv's lane and block placement (include/odesat.h odesat_cv_layout; a host-only test hook):
+    (slot_clause, slot_order, blk, cost_plain, cost_opt) for the 3-SAT literals lits[3 m] (var << 1 |
+    neg) with variable-major term starts vst[n + 1]."""
+    import numpy as np
+    lits = np.ascontiguousarray(lits, np.int32)
+    vst = np.ascontiguousarray(vst, np.int32)
+    n, m = len(vst) - 1, len(lits) // 3
+    sc = np.zeros(nl * cpl, np.int32)
+    so = np.zeros(3 * nl * cpl, np.int32)
+    blk = np.zeros(n + 1, np.int32)
+    cp, co = C.c_int64(0), C.c_int64(0)
+    check(lib().odesat_cv_layout(n, m, i32ptr(lits), i32ptr(vst), nl, cpl, tsize, blk_cap, iters, i32ptr(sc),
+                                 i32ptr(so), i32ptr(blk), C.byref(cp), C.byref(co)))
+    return sc, so.reshape(-1, 3), blk, cp.value, co.value
 
 
 def set_experiment(key: str, value) -> None:

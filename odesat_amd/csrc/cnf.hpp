@@ -30,3 +30,17 @@ int64_t xp_get(const char *key, int64_t dflt);
 inline bool xp_isset(const char *key) { return xp_get(key, -1) >= 0; }
 
 }  // namespace odesat
+
+namespace odesat {
+
+// k_solo_cv's lane and block placement (cv_layout.cpp): for the 3-SAT formula lits[3 m] (var << 1 |
+// neg) with term starts vst[n + 1], nl lanes of cpl clause slots and term blocks 0 .. blk_cap - 1:
+// slot_clause[nl cpl] (clause or -1), slot_order[3 nl cpl] (the clause's literal index 0..2 at each
+// position),
+// blk[n + 1] (each variable's block, blk[n] the zero block), and the bank model's LDS cycles of the
+// plain and the chosen layout.  false: no layout (the caller keeps k_solo_fast).
+bool cv_layout(int64_t n, int64_t m, const int32_t *lits, const int32_t *vst, int nl, int cpl, int tsize, int blk_cap,
+               int iters, std::vector<int32_t> &slot_clause, std::vector<int32_t> &slot_order,
+               std::vector<int32_t> &blk, int64_t *cost_plain, int64_t *cost_opt);
+
+}  // namespace odesat

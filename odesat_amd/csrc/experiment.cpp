@@ -30,6 +30,7 @@ const char *const KNOBS[] = {
     "SOLO_LANES",       // k_solo lanes per replica (a multiple of 64)
     "SOLO_FAST",        // 0: k_solo's general arithmetic on in-range states
     "SOLO_CV",          // 0: k_solo_fast instead of k_solo_cv (clause-held voltages) on in-range states
+    "CV_ITERS",         // k_solo_cv layout search steps (cv_layout.cpp; 0: the plain layout)
     "RES_NARROW",       // 1 / 0: k_resident with one wave (64-clause tiles) per replica / never
     "RES_FAST",         // 0: k_resident's general arithmetic on 3-SAT
     "RES_RC",           // 0: no register-cached tiles in the f64 k_resident

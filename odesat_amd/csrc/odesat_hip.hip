@@ -74,6 +74,11 @@ struct odesat_solver {
     int solo_nl = 64, solo_cpl = 1, solo_vpl = 1;  // k_solo: lanes per replica, clause / variable slots per lane
     bool solo_fast = true;      // k_solo's short arithmetic on in-range states (ODESAT_SOLO_FAST=0: the general form)
     bool solo_cv = true;        // k_solo_cv (clause-held voltages) for the short arithmetic when it fits
+    bool solo_cv_z0 = false;    // the formula has variables of degree 0 (k_solo_cv's variable slots)
+    int4 *cv_rec = nullptr;     // [solo_nl solo_cpl] k_solo_cv's per-slot records (cv_layout.cpp)
+    int32_t *cv_blk = nullptr;  // [n + 1] k_solo_cv's term block per variable (n: the zero block)
+    int32_t cv_nb = 0;          // blocks in use
+    int64_t cv_cost_plain = 0, cv_cost = 0;  // the bank model's LDS cycles per pass, plain / chosen layout
     bool wave_fast = true;      // k_wave's likewise (ODESAT_WAVE_FAST=0)
     bool res_fast = true;       // k_resident's likewise, 3-SAT only (ODESAT_RES_FAST=0)
     bool res_rc = true;         // f64 fixed steps: register-cached tiles (resident.hpp; ODESAT_RES_RC=0)
@@ -806,7 +811,7 @@ template <typename T, bool ADA, int CPL, int VPL, bool FAST> int launch_solo_k(o
 }
 
 template <typename T, bool ADA, int CPL, int VPL> int launch_solo_cv_k(odesat_solver *s, WArgs<T> a) {
-    const size_t lds = solo_cv_elems(s->n, sizeof(T)) * sizeof(T);
+    const size_t lds = 2 * (size_t)SOLO_CV_AREA;
     const unsigned grid = (unsigned)s->G, block = (unsigned)s->solo_nl;
     if (block > (unsigned)SOLO_CV_MAX_NL) return fail(ODESAT_EINVAL, "k_solo_cv: too many lanes");
     HIP_TRY((solo_cv_launch<T, ADA, CPL, VPL>(true, a, grid, block, lds, (int)RES_LDS_MAX, s->stream)));
@@ -848,12 +853,18 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     a.tol = tol;
     a.io = take_io(s);
     a.G = s->G;
+    a.cvrec = s->cv_rec;
+    a.cvblk = s->cv_blk;
+    a.cvnb = s->cv_nb;
     if (s->solo) {
         auto so = [&](auto cc, auto vv) -> int {
             constexpr int CPL = decltype(cc)::value, VPL = decltype(vv)::value;
             if constexpr (CPL <= 2)
-                if (fast && s->solo_fast && s->solo_cv)
+                if (fast && s->solo_fast && s->solo_cv) {
+                    if (!s->solo_cv_z0)  // no variable of degree 0: no variable slots
+                        return adaptive ? launch_solo_cv_k<T, true, CPL, 0>(s, a) : launch_solo_cv_k<T, false, CPL, 0>(s, a);
                     return adaptive ? launch_solo_cv_k<T, true, CPL, VPL>(s, a) : launch_solo_cv_k<T, false, CPL, VPL>(s, a);
+                }
             if (fast && s->solo_fast)
                 return adaptive ? launch_solo_k<T, true, CPL, VPL, true>(s, a) : launch_solo_k<T, false, CPL, VPL, true>(s, a);
             return adaptive ? launch_solo_k<T, true, CPL, VPL, false>(s, a) : launch_solo_k<T, false, CPL, VPL, false>(s, a);
@@ -1228,7 +1239,8 @@ extern "C" void odesat_solver_destroy(odesat_solver *s) {
     for (auto e : s->pool) (void)hipEventDestroy(e);
     void *ptrs[] = {s->cptr, s->lits, s->wpos, s->vptr, s->pc, s->ps, s->empty, s->inc, s->v[0], s->v[1], s->c[0],
                     s->c[1], s->par, s->w, s->vh, s->vf, s->ch, s->cf, s->dtr, s->err, s->unsat, s->act,
-                    s->sat_step, s->stop, s->res_tc, s->res_tcw, s->cmap, s->res_cl4, s->oc_rec, s->oc_rec12, s->oc_tcp, s->wv_rec4, s->wv_vst};
+                    s->sat_step, s->stop, s->res_tc, s->res_tcw, s->cmap, s->res_cl4, s->oc_rec, s->oc_rec12, s->oc_tcp, s->wv_rec4, s->wv_vst,
+                    s->cv_rec, s->cv_blk};
     for (void *p : ptrs) dfree(p);
     void *snaps[] = {s->snap_par, s->snap_sat, s->snap_done, s->snap_dt, s->ck_v, s->ck_c, s->ck_dt, s->ck_par,
                      s->ck_act, s->ck_sat, s->ck_done, s->ck_stop};
@@ -1529,9 +1541,36 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             // 512 lanes, no variable with more terms than a padded block holds, and its two term
             // areas in LDS.  The SOLO_CV knob (0) turns it off.
             int64_t dmax = 0;
-            for (int64_t i = 0; i < n; ++i) dmax = std::max<int64_t>(dmax, vst[i + 1] - vst[i]);
-            s->solo_cv = s->solo_cpl <= 2 && nl <= SOLO_CV_MAX_NL && dmax <= SOLO_DPAD &&
-                         solo_cv_elems(n, s->tsize) * s->tsize <= RES_LDS_MAX && odesat::xp_get("SOLO_CV", 1) != 0;
+            s->solo_cv_z0 = false;
+            for (int64_t i = 0; i < n; ++i) {
+                dmax = std::max<int64_t>(dmax, vst[i + 1] - vst[i]);
+                s->solo_cv_z0 = s->solo_cv_z0 || vst[i + 1] == vst[i];
+            }
+            s->solo_cv = s->solo && s->solo_cpl <= 2 && nl <= SOLO_CV_MAX_NL && dmax <= SOLO_DPAD &&
+                         n + 1 <= solo_cv_blk_cap(s->tsize) && odesat::xp_get("SOLO_CV", 1) != 0;
+            if (s->solo_cv) {  // the lanes' clauses and the term blocks (cv_layout.cpp; knob CV_ITERS = 0: plain)
+                const int nslot = (int)nl * s->solo_cpl;
+                std::vector<int32_t> sc, so, blk;
+                const int iters = (int)odesat::xp_get("CV_ITERS", 20000);
+                s->solo_cv = odesat::cv_layout(n, m, lits.data(), vst.data(), (int)nl, s->solo_cpl, (int)s->tsize,
+                                               solo_cv_blk_cap(s->tsize), iters, sc, so, blk, &s->cv_cost_plain,
+                                               &s->cv_cost);
+                if (s->solo_cv) {
+                    std::vector<int4> cr((size_t)nslot);
+                    for (int t = 0; t < nslot; ++t) {
+                        const int c = sc[t] >= 0 ? sc[t] : 0;
+                        const int f[3] = {rec4[c].x, rec4[c].y, rec4[c].z};
+                        cr[t] = make_int4(f[so[3 * t]], f[so[3 * t + 1]], f[so[3 * t + 2]], sc[t]);
+                    }
+                    s->cv_nb = 1 + *std::max_element(blk.begin(), blk.end());
+                    if ((rc = dmalloc(s, (void **)&s->cv_rec, (size_t)nslot * 16)) ||
+                        (rc = dmalloc(s, (void **)&s->cv_blk, (n + 1) * 4)))
+                        return bail(rc);
+                    if (hipMemcpy(s->cv_rec, cr.data(), (size_t)nslot * 16, hipMemcpyHostToDevice) != hipSuccess ||
+                        hipMemcpy(s->cv_blk, blk.data(), (n + 1) * 4, hipMemcpyHostToDevice) != hipSuccess)
+                        return bail(fail(ODESAT_EDEVICE, "topology upload failed"));
+                }
+            }
             s->wave_fast = odesat::xp_get("WAVE_FAST", 1) != 0;
         }
         if ((rc = onchip_setup(s, tiles, wst, lits))) return bail(rc);

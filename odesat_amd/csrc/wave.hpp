@@ -45,6 +45,12 @@ template <typename T> struct WArgs {
     T dt, zeta, xl_max;
     double tol;
     CallIO io;  // per-call bookkeeping (callio.hpp)
+    // k_solo_cv's layout (cv_layout.cpp): per clause slot l + k NL its record (the literals' rec4 fields
+    // in the chosen order, w = the clause or -1), each variable's term block (cvblk[n]: the zero block),
+    // and the blocks in use (the lanes' sink words follow)
+    const int4 *__restrict__ cvrec;
+    const int32_t *__restrict__ cvblk;
+    int32_t cvnb;
 };
 
 // LDS bytes of one replica: v, its full-step clone (adaptive), the terms, the memories and (adaptive)
@@ -125,8 +131,10 @@ __device__ __forceinline__ bool clause_math(const int (&lit)[3], const T (&v)[3]
 
 // The max of x over the wave (all 64 lanes active), uniform: a DPP butterfly within each quad, row
 // rotations within each row of 16, then the four rows' maxima by readlane.
+// (bound_ctrl with old = 0: every lane has a source under these controls, and the form lets the
+// compiler fold the move into one v_max_u32_dpp instead of a copy, a v_mov_b32_dpp and the max)
 template <int CTRL> __device__ __forceinline__ uint32_t max_dpp(uint32_t x) {
-    return max(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, 0xf, 0xf, false));
+    return max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, true));
 }
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
     x = max_dpp<0xB1>(x);   // quad_perm [1, 0, 3, 2]
@@ -955,16 +963,24 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
 // lanes.  Per step: fixed 1 barrier (k_solo_fast 2), adaptive 2 (4).
 //   * LDS banks: a block's 16-byte reads from random variables conflict.  Blocks are SOLO_CV_BS
 //     slots apart (one 16-byte pad: 80 bytes in f64, 48 in f32), so a block's bank set is one of 16
-//     instead of 4; and a read past the variable's degree goes to one shared block of zeros (every
-//     lane on it reads the same address: no conflict) instead of the block's +0 padding.
+//     instead of 4; a read past the variable's degree, and every read of a slot without a clause,
+//     goes to one shared block of zeros (every lane on it reads the same address: no conflict)
+//     instead of the block's +0 padding; and the host places the clauses on lanes, orders each
+//     clause's literals and places the blocks so that the lanes of a read's 16-lane groups meet few
+//     shared bank sets (cv_layout.cpp).
 //   * The two passes (and consecutive fixed steps) use two term areas, so a pass's stores never meet
 //     the previous pass's reads: a slow lane's reads of area A finish before it reaches the barrier
 //     that the next writer of A must pass first.
-//   * Between barriers the step is one basic block: the adaptive step computes its update whether or
-//     not the replica is allsat and commits it by select (an allsat replica takes no step, :122), a
-//     clause slot past m stores its terms to a sink word of its own lane, and the fold adds every
-//     padded slot.  So the term reads go out right after the barrier, under the dt update's divide
-//     and square root (system.rs:133-135) and the vote, instead of after them.
+//   * The region after the first barrier has no branch: the adaptive step computes its first half
+//     whether or not the replica is allsat (only the second half, after the second barrier, commits,
+//     under the uniform vote: an allsat replica takes no step, :122), a clause slot past m stores its
+//     terms to a sink word of its own lane, and the fold adds every padded slot.  So the term reads
+//     go out right after the barrier, under the dt update's divide and square root (system.rs:133-135)
+//     and the vote, instead of after them.
+//   * Instruction count (the step is VALU-issue bound: ~300 instructions per wave per adaptive step
+//     at ~4 cycles, PMC): the two areas sit SOLO_CV_AREA bytes apart, so one set of address VGPRs
+//     serves both (the ds offset field); a literal's value 1 - q v is one fma with q v exact (=
+//     solo_terms' 1 - flip(v)); VPL = 0 drops the degree-0 code when the formula has none.
 //   * The adaptive error's wave max and LDS atomic max run after the second barrier and are read after
 //     the next step's first.
 //   * Variables of degree 0 (no clause holds them) belong to variable slots l, l + NL, ... that apply
@@ -975,15 +991,15 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo_fast(WArgs<T> a) {
 // in f64).
 // ------------------------------------------------------------------------------------------------
 constexpr int SOLO_CV_MAX_NL = 512;
+constexpr uint32_t SOLO_CV_AREA = 32768;  // bytes per term area: the second at a static offset (the ds
+                                          // instructions' immediate), so both share the address VGPRs
 
-// LDS elements of one k_solo_cv term area: n padded blocks of SOLO_CV_BS slots, the zero block, then a
-// sink word per lane
+// A k_solo_cv term area: blocks of SOLO_CV_BS slots (the variables' and the zero block, placed by
+// cv_layout.cpp), then a sink word per lane; the blocks that fit SOLO_CV_AREA bytes
 __host__ __device__ constexpr int solo_cv_bs(size_t tsize) { return SOLO_DPAD + 16 / (int)tsize; }
-__host__ __device__ inline size_t solo_cv_area(int64_t n, size_t tsize) {
-    const int64_t per16 = 16 / (int64_t)tsize;
-    return (size_t)(((n + 1) * solo_cv_bs(tsize) + SOLO_CV_MAX_NL + per16 - 1) / per16 * per16);
+__host__ __device__ constexpr int solo_cv_blk_cap(size_t tsize) {
+    return ((int)(SOLO_CV_AREA / tsize) - SOLO_CV_MAX_NL) / solo_cv_bs(tsize);
 }
-__host__ __device__ inline size_t solo_cv_elems(int64_t n, size_t tsize) { return 2 * solo_cv_area(n, tsize); }
 
 template <typename T, bool ADAPTIVE, int CPL, int VPL>
 __global__ __launch_bounds__(SOLO_CV_MAX_NL) void k_solo_cv(WArgs<T> a) {
@@ -1001,48 +1017,54 @@ __global__ __launch_bounds__(SOLO_CV_MAX_NL) void k_solo_cv(WArgs<T> a) {
     if (a.stop_mode == ODESAT_STOP_ANY && *a.stop < a.step0) return;  // an earlier step stopped every replica
     if (g >= a.G || !io_active(a.io, a.act, g)) return;                // uniform per workgroup
     const int n = a.n, m = a.m;
-    const int area = (int)solo_cv_area(n, sizeof(T));
-    T *P0 = reinterpret_cast<T *>(wave_smem);  // pass 1 / even fixed steps
-    T *P1 = P0 + area;                         // pass 2 / odd fixed steps
-    for (int i = l; i < (n + 1) * BS; i += NL) {
-        P0[i] = (T)0.0;
-        P1[i] = (T)0.0;
+    {
+        T *P0 = reinterpret_cast<T *>(wave_smem), *P1 = reinterpret_cast<T *>(wave_smem + SOLO_CV_AREA);
+        for (int i = l; i < a.cvnb * BS; i += NL) {
+            P0[i] = (T)0.0;
+            P1[i] = (T)0.0;
+        }
     }
     const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;
     const T *V = (p ? a.v1 : a.v0) + (size_t)g * n;
     const T *CM = (p ? a.c1 : a.c0) + (size_t)g * m * 2;
-    const int mlast = m - 1, nlast = n - 1;
-    int vi[CPL][3], tp[CPL][3];  // variable and term slot of each literal
-    int ra[CPL][3][NB];          // the element read by each 16-byte read of its block (the zero block past the degree)
+    int ci[CPL];                  // the slot's clause (-1: none)
+    int vi[CPL][3];               // variable of each literal
+    uint32_t tp[CPL][3];          // byte offset of its term slot in an area (a slot past m: its lane's sink word)
+    uint32_t ra[CPL][3][NB];      // byte offset of each 16-byte read of its block (the zero block past the degree)
     uint32_t sg[CPL][3];
-    bool ok[CPL], own[CPL][3];  // a clause slot below m; the literal is its variable's first incidence
+    T nq[CPL][3];                 // -q_j: 1 for a negated literal, -1 otherwise (val = 1 - q v = fma(nq, v, 1))
+    bool ok[CPL], own[CPL][3];    // a clause slot below m; the literal is its variable's first incidence
     T vv[CPL][3], xs[CPL], xl[CPL];
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
-        ok[k] = l + k * NL < m;
-        const int c = min(l + k * NL, mlast);
-        const int4 r4 = a.rec4[c];
+        const int4 r4 = a.cvrec[l + k * NL];  // (a slot without a clause: clause 0's literals, w = -1)
+        ci[k] = r4.w;
+        ok[k] = r4.w >= 0;
+        const int c = ok[k] ? r4.w : 0;
         const int lit[3] = {r4.x & 0xffff, r4.y & 0xffff, r4.z & 0xffff};
         const int pos[3] = {(int)((uint32_t)r4.x >> 16), (int)((uint32_t)r4.y >> 16), (int)((uint32_t)r4.z >> 16)};
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             const int v = lit[j] >> 1, rank = pos[j] - a.vst[v], deg = a.vst[v + 1] - a.vst[v];
+            const int b = a.cvblk[v], zb = a.cvblk[n];
             vi[k][j] = v;
-            tp[k][j] = ok[k] ? v * BS + rank : (n + 1) * BS + l;  // (rank < SOLO_DPAD: host selection)
+            tp[k][j] = (uint32_t)(ok[k] ? b * BS + rank : a.cvnb * BS + l) * (uint32_t)sizeof(T);  // (rank < SOLO_DPAD: host)
 #pragma unroll
-            for (int q = 0; q < NB; ++q) ra[k][j][q] = (q * PER16 < deg ? v : n) * BS + q * PER16;
+            for (int q = 0; q < NB; ++q)
+                ra[k][j][q] = (uint32_t)((ok[k] && q * PER16 < deg ? b : zb) * BS + q * PER16) * (uint32_t)sizeof(T);
             sg[k][j] = (lit[j] & 1) ? 0x80000000u : 0u;
+            nq[k][j] = (lit[j] & 1) ? (T)1.0 : (T)-1.0;
             own[k][j] = ok[k] && rank == 0;
             vv[k][j] = V[v];
         }
         xs[k] = CM[2 * c];
         xl[k] = CM[2 * c + 1];
     }
-    bool z0[VPL];  // variable slots of degree 0
-    T vr[VPL];
+    bool z0[VPL > 0 ? VPL : 1];  // variable slots of degree 0 (VPL = 0: the formula has none)
+    T vr[VPL > 0 ? VPL : 1];
 #pragma unroll
     for (int j = 0; j < VPL; ++j) {
-        const int i = l + j * NL, ii = min(i, nlast);
+        const int i = l + j * NL, ii = min(i, n - 1);
         z0[j] = i < n && a.vst[ii + 1] == a.vst[ii];
         vr[j] = V[ii];
     }
@@ -1067,16 +1089,22 @@ __global__ __launch_bounds__(SOLO_CV_MAX_NL) void k_solo_cv(WArgs<T> a) {
         for (int j = 0; j < SOLO_CV_MAX_NL / 256; ++j) r |= r4[j].x | r4[j].y | r4[j].z | r4[j].w;
         return r != 0;
     };
-    // a pass's clause arithmetic at voltages x with memories (txs, txl): terms into area A (a slot past
-    // m into its lane's sink word), mn into mn_o; unsat
-    auto terms = [&](const T (&x)[CPL][3], const T (&txs)[CPL], const T (&txl)[CPL], T *A, T (&mn_o)[CPL]) -> bool {
+    // a pass's clause arithmetic (solo_terms' expressions, the literal's sign by fma: 1 - q v with q v
+    // exact) at voltages x with memories (txs, txl): terms into the area at byte offset OFF, mn into
+    // mn_o; unsat
+    auto terms = [&](auto off_c, const T (&x)[CPL][3], const T (&txs)[CPL], const T (&txl)[CPL], T (&mn_o)[CPL]) -> bool {
+        constexpr uint32_t OFF = decltype(off_c)::value;
         bool uns = false;
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
-            T d[3];
-            mn_o[k] = solo_terms<T>(x[k], sg[k], txl[k] * txs[k], d);
+            const T tt = txl[k] * txs[k];
+            const T val0 = fma(nq[k][0], x[k][0], (T)1.0), val1 = fma(nq[k][1], x[k][1], (T)1.0),
+                    val2 = fma(nq[k][2], x[k][2], (T)1.0);  // :47
+            const T sel[3] = {dmin(val1, val2), dmin(val0, val2), dmin(val0, val1)};
+            mn_o[k] = dmin(sel[2], val2);  // :49-57
 #pragma unroll
-            for (int j = 0; j < 3; ++j) A[tp[k][j]] = d[j];
+            for (int j = 0; j < 3; ++j)
+                *reinterpret_cast<T *>(wave_smem + tp[k][j] + OFF) = sflip(tt * sel[j], sg[k][j]);  // 2 xl xs G (:64-70, :80)
             uns = uns || (ok[k] && !(mn_o[k] < (T)0.5));  // :88
         }
         return uns;
@@ -1084,14 +1112,15 @@ __global__ __launch_bounds__(SOLO_CV_MAX_NL) void k_solo_cv(WArgs<T> a) {
     struct Blocks {
         TV t[CPL][3][NB];
     };
-    auto reads = [&](const T *A) {  // every literal's padded block
+    auto reads = [&](auto off_c) {  // every literal's padded block in the area at byte offset OFF
+        constexpr uint32_t OFF = decltype(off_c)::value;
         Blocks r;
 #pragma unroll
         for (int k = 0; k < CPL; ++k)
 #pragma unroll
             for (int j = 0; j < 3; ++j)
 #pragma unroll
-                for (int q = 0; q < NB; ++q) r.t[k][j][q] = *reinterpret_cast<const TV *>(A + ra[k][j][q]);
+                for (int q = 0; q < NB; ++q) r.t[k][j][q] = *reinterpret_cast<const TV *>(wave_smem + ra[k][j][q] + OFF);
         return r;
     };
     // 2 dv of every literal's variable: the reference's left fold of the 2x terms (:33, :80).  Every
@@ -1111,6 +1140,8 @@ __global__ __launch_bounds__(SOLO_CV_MAX_NL) void k_solo_cv(WArgs<T> a) {
     };
     auto clamp1 = [](T x) { return dmin(dmax(x, (T)-1.0), (T)1.0); };
     const T zero = (T)0.0 + (T)0.0;  // 2 dv of a variable without terms (k_solo_fast's fold of a +0 block)
+    using A0 = std::integral_constant<uint32_t, 0>;
+    using A1 = std::integral_constant<uint32_t, SOLO_CV_AREA>;
     T mn1[CPL], mn2[CPL];
     auto dt_next = [&](int k) { return dmax(dmin(dtr * dsqrt((T)a.tol / frombits(errM[k & 1])), (T)1e3), (T)0.0078125); };
     bool pend = false;  // the previous step was taken and its dt update is still due
@@ -1119,19 +1150,28 @@ __global__ __launch_bounds__(SOLO_CV_MAX_NL) void k_solo_cv(WArgs<T> a) {
     uint64_t st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = solo_memtime();
 #endif
-    for (int k = 0; k < a.nsteps; ++k) {
-        const int step = a.step0 + k;
-        klast = k;
-        bool uns;
-        if (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
-            const T h = dtr, hh = (T)0.5 * h;
-            T *A = (k & 1) ? P1 : P0;
-            vote(terms(vv, xs, xl, A, mn1), k);
+    // the bookkeeping after step k (uns: some clause unsat); false: the replica stops
+    auto book = [&](int k, bool uns) {
+        done += 1;
+        if (!uns) {  // allsat: the fixed step was still taken (:148-152); adaptive took none
+            const int step = a.step0 + k;
+            if (sat < 0) sat = step;
+            if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                            // simulate() breaks (:193)
+            if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
+        }
+        SOLO_STAMP(5);
+        return act != 0;
+    };
+    if constexpr (!ADAPTIVE) {  // euler_step_fixed (system.rs:141-154): the update is taken regardless
+        const T h = dtr, hh = (T)0.5 * h;
+        // one step with its terms in the area at OFF (steps alternate areas: unrolled by two)
+        auto step = [&](auto off_c, int k) {
+            vote(terms(off_c, vv, xs, xl, mn1), k);
             SOLO_STAMP(0);
             __syncthreads();  // the terms (and the votes) before the fold
             SOLO_STAMP(1);
-            const Blocks r = reads(A);
-            uns = votes(k);
+            const Blocks r = reads(off_c);
+            const bool uns = votes(k);
 #pragma unroll
             for (int c = 0; c < CPL; ++c) solo_mem<T>(xs[c], xl[c], mn1[c], hh, h, a.xl_max, xs[c], xl[c]);
             T dv[CPL][3];
@@ -1146,18 +1186,29 @@ __global__ __launch_bounds__(SOLO_CV_MAX_NL) void k_solo_cv(WArgs<T> a) {
                 vr[j] = z0[j] ? x : vr[j];
             }
             SOLO_STAMP(2);
-        } else {  // euler_step (:111-139)
-            vote(terms(vv, xs, xl, P0, mn1), k);  // the RHS at y, y's memories
+            return book(k, uns);
+        };
+        for (int k = 0; k < a.nsteps; k += 2) {
+            if (!step(A0{}, k)) break;
+            if (k + 1 < a.nsteps && !step(A1{}, k + 1)) break;
+        }
+    } else {  // euler_step (:111-139)
+        for (int k = 0; k < a.nsteps; ++k) {
+            klast = k;
+            vote(terms(A0{}, vv, xs, xl, mn1), k);  // the RHS at y, y's memories
             SOLO_STAMP(0);
             __syncthreads();  // B1: the first pass's terms, the votes, the previous step's error
             SOLO_STAMP(1);
             const T nd = dt_next(k - 1);  // (its read first: the divide starts under the blocks' reads)
-            const Blocks r1 = reads(P0);
-            uns = votes(k);
-            const bool go = uns;  // an allsat replica takes no step (:122): the update below is discarded
+            const Blocks r1 = reads(A0{});
+            const bool uns = votes(k);
+            const bool go = uns;  // an allsat replica takes no step (:122)
             dtr = pend ? nd : dtr;
             const T h = dtr, hh = (T)0.5 * h, hq = (T)0.25 * h;
-            T xsf[CPL], xlf[CPL], xsh[CPL], xlh[CPL], vf[CPL][3], vh[CPL][3], vf0[VPL], vh0[VPL];
+            // the first half of the step whether or not the replica is allsat (so the reads above go
+            // out right after B1); only the second half, after B2, commits
+            T xsf[CPL], xlf[CPL], xsh[CPL], xlh[CPL], vf[CPL][3], vh[CPL][3];
+            T vf0[VPL > 0 ? VPL : 1], vh0[VPL > 0 ? VPL : 1];
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {  // the memories' full-step clone and first half step (:124-128)
                 solo_mem<T>(xs[c], xl[c], mn1[c], hh, h, a.xl_max, xsf[c], xlf[c]);
@@ -1177,54 +1228,48 @@ __global__ __launch_bounds__(SOLO_CV_MAX_NL) void k_solo_cv(WArgs<T> a) {
                 vf0[j] = clamp1(vr[j] + hh * zero);
                 vh0[j] = clamp1(vr[j] + hq * zero);
             }
-            terms(vh, xsh, xlh, P1, mn2);  // the RHS at the half step
+            terms(A1{}, vh, xsh, xlh, mn2);  // the RHS at the half step
             SOLO_STAMP(2);
             __syncthreads();  // B2: the second pass's terms
             SOLO_STAMP(3);
-            const Blocks r2 = reads(P1);
-            T e = (T)0.0;
+            if (go) {  // (uniform)
+                const Blocks r2 = reads(A1{});
+                T ec[CPL];  // each slot's max_error terms (a slot past m does not count)
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) {  // second half step of the memories (:130), max_error (:132)
-                T xsn, xln;
-                solo_mem<T>(xsh[c], xlh[c], mn2[c], hq, hh, a.xl_max, xsn, xln);
-                const T ec = dmax(e, dmax(dabs(xsf[c] - xsn), dabs(xlf[c] - xln)));
-                e = ok[c] ? ec : e;
-                xs[c] = go ? xsn : xs[c];
-                xl[c] = go ? xln : xl[c];
-            }
-            fold(r2, dv);
-#pragma unroll
-            for (int c = 0; c < CPL; ++c)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    const T vn = clamp1(vh[c][j] + hq * dv[c][j]);  // second half step
-                    const T ev = dmax(e, dabs(vf[c][j] - vn));       // :101-108
-                    e = ok[c] ? ev : e;
-                    vv[c][j] = go ? vn : vv[c][j];
+                for (int c = 0; c < CPL; ++c) {  // second half step of the memories (:130), max_error (:132)
+                    T xsn, xln;
+                    solo_mem<T>(xsh[c], xlh[c], mn2[c], hq, hh, a.xl_max, xsn, xln);
+                    ec[c] = dmax(dabs(xsf[c] - xsn), dabs(xlf[c] - xln));
+                    xs[c] = xsn;
+                    xl[c] = xln;
                 }
+                fold(r2, dv);
 #pragma unroll
-            for (int j = 0; j < VPL; ++j) {
-                const T vn = clamp1(vh0[j] + hq * zero);
-                const T ev = dmax(e, dabs(vf0[j] - vn));
-                e = z0[j] ? ev : e;
-                vr[j] = z0[j] && go ? vn : vr[j];
+                for (int c = 0; c < CPL; ++c)
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) {
+                        const T vn = clamp1(vh[c][j] + hq * dv[c][j]);  // second half step
+                        ec[c] = dmax(ec[c], dabs(vf[c][j] - vn));        // :101-108
+                        vv[c][j] = vn;
+                    }
+                T e = (T)0.0;  // (the max of finite non-negative terms: any order)
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) e = ok[c] ? dmax(e, ec[c]) : e;
+#pragma unroll
+                for (int j = 0; j < VPL; ++j) {
+                    const T vn = clamp1(vh0[j] + hq * zero);
+                    const T ev = dmax(e, dabs(vf0[j] - vn));
+                    e = z0[j] ? ev : e;
+                    vr[j] = z0[j] ? vn : vr[j];
+                }
+                const U eb = wave_max_bits(tobits(e));  // non-negative floats order as their bits
+                if ((l & 63) == 0) atomicMax(&errM[k & 1], eb);  // read after the next step's B1
             }
-            const U eb = wave_max_bits(tobits(e));  // non-negative floats order as their bits
-            if ((l & 63) == 0) atomicMax(&errM[k & 1], eb);  // read after the next step's B1 (when go)
-            if (l == 0) errM[(k + 1) & 1] = 0;              // the previous step's error was read before B2
+            if (l == 0) errM[(k + 1) & 1] = 0;  // the previous step's error was read before B2
             pend = go;
             SOLO_STAMP(4);
+            if (!book(k, uns)) break;
         }
-        done += 1;
-        if (!uns) {  // allsat: the fixed step was still taken (:148-152); adaptive took none
-            if (sat < 0) sat = step;
-            if (a.stop_mode == ODESAT_STOP_EACH) act = 0;                            // simulate() breaks (:193)
-            if (a.stop_mode == ODESAT_STOP_ANY && l == 0) atomicMin(a.stop, step);  // simulate_inter (:291)
-        }
-        SOLO_STAMP(5);
-        if (!act) break;  // uniform
-    }
-    if (ADAPTIVE) {
         __syncthreads();  // the last step's atomic max
         if (pend) dtr = dt_next(klast);
     }
@@ -1244,13 +1289,11 @@ __global__ __launch_bounds__(SOLO_CV_MAX_NL) void k_solo_cv(WArgs<T> a) {
     for (int j = 0; j < VPL; ++j)
         if (z0[j]) Vo[l + j * NL] = vr[j];
 #pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-        const int c = l + k * NL;
-        if (c < m) {
-            CMo[2 * c] = xs[k];
-            CMo[2 * c + 1] = xl[k];
+    for (int k = 0; k < CPL; ++k)
+        if (ok[k]) {
+            CMo[2 * ci[k]] = xs[k];
+            CMo[2 * ci[k] + 1] = xl[k];
         }
-    }
     if (l == 0) {
         if (a.oop) a.par[g] = (uint8_t)q;
         a.act[g] = (uint8_t)act;

@@ -67,9 +67,9 @@ SOLO_SHAPES(double)
 #define SOLO_CV_ONE(T, A, C, V)                                                                          \
     template hipError_t solo_cv_launch<T, A, C, V>(bool, const WArgs<T> &, unsigned, unsigned, size_t, int, \
                                                    hipStream_t);
-#define SOLO_CV_SHAPES(T) SOLO_CV_ONE(T, false, 1, 1) SOLO_CV_ONE(T, true, 1, 1) SOLO_CV_ONE(T, false, 1, 2) \
-    SOLO_CV_ONE(T, true, 1, 2) SOLO_CV_ONE(T, false, 2, 1) SOLO_CV_ONE(T, true, 2, 1) SOLO_CV_ONE(T, false, 2, 2) \
-    SOLO_CV_ONE(T, true, 2, 2)
+#define SOLO_CV_FA(T, C, V) SOLO_CV_ONE(T, false, C, V) SOLO_CV_ONE(T, true, C, V)
+#define SOLO_CV_SHAPES(T) SOLO_CV_FA(T, 1, 0) SOLO_CV_FA(T, 1, 1) SOLO_CV_FA(T, 1, 2) SOLO_CV_FA(T, 2, 0) \
+    SOLO_CV_FA(T, 2, 1) SOLO_CV_FA(T, 2, 2)
 SOLO_CV_SHAPES(float)
 SOLO_CV_SHAPES(double)
 

@@ -12,7 +12,7 @@ extra=""; [ "$src" = onchip ] && extra="-fno-slp-vectorize -mllvm -amdgpu-sched-
 [ "$src" = wave_k ] && extra="-mllvm -amdgpu-sched-strategy=max-ilp"  # (WAVE_FLAGS)
 $H $extra $flags -c -o build/vobj/$name/$src.o odesat_amd/csrc/$src.hip
 objs=""
-for o in odesat_hip onchip wave_k partition cnf preprocess stoch run_abi experiment; do
+for o in odesat_hip onchip wave_k partition cnf preprocess stoch run_abi experiment cv_layout; do
   if [ "$o" = "$src" ]; then objs="$objs build/vobj/$name/$o.o"; else objs="$objs build/obj/$o.o"; fi
 done
 $H -shared -fPIC -o expt/lib$name.so $objs
