@@ -18,6 +18,9 @@ the same way (barrier + device sync around K steps, max over ranks) with its own
   adaptive       config 2, B=1024, adaptive step tol 1e-3 (the reference's default mode, system.rs:111-139)
   f64_adaptive   config 2, B=1024, f64 and adaptive steps together (the reference CLI's defaults)
   config3        BASELINE configs[2]: uf250-1065-style n=250 m=1065, adaptive tol 1e-3, B=1024 (k_wave)
+  criterion      the reference's criterion benches (benches/benchmarks.rs:25-51, BASELINE configs[0]'s
+                 tests/hard.cnf): ONE replica, f64, 10 000 steps per call, "adaptive hard" (tol 0.01) and
+                 "fixed hard" (dt 0.01), milliseconds per call (a latency, lower is better; k_solo_cv)
   inter          config 2 under STOP_ANY (simulate_inter)
   inter_config4  config 4 (n=50k, m=210k), B=1024 per rank, the sharded inter protocol
                  (sharding.run_inter: lock-step chunks, MIN all-reduce of the stop step, rollback) --
@@ -53,7 +56,7 @@ VALU_PEAK_GINST = 1024 * 2.4e9 / 2 / 1e9
 # LDS instruction issue: one LDS (DS) wave instruction per CU per cycle at 2.4 GHz (an upper bound: a
 # wave64 DS access of 4-byte words moves 256 B, two cycles of the 128 B/clk LDS, MI355X_MICROARCH.md)
 LDS_PEAK_GINST = 256 * 2.4e9 / 1e9
-LEGS = ("f64", "adaptive", "f64_adaptive", "config3", "inter", "config4", "config5", "extra", "ab")
+LEGS = ("f64", "adaptive", "f64_adaptive", "config3", "criterion", "inter", "config4", "config5", "extra", "ab")
 CLAUSES_TOL = 1e-5       # the CLAUSES partitions' stated tolerance against a world-1 run
 DIGEST_REPLICAS = 4      # inter_config4: replicas per rank re-integrated by rank 0
 # config 5: the measured floor of a step's random accesses at world 1
@@ -620,6 +623,32 @@ def main():
 
     if "config3" in legs and args.config == "config2" and args.dtype == "f32":
         leg("config3", config3_leg)
+
+    def criterion_leg(calls=5, steps=10_000):  # benches/benchmarks.rs:25-51 on tests/hard.cnf (scripts/bench_criterion.py)
+        from odesat_amd import cnf as cnf_
+        with open(os.path.join(ROOT, "tests", "golden", "hard.cnf")) as fh:
+            _, fh_ = cnf_.normalize_cnf_variables(cnf_.parse_dimacs_format(fh.read()))
+        out = {"unit": "ms per call", "higher_is_better": False, "dtype": "fp64", "batch": 1,
+               "steps_per_call": steps, "calls": calls,
+               "workload": "the reference's criterion benches: tests/hard.cnf (n=100, m=160, UNSAT: every call "
+                           "runs all its steps), one replica whose state carries over between calls, after one "
+                           "untimed call; max over ranks"}
+        for name, kw in (("adaptive_hard", dict(adaptive=True, tol=0.01)), ("fixed_hard", dict(adaptive=False, dt=0.01))):
+            with Solver(fh_, 1, "f64", device=local) as s:
+                out["kernel"] = s.step_kernel(kw["adaptive"])
+                s.init_state(42)
+                s.simulate(max_steps=steps, stop=ODESAT_STOP_NONE, poll_interval=steps, **kw)
+                s.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(calls):
+                    s.simulate(max_steps=steps, stop=ODESAT_STOP_NONE, poll_interval=steps, **kw)
+                s.synchronize()
+                ms_ = (time.perf_counter() - t0) * 1e3 / calls
+            out[name + "_ms_per_call"] = max_over_ranks(dist, ms_)
+        res["criterion"] = out
+
+    if "criterion" in legs and args.config == "config2" and args.dtype == "f32":
+        leg("criterion", criterion_leg)
 
     def inter_leg():  # simulate_inter (STOP_ANY): multi-step launches with replay at the stop step
         ri = run_batch(B, False, stop=ODESAT_STOP_ANY)

@@ -1067,11 +1067,23 @@ template <typename T> __device__ __forceinline__ T sflip(T x, uint32_t sg) {
     }
 }
 
-// the terms (2 x the reference's) of one clause at voltages v, memories product tt; returns mn
+// -q for the literal's sign word: 1.0 for a negated literal (sg = 0x80000000), -1.0 otherwise
+template <typename T> __device__ __forceinline__ T nq_of(uint32_t sg) {
+    if constexpr (sizeof(T) == 8) {
+        return __hiloint2double((int)(0xBFF00000u ^ sg), 0);
+    } else {
+        return __uint_as_float(0xBF800000u ^ sg);
+    }
+}
+
+// the terms (2 x the reference's) of one clause at voltages v, memories product tt; returns mn.
+// val_j = 1 - q_j v_j is one fma: q_j v_j = +-v_j is exact, so fma(-q_j, v_j, 1) rounds once, as the
+// subtraction does (and a sign flip of a live f64 register pair would cost a copy besides).
 template <typename T>
 __device__ __forceinline__ T solo_terms(const T (&v)[3], const uint32_t (&sg)[3], T tt, T (&d)[3]) {
     const T one = (T)1.0;
-    const T val0 = one - sflip(v[0], sg[0]), val1 = one - sflip(v[1], sg[1]), val2 = one - sflip(v[2], sg[2]);  // :47
+    const T val0 = fma(nq_of<T>(sg[0]), v[0], one), val1 = fma(nq_of<T>(sg[1]), v[1], one),
+            val2 = fma(nq_of<T>(sg[2]), v[2], one);  // :47 (f64 legs: neutral, profiles/r05p_solo_terms_fma_ab.txt)
     const T sel0 = dmin(val1, val2), sel1 = dmin(val0, val2), sel2 = dmin(val0, val1);
     d[0] = sflip(tt * sel0, sg[0]);  // 2 xl xs G (:64-70, :80)
     d[1] = sflip(tt * sel1, sg[1]);
