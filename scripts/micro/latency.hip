@@ -7,6 +7,8 @@
 //                                   stride, conflicts as in k_solo_cv), then their sum: per round (the
 //                                   next round's addresses wait for the sum)
 //   ds_read_b128_x12_bcast          the same 12 reads all from one block (broadcast)
+//   ds_read_b128_x12_Kway           the same reads with exactly K distinct blocks on each bank set of a
+//                                   16-lane group (1: conflict-free)
 //   handoff                         ds_write, s_waitcnt, s_barrier, ds_read of another lane's word: per
 //                                   round (the exchange k_solo_cv does twice per adaptive step)
 //   hipcc --offload-arch=gfx950 -O3 -o latency latency.hip && ./latency
@@ -78,6 +80,18 @@ __global__ __launch_bounds__(512) void k_lat(double *sink, long long *cyc, doubl
 #pragma unroll
             for (int j = 0; j < 12; ++j) s = s + t[j];
             x = x + s.x + s.y;
+        } else if constexpr (KIND >= 10) {  // 12 reads per round, (KIND - 10)-way conflicts per 16-lane group
+            constexpr int K = KIND - 10, S = 16 / K;
+            typedef double TV __attribute__((ext_vector_type(2)));
+            TV s = {0.0, 0.0};
+            TV t[12];
+            const int dep = x > 1e300 ? 1 : 0;
+            const int blk = (l % 16) % S + 16 * ((l % 16) / S) + 16 * dep;
+#pragma unroll
+            for (int j = 0; j < 12; ++j) t[j] = *reinterpret_cast<const TV *>(lds + blk * 10 + (j & 3) * 2);
+#pragma unroll
+            for (int j = 0; j < 12; ++j) s = s + t[j];
+            x = x + s.x + s.y;
         } else if constexpr (KIND == 7) {
             lds[4096 + l] = x;
             __syncthreads();
@@ -112,7 +126,9 @@ int main() {
         if (run<0>("add_f64", nt, 16) || run<1>("mul_f64", nt, 16) || run<2>("min_f64", nt, 16) ||
             run<3>("add_f64_x3", nt, 16) || run<4>("ds_read_b32_chain", nt, 16) ||
             run<5>("ds_read_b128_x12_round", nt, 1) || run<6>("ds_read_b128_x12_bcast_round", nt, 1) ||
-            run<7>("handoff_round", nt, 2))
+            run<7>("handoff_round", nt, 2) || run<11>("ds_read_b128_x12_1way_round", nt, 1) ||
+            run<12>("ds_read_b128_x12_2way_round", nt, 1) || run<14>("ds_read_b128_x12_4way_round", nt, 1) ||
+            run<18>("ds_read_b128_x12_8way_round", nt, 1) || run<26>("ds_read_b128_x12_16way_round", nt, 1))
             return 1;
     }
     return 0;
