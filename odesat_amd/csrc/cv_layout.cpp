@@ -56,13 +56,16 @@ struct Search {
 
     int lit(int c, int j) const { return lits[3 * c + PERMS[perm[c]][j]]; }
 
-    // LDS cycles of the group's 3 NB reads
+    mutable std::vector<uint32_t> seen;  // [n + 1] epoch of the last count of each block address
+    mutable uint32_t epoch = 0;
+    // LDS cycles of the group's 3 NB reads: per read, the most distinct addresses on one bank set
     int group_cost(int gi) const {
         int total = 0;
         const auto &sl = group_slots[gi];
         for (int j = 0; j < 3; ++j)
             for (int q = 0; q < nb_reads; ++q) {
-                int key[17], col[17], k = 0;
+                ++epoch;
+                int cnt[16] = {0}, mx = 1;
                 for (int s : sl) {
                     const int c = slot_clause[s];
                     int v = n;  // the zero block
@@ -70,17 +73,12 @@ struct Search {
                         const int x = lit(c, j) >> 1;
                         if (q * per16 < deg[x]) v = x;
                     }
-                    bool seen = false;
-                    for (int t = 0; t < k; ++t) seen = seen || key[t] == v;
-                    if (!seen) {
-                        key[k] = v;
-                        col[k] = colour[v];
-                        ++k;
+                    if (seen[v] != epoch) {
+                        seen[v] = epoch;
+                        mx = std::max(mx, ++cnt[colour[v]]);
                     }
                 }
-                int cnt[16] = {0}, mx = 0;
-                for (int t = 0; t < k; ++t) mx = std::max(mx, ++cnt[col[t]]);
-                total += std::max(mx, 1);
+                total += mx;
             }
         return total;
     }
@@ -142,6 +140,7 @@ bool cv_layout(int64_t n, int64_t m, const int32_t *lits, const int32_t *vst, in
     }
     S.perm.assign(m, 0);
     S.colour.resize(n + 1);
+    S.seen.assign(n + 1, 0);
     for (int64_t v = 0; v <= n; ++v) S.colour[v] = (int)((v * stride) % 16);
     S.gcost.resize(S.ngroups);
     for (int g = 0; g < S.ngroups; ++g) S.gcost[g] = S.group_cost(g);
