@@ -64,6 +64,29 @@ __device__ __forceinline__ uint64_t memtime() {
 #else
 struct Stamps {};
 #endif
+// Diagnostic build only (-DONCHIP_ADA_STAMPS): the adaptive step of workgroup 0 split by s_memtime into
+// pass 1, the first voltage phase (+ its barrier), pass 2, the second voltage phase with the error
+// terms, and the step's closing barrier with the dt update; per wave sums in g_onchip_ada_stamps[w][5]
+// (read by odesat_onchip_ada_stamps; scripts/onchip_ada_stamps.py).  Each stamp drains the wave's LDS
+// operations, so the segments include that drain.
+#ifdef ONCHIP_ADA_STAMPS
+__device__ unsigned long long g_onchip_ada_stamps[8 * 5];
+__device__ __forceinline__ uint64_t ada_memtime() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define ADA_STAMP(acc)                      \
+    do {                                    \
+        const uint64_t t_ = ada_memtime();  \
+        (acc) += t_ - ada_last;             \
+        ada_last = t_;                      \
+    } while (0)
+#else
+#define ADA_STAMP(acc) do {} while (0)
+#endif
 // Diagnostic build only (-DONCHIP_PHASES): per workgroup, wave 0 records s_memrealtime (100 MHz)
 // at kernel start, after the state load (its barrier), after the step loop and at the end, into
 // g_onchip_phases[g][4] (read by odesat_onchip_phases).
@@ -784,6 +807,10 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     Stamps S{};
     float dtr = ADA ? io_dt<float>(a.io, a.dtr, g) : a.dt;
     if constexpr (ADA) {
+#ifdef ONCHIP_ADA_STAMPS
+        uint64_t ada_st[5] = {0, 0, 0, 0, 0};
+        uint64_t ada_last = ada_memtime();
+#endif
         for (int k = 0; k < a.nsteps; ++k) {  // euler_step (system.rs:111-139)
             const float hk = dtr, hhk = 0.5f * dtr, hqk = 0.25f * dtr;
             const uint32_t flag = UNS + 4u * (k & 1);
@@ -794,6 +821,9 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
             for (int ps = 0; ps < 2; ++ps) {
                 const bool p2 = ps == 1;
                 passA<TR, OFF>(a, mr, hk, lane, p2 ? ADA_H : 0u, p2, flag, e, CNT, ep);  // RHS at y, then at the half step
+#ifdef ONCHIP_ADA_STAMPS
+                if (p2) ADA_STAMP(ada_st[2]); else ADA_STAMP(ada_st[0]);
+#endif
                 if (!p2) {
                     uns = lds_f(flag) != 0.0f;  // uniform
                     if (!uns) {  // an allsat replica takes no step (:122): drop pass 1's terms
@@ -822,6 +852,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                         lds_st(4u * i + ADA_H, __builtin_amdgcn_fmed3f(y + hqk * d2, -1.0f, 1.0f));
                     }
                     __syncthreads();
+                    ADA_STAMP(ada_st[1]);
                 } else {
                     // second half step (:130), max_error (:101-108); the same lane ownership as the
                     // final store below
@@ -848,6 +879,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
 #pragma unroll
                     for (int off = 32; off >= 1; off >>= 1) eb = max(eb, (uint32_t)__shfl_xor((int)eb, off, 64));
                     if ((lane & 63) == 0) lds_st(UNS + 8u + 4u * (uint32_t)(lane >> 6), __uint_as_float(eb));
+                    ADA_STAMP(ada_st[3]);
                 }
             }
             if (lane == 0) lds_st(UNS + 4u * ((k + 1) & 1), 0.0f);  // read by everyone after this step's first pass
@@ -858,6 +890,7 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                 for (int w = 0; w < WAVES; ++w) eb = max(eb, __float_as_uint(lds_f(UNS + 8u + 4u * w)));
                 dtr = fmaxf(fminf(dtr * sqrtf(a.tol / __uint_as_float(eb)), 1e3f), 0.0078125f);
             }
+            ADA_STAMP(ada_st[4]);
             done += 1;
             if (!uns) {  // allsat: no step taken (:122)
                 const int step = a.step0 + k;
@@ -869,6 +902,10 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                 }
             }
         }
+#ifdef ONCHIP_ADA_STAMPS
+        if ((lane & 63) == 0 && g == 0)
+            for (int i = 0; i < 5; ++i) g_onchip_ada_stamps[(lane >> 6) * 5 + i] = ada_st[i];
+#endif
     } else
     for (int k = 0; k < a.nsteps; ++k) {  // euler_step_fixed (system.rs:141-154)
         uint32_t cmax = 0u;
@@ -1015,6 +1052,14 @@ extern "C" int odesat_onchip_phases(unsigned long long *out, int count) {
 }
 extern "C" int odesat_onchip_clk(unsigned long long *out, int count) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(onchip::g_onchip_clk), sizeof(unsigned long long) * (size_t)count, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef ONCHIP_ADA_STAMPS
+// Diagnostic build only: workgroup 0's adaptive-step segment sums of the last launch (8 waves x 5).
+extern "C" int odesat_onchip_ada_stamps(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(onchip::g_onchip_ada_stamps), sizeof(unsigned long long) * 40, 0,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
