@@ -312,6 +312,27 @@ def cpu_baseline(cp, var, neg, n, m, replicas, steps, threads=1):
                       f"({dt:.1f} s)"}
 
 
+def cpu_criterion(steps=10_000):
+    """The `criterion` leg's calls on the host (part of the CPU baseline): the f64 C oracle, one core, one
+    call of each criterion bench on tests/hard.cnf from the same initial state, milliseconds per call."""
+    import numpy as np
+
+    from odesat_amd import cnf as cnf_
+    from oracle.oracle import Oracle, init_voltages
+    with open(os.path.join(ROOT, "tests", "golden", "hard.cnf")) as fh:
+        _, f = cnf_.normalize_cnf_variables(cnf_.parse_dimacs_format(fh.read()))
+    cp, var, neg = f.arrays()
+    o = Oracle(cp, var, neg, f.varnum, "f64")
+    out = {}
+    for name, kw in (("adaptive_hard", dict(tol=0.01)), ("fixed_hard", dict(dt=0.01))):
+        v = init_voltages(42, 0, 1, f.varnum)[0]
+        xs, xl = o.init_short_term_memory(), np.ones(f.nclauses)
+        t0 = time.perf_counter()
+        o.simulate(v, xs, xl, tol=kw.get("tol"), dt=kw.get("dt"), steps=steps)
+        out[name] = (time.perf_counter() - t0) * 1e3
+    return out
+
+
 def load_profile(profile_dir, short, B, dtype, config, mode="fixed"):
     """PMC fits of one kernel on this workload (scripts/make_profile_json.py), or None."""
     for path in sorted(glob.glob(os.path.join(profile_dir, "profile_*.json"))):
@@ -684,6 +705,11 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(cp, v_, n_, n, m, args.cpu_replicas, args.cpu_steps)
+        if isinstance(res.get("criterion"), dict) and "error" not in res["criterion"]:
+            try:  # beside the `criterion` leg's GPU calls; never at the cost of the baseline line
+                cpu["criterion_ms_per_call"] = cpu_criterion()
+            except Exception as e:  # noqa: BLE001
+                cpu["criterion_ms_per_call"] = {"error": f"{type(e).__name__}: {e}"}
         t = cpu_threads()
         if t > 1:  # the same oracle on every host core this job has, beside the 1-core line
             cpu_all = cpu_baseline(cp, v_, n_, n, m, args.cpu_replicas * t, args.cpu_steps, threads=t)
