@@ -230,6 +230,9 @@ __device__ __forceinline__ void front(const Gath &G, Front &F) {
 
 // Second half: the three dv terms into Q, the sat fold and the memory update in place
 // (:60-88, :94-95).
+// (UPD = false: the terms and the sat fold only, the memories left as they are -- the adaptive
+// step's first pass, pass1.)
+template <bool UPD = true>
 __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem, float h, float hh, Pend &Q,
                                      uint32_t &cmax) {
     const float mn = F.mn;
@@ -243,6 +246,7 @@ __device__ __forceinline__ void back(const Args &a, const Front &F, float2 &mem,
     Q.d2 = tt * F.sel2;
     cmax = max(cmax, __float_as_uint(mn));  // :88 -- unsat iff max mn >= 0.5
     asm volatile("" : "+v"(cmax));          // fold now: deferred, it would keep every tile's mn live
+    if constexpr (!UPD) return;
     const float dxs2 = (20.0f * (xs + 0.001f)) * (mn - 0.5f);  // 2 dxs (:84)
     const float dxl = 2.5f * (mn - 0.1f);                       // :85
     mem.x = __builtin_amdgcn_fmed3f(xs + hh * dxs2, 0.001f, 1.0f - 0.001f);  // :94
@@ -330,15 +334,15 @@ __device__ __forceinline__ void pair_wait(uint32_t cnt, uint32_t target, uint32_
 // t+2's first half -- independent, so they interleave -- while the writes and the gathers drain.
 // After the second tile of a pair (bar), the barrier orders the pair's dv updates against the next
 // pair's; inside a pair the same-wave order suffices (see the header).
-template <bool SPL = false>
+template <bool SPL = false, uint32_t DVO = DVC, bool UPD = true>
 __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, SlotF &slot3, float2 &mem1, Pend &P, Front &Fn,
                                           Gath &Gn, int t, float h, float hh, uint32_t &cmax, Stamps &S, bool bar,
                                           bool first = false, uint32_t cnt = 0, uint32_t *ep = nullptr) {
     if (SPL && first) pair_wait(cnt, *ep, a.poll_limit);  // every wave's dv writes of the previous pair are performed
-    const float o0 = lds_f(P.a0 + DVC), o1 = lds_f(P.a1 + DVC), o2 = lds_f(P.a2 + DVC);
-    lds_st(P.a0 + DVC, o0 + P.d0);
-    lds_st(P.a1 + DVC, o1 + P.d1);
-    lds_st(P.a2 + DVC, o2 + P.d2);
+    const float o0 = lds_f(P.a0 + DVO), o1 = lds_f(P.a1 + DVO), o2 = lds_f(P.a2 + DVO);
+    lds_st(P.a0 + DVO, o0 + P.d0);
+    lds_st(P.a1 + DVO, o1 + P.d1);
+    lds_st(P.a2 + DVO, o2 + P.d2);
     __builtin_amdgcn_sched_barrier(0);
     if (SPL && bar) pair_signal(cnt, ++*ep);
 #if defined(ONCHIP_STAMPS) && ONCHIP_STAMPS == 2
@@ -349,7 +353,7 @@ __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, SlotF &s
     gather(slot3, G3);
     slot3 = load_recf(R, t + 7);
     __builtin_amdgcn_sched_barrier(0);
-    back(a, Fn, mem1, h, hh, P, cmax);  // P <- tile t+1's terms (tile t's were written above)
+    back<UPD>(a, Fn, mem1, h, hh, P, cmax);  // P <- tile t+1's terms (tile t's were written above)
     front(Gn, Fn);                      // Fn <- tile t+2's first half
     __builtin_amdgcn_sched_barrier(0);  // a tile's work stays between its barriers
 #ifdef ONCHIP_STAMPS
@@ -454,36 +458,36 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
 
 // ------------------------------------------------------------------------------------------------
 // Adaptive steps (system.rs:111-139, onchip.hpp's ADA_* map).  Pass 1 is the RHS at y (terms with
-// y's memories, which stay in the registers); pass 2 the RHS at the half step.  One code path
-// serves both passes (a uniform flag selects), so a step runs the same ~40 KB of unrolled tile code
-// twice instead of two such sequences that would not share the instruction cache: each clause
-// gathers its voltages from the pass's source (A in pass 1, H in pass 2) and from A (y: their min
-// is pass 1's C, recomputed instead of stored), rebuilds its memories' full-step clone and first
-// half step from y's memories and that C (:124-128), and in pass 2 takes the second half step
-// (:130) and its max_error terms (:101-108).  The arithmetic is k_resident's / k_wave's in the
+// y's memories, which stay in the registers: pass1 below, the fixed pass's tile step); pass 2 the RHS
+// at the half step.  Each pass is its own unrolled code instance (round 5; until then one instance
+// served both under a uniform flag, on the assumption that two would not share the instruction cache
+// -- measured, the split is 14 % faster).  In pass 2 each clause gathers its voltages from H and from A
+// (y: their min is pass 1's C, recomputed instead of stored), rebuilds its memories' full-step clone
+// and first half step from y's memories and that C (:124-128), takes the second half step (:130) and
+// its max_error terms (:101-108).  The arithmetic is k_resident's / k_wave's in the
 // exact rewritten forms of the header (h dxs = (h/2) (2 dxs), (h/2) dxs = (h/4) (2 dxs), ...).
 // Empty slots compute on stand-in memories (0.001, 1): their literals sit at sink words (v = 1.0, so
 // mn = 0 in both passes), where xs = 0.001 and xl = 1 are fixed points of both clamped half steps and
 // of the full step -- so their error terms are exactly 0 and need no mask.
 
-struct GathA {  // a clause's gathered inputs: addresses, sign word, voltages from S and from A (y)
+struct GathA {  // a clause's gathered inputs: addresses, sign word, voltages from H and from A (y)
     uint32_t a0, a1, a2, hi;
     float v0, v1, v2, y0, y1, y2;
 };
 
-struct FrontA {  // the min at S and each literal's selected value (see Front); the voltages at y (pass 2's use)
+struct FrontA {  // the min at H and each literal's selected value (see Front); the voltages at y
     uint32_t a0, a1, a2, hi;
     float sel0, sel1, sel2, mn, y0, y1, y2;
 };
 
-__device__ __forceinline__ void gatherA(const Slot &S, GathA &G, uint32_t sb) {
+__device__ __forceinline__ void gatherA(const Slot &S, GathA &G) {
     G.a0 = S.lo & 0xffffu;
     G.a1 = S.lo >> 16;
     G.a2 = S.hi & 0xffffu;
     G.hi = S.hi;
-    G.v0 = lds_f(G.a0 + sb);
-    G.v1 = lds_f(G.a1 + sb);
-    G.v2 = lds_f(G.a2 + sb);
+    G.v0 = lds_f(G.a0 + ADA_H);
+    G.v1 = lds_f(G.a1 + ADA_H);
+    G.v2 = lds_f(G.a2 + ADA_H);
     G.y0 = lds_f(G.a0);
     G.y1 = lds_f(G.a1);
     G.y2 = lds_f(G.a2);
@@ -507,26 +511,23 @@ __device__ __forceinline__ void frontA(const GathA &G, FrontA &F) {
     F.y2 = G.y2;
 }
 
-__device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &mem, float h, float hh, float hq, bool p2,
-                                      Pend &Q, uint32_t &cmax, float &e) {
+__device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &mem, float h, float hh, float hq,
+                                      Pend &Q, float &e) {
     const uint32_t s0 = F.hi & 0x80000000u, s1 = (F.hi << 1) & 0x80000000u, s2 = (F.hi << 2) & 0x80000000u;
     const float xs = mem.x, xl = mem.y;  // y's memories
-    float xs_t = xs, xl_t = xl, xs_f = 0.0f, xl_f = 0.0f;
-    if (p2) {  // uniform: pass 1 computes none of this
-        // pass 1's 2 C (:60) from the voltages at y, then the full-step clone and the first half
-        // step of the memories (:124-128)
-        const float y0 = 1.0f - __uint_as_float(__float_as_uint(F.y0) ^ s0);
-        const float y1 = 1.0f - __uint_as_float(__float_as_uint(F.y1) ^ s1);
-        const float y2 = 1.0f - __uint_as_float(__float_as_uint(F.y2) ^ s2);
-        const float mn1 = fminf(fminf(y0, y1), y2);
-        const float dxs1 = (20.0f * (xs + 0.001f)) * (mn1 - 0.5f);  // 2 dxs (:84)
-        const float dxl1 = 2.5f * (mn1 - 0.1f);                      // :85
-        xs_f = __builtin_amdgcn_fmed3f(xs + hh * dxs1, 0.001f, 1.0f - 0.001f);
-        xl_f = __builtin_amdgcn_fmed3f(xl + h * dxl1, 1.0f, a.xl_max);
-        xs_t = __builtin_amdgcn_fmed3f(xs + hq * dxs1, 0.001f, 1.0f - 0.001f);  // the half step's memories
-        xl_t = __builtin_amdgcn_fmed3f(xl + hh * dxl1, 1.0f, a.xl_max);
-    }
-    // the pass's RHS: at y (pass 1) or at the half step (pass 2)
+    // pass 1's 2 C (:60) from the voltages at y, then the full-step clone and the first half step of
+    // the memories (:124-128)
+    const float y0 = 1.0f - __uint_as_float(__float_as_uint(F.y0) ^ s0);
+    const float y1 = 1.0f - __uint_as_float(__float_as_uint(F.y1) ^ s1);
+    const float y2 = 1.0f - __uint_as_float(__float_as_uint(F.y2) ^ s2);
+    const float mn1 = fminf(fminf(y0, y1), y2);
+    const float dxs1 = (20.0f * (xs + 0.001f)) * (mn1 - 0.5f);  // 2 dxs (:84)
+    const float dxl1 = 2.5f * (mn1 - 0.1f);                      // :85
+    const float xs_f = __builtin_amdgcn_fmed3f(xs + hh * dxs1, 0.001f, 1.0f - 0.001f);
+    const float xl_f = __builtin_amdgcn_fmed3f(xl + h * dxl1, 1.0f, a.xl_max);
+    const float xs_t = __builtin_amdgcn_fmed3f(xs + hq * dxs1, 0.001f, 1.0f - 0.001f);  // the half step's memories
+    const float xl_t = __builtin_amdgcn_fmed3f(xl + hh * dxl1, 1.0f, a.xl_max);
+    // the RHS at the half step
     const float mn = F.mn;
     const float tt = xl_t * xs_t;
     Q.a0 = F.a0;
@@ -535,24 +536,20 @@ __device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &me
     Q.d0 = __uint_as_float(__float_as_uint(tt * F.sel0) ^ s0);  // 2 xl xs G (:64-70, :80)
     Q.d1 = __uint_as_float(__float_as_uint(tt * F.sel1) ^ s1);
     Q.d2 = __uint_as_float(__float_as_uint(tt * F.sel2) ^ s2);
-    cmax = max(cmax, __float_as_uint(mn));  // :88 (pass 1)
-    asm volatile("" : "+v"(cmax));
-    if (p2) {  // second half step (:130) and its max_error terms (:132)
-        const float dxs2 = (20.0f * (xs_t + 0.001f)) * (mn - 0.5f);
-        const float dxl2 = 2.5f * (mn - 0.1f);
-        const float xs_n = __builtin_amdgcn_fmed3f(xs_t + hq * dxs2, 0.001f, 1.0f - 0.001f);
-        const float xl_n = __builtin_amdgcn_fmed3f(xl_t + hh * dxl2, 1.0f, a.xl_max);
-        e = fmaxf(e, fmaxf(fabsf(xs_f - xs_n), fabsf(xl_f - xl_n)));
-        mem.x = xs_n;
-        mem.y = xl_n;
-    }
+    // second half step (:130) and its max_error terms (:132)
+    const float dxs2 = (20.0f * (xs_t + 0.001f)) * (mn - 0.5f);
+    const float dxl2 = 2.5f * (mn - 0.1f);
+    const float xs_n = __builtin_amdgcn_fmed3f(xs_t + hq * dxs2, 0.001f, 1.0f - 0.001f);
+    const float xl_n = __builtin_amdgcn_fmed3f(xl_t + hh * dxl2, 1.0f, a.xl_max);
+    e = fmaxf(e, fmaxf(fabsf(xs_f - xs_n), fabsf(xl_f - xl_n)));
+    mem.x = xs_n;
+    mem.y = xl_n;
     asm volatile("" : "+v"(mem.x), "+v"(mem.y), "+v"(e));
 }
 
 __device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &slot3, float2 &mem1, Pend &P,
-                                           FrontA &Fn, GathA &Gn, int t, float h, float hh, float hq, uint32_t sb,
-                                           bool p2, uint32_t &cmax, float &e, bool bar, bool first, uint32_t cnt,
-                                           uint32_t &ep) {
+                                           FrontA &Fn, GathA &Gn, int t, float h, float hh, float hq, float &e,
+                                           bool bar, bool first, uint32_t cnt, uint32_t &ep) {
     constexpr bool SPL = (ONCHIP_SPLITBAR & 2) != 0;
     if (SPL && first) pair_wait(cnt, ep, a.poll_limit);  // (split barriers: see tile_step)
     const float o0 = lds_f(P.a0 + ADA_D), o1 = lds_f(P.a1 + ADA_D), o2 = lds_f(P.a2 + ADA_D);
@@ -562,10 +559,10 @@ __device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &s
     __builtin_amdgcn_sched_barrier(0);
     if (SPL && bar) pair_signal(cnt, ++ep);
     GathA G3;
-    gatherA(slot3, G3, sb);
+    gatherA(slot3, G3);
     slot3 = load_rec(R, t + 7);
     __builtin_amdgcn_sched_barrier(0);
-    backA(a, Fn, mem1, h, hh, hq, p2, P, cmax, e);
+    backA(a, Fn, mem1, h, hh, hq, P, e);
     frontA(Gn, Fn);
     __builtin_amdgcn_sched_barrier(0);
     if (bar && !SPL) __syncthreads();
@@ -573,60 +570,116 @@ __device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &s
     Gn = G3;
 }
 
-// Register tile T of an adaptive pass; the pass's last tile ends no pair (passA closes with a barrier).
+// Register tile T of pass 2; the pass's last tile ends no pair (pass2 closes with a barrier).
 template <int TR, int OFF, int T>
 __device__ __forceinline__ void reg_tileA(const Args &a, const Recs &R, float2 (&mr)[TR], Slot (&ring)[4], Pend &P,
-                                          FrontA &Fn, GathA &Gn, float h, float hh, float hq, uint32_t sb, bool p2,
-                                          uint32_t &cmax, float &e, uint32_t cnt, uint32_t &ep) {
+                                          FrontA &Fn, GathA &Gn, float h, float hh, float hq, float &e, uint32_t cnt,
+                                          uint32_t &ep) {
     constexpr bool bar = ((T + OFF) & 1) != 0 && T + 1 < TR;
     constexpr bool first = T > 0 && ((T - 1 + OFF) & 1) != 0;  // the first tile of a pair after another pair
     if constexpr (T + 1 < TR) {
-        tile_stepA(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, hq, sb, p2, cmax, e, bar, first, cnt, ep);
+        tile_stepA(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, h, hh, hq, e, bar, first, cnt, ep);
     } else {  // the (empty) tile after the last: stand-in memories (zero error terms), nothing stored
         float2 m = make_float2(0.001f, 1.0f);
-        tile_stepA(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, hq, sb, p2, cmax, e, bar, first, cnt, ep);
+        tile_stepA(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, h, hh, hq, e, bar, first, cnt, ep);
     }
 }
 
 template <int TR, int OFF, int... Ts>
 __device__ __forceinline__ void reg_tilesA(std::integer_sequence<int, Ts...>, const Args &a, const Recs &R,
                                            float2 (&mr)[TR], Slot (&ring)[4], Pend &P, FrontA &Fn, GathA &Gn, float h,
-                                           float hh, float hq, uint32_t sb, bool p2, uint32_t &cmax, float &e,
-                                           uint32_t cnt, uint32_t &ep) {
-    (reg_tileA<TR, OFF, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, hq, sb, p2, cmax, e, cnt, ep), ...);
+                                           float hh, float hq, float &e, uint32_t cnt, uint32_t &ep) {
+    (reg_tileA<TR, OFF, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, hq, e, cnt, ep), ...);
 }
 
-// One adaptive pass over every tile (all in registers): the RHS at the source sb (0: A, ADA_H: H)
-// into D and, in pass 2, the memories' second half step; pass 1 raises the unsat flag at `flag`
-// (:88).  Ends with a barrier.
+// Pass 2 of an adaptive step over every tile (all in registers): the RHS at the half step (H) into D
+// and the memories' second half step, with their error terms.  Ends with a barrier.
 template <int TR, int OFF>
-__device__ __forceinline__ void passA(const Args &a, float2 (&mr)[TR], float h, int lane, uint32_t sb, bool p2,
-                                      uint32_t flag, float &e, uint32_t cnt, uint32_t &ep) {
+__device__ __forceinline__ void pass2(const Args &a, float2 (&mr)[TR], float h, int lane, float &e, uint32_t cnt,
+                                      uint32_t &ep) {
     Recs R;
     R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec, 0, (int)a.rec_bytes, 0x00020000);
     R.voff = (uint32_t)lane * 8u;
     R.soff = 0u;
     asm volatile("" : "+s"(R.soff));
     const float hh = 0.5f * h, hq = 0.25f * h;
-    uint32_t cmax = 0u;
     Slot ring[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) ring[s] = load_rec(R, s);
     Pend P;
     GathA G0, G1, Gn;
-    gatherA(ring[0], G0, sb);
+    gatherA(ring[0], G0);
     ring[0] = load_rec(R, 4);
-    gatherA(ring[1], G1, sb);
+    gatherA(ring[1], G1);
     ring[1] = load_rec(R, 5);
-    gatherA(ring[2], Gn, sb);
+    gatherA(ring[2], Gn);
     ring[2] = load_rec(R, 6);
     FrontA F0, Fn;
     frontA(G0, F0);
     frontA(G1, Fn);
-    backA(a, F0, mr[0], h, hh, hq, p2, P, cmax, e);
-    reg_tilesA<TR, OFF>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, hq, sb, p2, cmax, e,
-                        cnt, ep);
-    if (!p2 && !(__uint_as_float(cmax) < 0.5f)) lds_st(flag, 1.0f);
+    backA(a, F0, mr[0], h, hh, hq, P, e);
+    reg_tilesA<TR, OFF>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, h, hh, hq, e, cnt, ep);
+    __syncthreads();
+}
+
+// The adaptive step's first pass: the fixed pass's tile step with the dv terms into D and no memory
+// update -- the 12-byte records, one gather per literal.
+template <int TR, int OFF, int T>
+__device__ __forceinline__ void reg_tile1(const Args &a, const Recs &R, float2 (&mr)[TR], SlotF (&ring)[4], Pend &P,
+                                          Front &Fn, Gath &Gn, uint32_t &cmax, Stamps &S, uint32_t cnt, uint32_t *ep) {
+    constexpr bool bar = ((T + OFF) & 1) != 0 && T + 1 < TR;  // (as reg_tileA: pass1 closes with a barrier)
+    constexpr bool first = T > 0 && ((T - 1 + OFF) & 1) != 0;
+    constexpr bool SPL = (ONCHIP_SPLITBAR & 2) != 0;
+    if constexpr (T + 1 < TR) {
+        tile_step<SPL, ADA_D, false>(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, 0.0f, 0.0f, cmax, S, bar, first,
+                                     cnt, ep);
+    } else {  // the (empty) tile after the last: its terms are never applied
+        float2 m = make_float2(0.001f, 1.0f);
+        tile_step<SPL, ADA_D, false>(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, 0.0f, 0.0f, cmax, S, bar, first, cnt, ep);
+    }
+}
+
+template <int TR, int OFF, int... Ts>
+__device__ __forceinline__ void reg_tiles1(std::integer_sequence<int, Ts...>, const Args &a, const Recs &R,
+                                           float2 (&mr)[TR], SlotF (&ring)[4], Pend &P, Front &Fn, Gath &Gn,
+                                           uint32_t &cmax, Stamps &S, uint32_t cnt, uint32_t *ep) {
+    (reg_tile1<TR, OFF, Ts>(a, R, mr, ring, P, Fn, Gn, cmax, S, cnt, ep), ...);
+}
+
+// Pass 1 of an adaptive step: the RHS at y (A) into D, the unsat flag at `flag` (:88).  Ends with a
+// barrier.  The term's sign rides on the selected value (pass 2: on the product; a sign flip commutes
+// with the rounding).
+template <int TR, int OFF>
+__device__ __forceinline__ void pass1(const Args &a, float2 (&mr)[TR], int lane, uint32_t flag, uint32_t cnt,
+                                      uint32_t &ep) {
+    Recs R;
+#if ONCHIP_REC12
+    R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec12, 0, (int)a.rec12_bytes, 0x00020000);
+#else
+    R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec, 0, (int)a.rec_bytes, 0x00020000);
+#endif
+    R.voff = (uint32_t)lane * RECF_BYTES;
+    R.soff = 0u;
+    asm volatile("" : "+s"(R.soff));
+    uint32_t cmax = 0u;
+    Stamps S{};
+    SlotF ring[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) ring[s] = load_recf(R, s);
+    Pend P;
+    Gath G0, G1, Gn;
+    gather(ring[0], G0);
+    ring[0] = load_recf(R, 4);
+    gather(ring[1], G1);
+    ring[1] = load_recf(R, 5);
+    gather(ring[2], Gn);
+    ring[2] = load_recf(R, 6);
+    Front F0, Fn;
+    front(G0, F0);
+    front(G1, Fn);
+    back<false>(a, F0, mr[0], 0.0f, 0.0f, P, cmax);
+    reg_tiles1<TR, OFF>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, cmax, S, cnt, &ep);
+    if (!(__uint_as_float(cmax) < 0.5f)) lds_st(flag, 1.0f);
     __syncthreads();
 }
 
@@ -815,72 +868,63 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
             const float hk = dtr, hhk = 0.5f * dtr, hqk = 0.25f * dtr;
             const uint32_t flag = UNS + 4u * (k & 1);
             float e = 0.0f;
-            bool uns = false;
-            // the two passes run ONE instance of the unrolled tile code (a loop the compiler keeps)
-#pragma clang loop unroll(disable)
-            for (int ps = 0; ps < 2; ++ps) {
-                const bool p2 = ps == 1;
-                passA<TR, OFF>(a, mr, hk, lane, p2 ? ADA_H : 0u, p2, flag, e, CNT, ep);  // RHS at y, then at the half step
-#ifdef ONCHIP_ADA_STAMPS
-                if (p2) ADA_STAMP(ada_st[2]); else ADA_STAMP(ada_st[0]);
-#endif
-                if (!p2) {
-                    uns = lds_f(flag) != 0.0f;  // uniform
-                    if (!uns) {  // an allsat replica takes no step (:122): drop pass 1's terms
-                        for (int i = lane; i < a.n; i += NTH) lds_st(4u * i + ADA_D, 0.0f);
-                        break;
-                    }
-                    // full-step clone and first half step (:124-128), four variables per LDS access
-                    // (A, D, H and F are 16-byte aligned), then the n % 4 last ones
-                    for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
-                        const uint32_t o = 16u * (uint32_t)i4;
-                        const f4v d2 = lds_f4(o + ADA_D), y = lds_f4(o);
-                        lds_st4(o + ADA_D, f4v{0.0f, 0.0f, 0.0f, 0.0f});
-                        f4v vf, vh;
+            pass1<TR, OFF>(a, mr, lane, flag, CNT, ep);  // the RHS at y into D, the unsat flag
+            ADA_STAMP(ada_st[0]);
+            const bool uns = lds_f(flag) != 0.0f;  // uniform
+            if (!uns) {  // an allsat replica takes no step (:122): drop pass 1's terms
+                for (int i = lane; i < a.n; i += NTH) lds_st(4u * i + ADA_D, 0.0f);
+            } else {
+                // full-step clone and first half step (:124-128), four variables per LDS access (A, D,
+                // H and F are 16-byte aligned), then the n % 4 last ones
+                for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
+                    const uint32_t o = 16u * (uint32_t)i4;
+                    const f4v d2 = lds_f4(o + ADA_D), y = lds_f4(o);
+                    lds_st4(o + ADA_D, f4v{0.0f, 0.0f, 0.0f, 0.0f});
+                    f4v vf, vh;
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            vf[u] = __builtin_amdgcn_fmed3f(y[u] + hhk * d2[u], -1.0f, 1.0f);
-                            vh[u] = __builtin_amdgcn_fmed3f(y[u] + hqk * d2[u], -1.0f, 1.0f);
-                        }
-                        lds_st4(o + ADA_F, vf);
-                        lds_st4(o + ADA_H, vh);
+                    for (int u = 0; u < 4; ++u) {
+                        vf[u] = __builtin_amdgcn_fmed3f(y[u] + hhk * d2[u], -1.0f, 1.0f);
+                        vh[u] = __builtin_amdgcn_fmed3f(y[u] + hqk * d2[u], -1.0f, 1.0f);
                     }
-                    for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) {
-                        const float d2 = lds_f(4u * i + ADA_D), y = lds_f(4u * i);
-                        lds_st(4u * i + ADA_D, 0.0f);
-                        lds_st(4u * i + ADA_F, __builtin_amdgcn_fmed3f(y + hhk * d2, -1.0f, 1.0f));
-                        lds_st(4u * i + ADA_H, __builtin_amdgcn_fmed3f(y + hqk * d2, -1.0f, 1.0f));
-                    }
-                    __syncthreads();
-                    ADA_STAMP(ada_st[1]);
-                } else {
-                    // second half step (:130), max_error (:101-108); the same lane ownership as the
-                    // final store below
-                    for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
-                        const uint32_t o = 16u * (uint32_t)i4;
-                        const f4v d2 = lds_f4(o + ADA_D), vh = lds_f4(o + ADA_H), vf = lds_f4(o + ADA_F);
-                        lds_st4(o + ADA_D, f4v{0.0f, 0.0f, 0.0f, 0.0f});
-                        f4v vn;
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            vn[u] = __builtin_amdgcn_fmed3f(vh[u] + hqk * d2[u], -1.0f, 1.0f);
-                            e = fmaxf(e, fabsf(vf[u] - vn[u]));
-                        }
-                        lds_st4(o, vn);
-                    }
-                    for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) {
-                        const float d2 = lds_f(4u * i + ADA_D);
-                        lds_st(4u * i + ADA_D, 0.0f);
-                        const float vn = __builtin_amdgcn_fmed3f(lds_f(4u * i + ADA_H) + hqk * d2, -1.0f, 1.0f);
-                        e = fmaxf(e, fabsf(lds_f(4u * i + ADA_F) - vn));
-                        lds_st(4u * i, vn);
-                    }
-                    uint32_t eb = __float_as_uint(e);  // non-negative: the bits order as the values
-#pragma unroll
-                    for (int off = 32; off >= 1; off >>= 1) eb = max(eb, (uint32_t)__shfl_xor((int)eb, off, 64));
-                    if ((lane & 63) == 0) lds_st(UNS + 8u + 4u * (uint32_t)(lane >> 6), __uint_as_float(eb));
-                    ADA_STAMP(ada_st[3]);
+                    lds_st4(o + ADA_F, vf);
+                    lds_st4(o + ADA_H, vh);
                 }
+                for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) {
+                    const float d2 = lds_f(4u * i + ADA_D), y = lds_f(4u * i);
+                    lds_st(4u * i + ADA_D, 0.0f);
+                    lds_st(4u * i + ADA_F, __builtin_amdgcn_fmed3f(y + hhk * d2, -1.0f, 1.0f));
+                    lds_st(4u * i + ADA_H, __builtin_amdgcn_fmed3f(y + hqk * d2, -1.0f, 1.0f));
+                }
+                __syncthreads();
+                ADA_STAMP(ada_st[1]);
+                pass2<TR, OFF>(a, mr, hk, lane, e, CNT, ep);  // the RHS at the half step, the memories' step
+                ADA_STAMP(ada_st[2]);
+                // second half step (:130), max_error (:101-108); the same lane ownership as the final
+                // store below
+                for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
+                    const uint32_t o = 16u * (uint32_t)i4;
+                    const f4v d2 = lds_f4(o + ADA_D), vh = lds_f4(o + ADA_H), vf = lds_f4(o + ADA_F);
+                    lds_st4(o + ADA_D, f4v{0.0f, 0.0f, 0.0f, 0.0f});
+                    f4v vn;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        vn[u] = __builtin_amdgcn_fmed3f(vh[u] + hqk * d2[u], -1.0f, 1.0f);
+                        e = fmaxf(e, fabsf(vf[u] - vn[u]));
+                    }
+                    lds_st4(o, vn);
+                }
+                for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) {
+                    const float d2 = lds_f(4u * i + ADA_D);
+                    lds_st(4u * i + ADA_D, 0.0f);
+                    const float vn = __builtin_amdgcn_fmed3f(lds_f(4u * i + ADA_H) + hqk * d2, -1.0f, 1.0f);
+                    e = fmaxf(e, fabsf(lds_f(4u * i + ADA_F) - vn));
+                    lds_st(4u * i, vn);
+                }
+                uint32_t eb = __float_as_uint(e);  // non-negative: the bits order as the values
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) eb = max(eb, (uint32_t)__shfl_xor((int)eb, off, 64));
+                if ((lane & 63) == 0) lds_st(UNS + 8u + 4u * (uint32_t)(lane >> 6), __uint_as_float(eb));
+                ADA_STAMP(ada_st[3]);
             }
             if (lane == 0) lds_st(UNS + 4u * ((k + 1) & 1), 0.0f);  // read by everyone after this step's first pass
             __syncthreads();

@@ -15,7 +15,8 @@ for r in $(seq 1 "${ROUNDS:-3}"); do
         cfg=${!side:-}
         if [[ "$cfg" == --* ]]; then  # bench.py options (--lib PATH, --knob K=V)
             out=$(timeout -k 10 300 $CMD $cfg 2>/dev/null) || { echo "$side failed"; exit 1; }
-        else  # an environment for scripts/tooling.py
+        else  # an environment for scripts/tooling.py (bench.py reads neither XP_LIB nor XP_KNOBS: use --lib / --knob)
+            if [[ -n "$cfg" && "$CMD" == *bench.py* ]]; then echo "$side: bench.py takes --lib / --knob, not [$cfg]"; exit 1; fi
             out=$(env $cfg timeout -k 10 300 $CMD 2>/dev/null) || { echo "$side failed"; exit 1; }
         fi
         echo "$side [$cfg] $(echo "$out" | val)"
