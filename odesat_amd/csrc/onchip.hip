@@ -475,9 +475,9 @@ struct GathA {  // a clause's gathered inputs: addresses, sign word, voltages fr
     float v0, v1, v2, y0, y1, y2;
 };
 
-struct FrontA {  // the min at H and each literal's selected value (see Front); the voltages at y
-    uint32_t a0, a1, a2, hi;
-    float sel0, sel1, sel2, mn, y0, y1, y2;
+struct FrontA {  // the min at H and each literal's signed selected value (see Front); the min at y
+    uint32_t a0, a1, a2;
+    float sel0, sel1, sel2, mn, mn1;
 };
 
 __device__ __forceinline__ void gatherA(const Slot &S, GathA &G) {
@@ -497,30 +497,27 @@ __device__ __forceinline__ void frontA(const GathA &G, FrontA &F) {
     F.a0 = G.a0;
     F.a1 = G.a1;
     F.a2 = G.a2;
-    F.hi = G.hi;
     const uint32_t s0 = G.hi & 0x80000000u, s1 = (G.hi << 1) & 0x80000000u, s2 = (G.hi << 2) & 0x80000000u;
     const float val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
     const float val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
     const float val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
-    F.sel0 = fminf(val1, val2);
-    F.sel1 = fminf(val0, val2);
-    F.sel2 = fminf(val0, val1);
-    F.mn = fminf(F.sel2, val2);
-    F.y0 = G.y0;
-    F.y1 = G.y1;
-    F.y2 = G.y2;
+    const float sel2 = fminf(val0, val1);
+    F.sel0 = __uint_as_float(__float_as_uint(fminf(val1, val2)) ^ s0);  // the sign q rides on sel (see Front)
+    F.sel1 = __uint_as_float(__float_as_uint(fminf(val0, val2)) ^ s1);
+    F.sel2 = __uint_as_float(__float_as_uint(sel2) ^ s2);
+    F.mn = fminf(sel2, val2);
+    // pass 1's 2 C (:60) from the voltages at y
+    const float y0 = 1.0f - __uint_as_float(__float_as_uint(G.y0) ^ s0);
+    const float y1 = 1.0f - __uint_as_float(__float_as_uint(G.y1) ^ s1);
+    const float y2 = 1.0f - __uint_as_float(__float_as_uint(G.y2) ^ s2);
+    F.mn1 = fminf(fminf(y0, y1), y2);
 }
 
 __device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &mem, float h, float hh, float hq,
                                       Pend &Q, float &e) {
-    const uint32_t s0 = F.hi & 0x80000000u, s1 = (F.hi << 1) & 0x80000000u, s2 = (F.hi << 2) & 0x80000000u;
     const float xs = mem.x, xl = mem.y;  // y's memories
-    // pass 1's 2 C (:60) from the voltages at y, then the full-step clone and the first half step of
-    // the memories (:124-128)
-    const float y0 = 1.0f - __uint_as_float(__float_as_uint(F.y0) ^ s0);
-    const float y1 = 1.0f - __uint_as_float(__float_as_uint(F.y1) ^ s1);
-    const float y2 = 1.0f - __uint_as_float(__float_as_uint(F.y2) ^ s2);
-    const float mn1 = fminf(fminf(y0, y1), y2);
+    // the full-step clone and the first half step of the memories (:124-128) from pass 1's C
+    const float mn1 = F.mn1;
     const float dxs1 = (20.0f * (xs + 0.001f)) * (mn1 - 0.5f);  // 2 dxs (:84)
     const float dxl1 = 2.5f * (mn1 - 0.1f);                      // :85
     const float xs_f = __builtin_amdgcn_fmed3f(xs + hh * dxs1, 0.001f, 1.0f - 0.001f);
@@ -533,9 +530,9 @@ __device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &me
     Q.a0 = F.a0;
     Q.a1 = F.a1;
     Q.a2 = F.a2;
-    Q.d0 = __uint_as_float(__float_as_uint(tt * F.sel0) ^ s0);  // 2 xl xs G (:64-70, :80)
-    Q.d1 = __uint_as_float(__float_as_uint(tt * F.sel1) ^ s1);
-    Q.d2 = __uint_as_float(__float_as_uint(tt * F.sel2) ^ s2);
+    Q.d0 = tt * F.sel0;  // 2 xl xs G (:64-70, :80), the sign q in sel
+    Q.d1 = tt * F.sel1;
+    Q.d2 = tt * F.sel2;
     // second half step (:130) and its max_error terms (:132)
     const float dxs2 = (20.0f * (xs_t + 0.001f)) * (mn - 0.5f);
     const float dxl2 = 2.5f * (mn - 0.1f);
@@ -647,8 +644,7 @@ __device__ __forceinline__ void reg_tiles1(std::integer_sequence<int, Ts...>, co
 }
 
 // Pass 1 of an adaptive step: the RHS at y (A) into D, the unsat flag at `flag` (:88).  Ends with a
-// barrier.  The term's sign rides on the selected value (pass 2: on the product; a sign flip commutes
-// with the rounding).
+// barrier.
 template <int TR, int OFF>
 __device__ __forceinline__ void pass1(const Args &a, float2 (&mr)[TR], int lane, uint32_t flag, uint32_t cnt,
                                       uint32_t &ep) {
