@@ -619,6 +619,11 @@ __device__ __forceinline__ void pass2(const Args &a, float2 (&mr)[TR], float h, 
     __syncthreads();
 }
 
+// Pass 1 takes plain barriers, as the fixed pass does (split barriers there: -2.7 %,
+// profiles/r05final2_ab_p1plain.txt; 1 = split barriers, A/B only); pass 2 keeps its split barriers.
+#ifndef ONCHIP_ADA_P1_SPL
+#define ONCHIP_ADA_P1_SPL 0
+#endif
 // The adaptive step's first pass: the fixed pass's tile step with the dv terms into D and no memory
 // update -- the 12-byte records, one gather per literal.
 template <int TR, int OFF, int T>
@@ -626,7 +631,7 @@ __device__ __forceinline__ void reg_tile1(const Args &a, const Recs &R, float2 (
                                           Front &Fn, Gath &Gn, uint32_t &cmax, Stamps &S, uint32_t cnt, uint32_t *ep) {
     constexpr bool bar = ((T + OFF) & 1) != 0 && T + 1 < TR;  // (as reg_tileA: pass1 closes with a barrier)
     constexpr bool first = T > 0 && ((T - 1 + OFF) & 1) != 0;
-    constexpr bool SPL = (ONCHIP_SPLITBAR & 2) != 0;
+    constexpr bool SPL = (ONCHIP_SPLITBAR & 2) != 0 && ONCHIP_ADA_P1_SPL;
     if constexpr (T + 1 < TR) {
         tile_step<SPL, ADA_D, false>(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, 0.0f, 0.0f, cmax, S, bar, first,
                                      cnt, ep);
