@@ -13,7 +13,7 @@
 // time, so the index is static), the remaining tiles in LDS next to v and dv.  A step then moves
 // no state through the memory hierarchy at all; the only per-step reads are the literal records
 // (slot-major, L2-resident and shared by every CU): 12 bytes per clause slot for fixed steps, one
-// word per literal (ONCHIP_REC12, onchip.hpp), 8 bytes for adaptive steps.
+// word per literal (ONCHIP_REC12, onchip.hpp), 8 bytes for the second pass of an adaptive step.
 //
 // Exactness of the short arithmetic (the host launches this kernel only on "in-range" states:
 // v in [-1, 1], xs in [-1, 1], xl in [1, 1e30], |zeta| <= 1e6 -- every state after one step is, by
