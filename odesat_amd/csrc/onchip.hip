@@ -13,7 +13,7 @@
 // time, so the index is static), the remaining tiles in LDS next to v and dv.  A step then moves
 // no state through the memory hierarchy at all; the only per-step reads are the literal records
 // (slot-major, L2-resident and shared by every CU): 12 bytes per clause slot for fixed steps, one
-// word per literal (ONCHIP_REC12, onchip.hpp), 8 bytes for the second pass of an adaptive step.
+// word per literal (ONCHIP_REC12, onchip.hpp), for both passes of an adaptive step too.
 //
 // Exactness of the short arithmetic (the host launches this kernel only on "in-range" states:
 // v in [-1, 1], xs in [-1, 1], xl in [1, 1e30], |zeta| <= 1e6 -- every state after one step is, by
@@ -470,17 +470,49 @@ __device__ __forceinline__ void pass(const Args &a, float2 (&mr)[TR], float h, i
 // mn = 0 in both passes), where xs = 0.001 and xl = 1 are fixed points of both clamped half steps and
 // of the full step -- so their error terms are exactly 0 and need no mask.
 
+// Pass 2's records: the 12-byte form, as pass 1 (round 5: +1.2 % on the adaptive leg against the 8-byte
+// form, profiles/r05ai_ab_p2r12.txt, at 10 spilled VGPRs instead of 1; 0 = the 8-byte form, A/B only).
+#ifndef ONCHIP_ADA_P2_REC12
+#define ONCHIP_ADA_P2_REC12 1
+#endif
+#if ONCHIP_ADA_P2_REC12 && ONCHIP_REC12
+typedef SlotF SlotA;
+constexpr uint32_t RECA_BYTES = 12;
+__device__ __forceinline__ SlotA load_recA(const Recs &R, int t) { return load_recf(R, t); }
+struct GathA {  // a clause's gathered inputs: the literals' record words, voltages from H and from A (y)
+    uint32_t w0, w1, w2;
+    float v0, v1, v2, y0, y1, y2;
+};
+#else
+typedef Slot SlotA;
+constexpr uint32_t RECA_BYTES = 8;
+__device__ __forceinline__ SlotA load_recA(const Recs &R, int t) { return load_rec(R, t); }
 struct GathA {  // a clause's gathered inputs: addresses, sign word, voltages from H and from A (y)
     uint32_t a0, a1, a2, hi;
     float v0, v1, v2, y0, y1, y2;
 };
+#endif
 
 struct FrontA {  // the min at H and each literal's signed selected value (see Front); the min at y
     uint32_t a0, a1, a2;
     float sel0, sel1, sel2, mn, mn1;
 };
 
-__device__ __forceinline__ void gatherA(const Slot &S, GathA &G) {
+#if ONCHIP_ADA_P2_REC12 && ONCHIP_REC12
+__device__ __forceinline__ void gatherA(const SlotA &S, GathA &G) {
+    G.w0 = S.w0;
+    G.w1 = S.w1;
+    G.w2 = S.w2;
+    const uint32_t a0 = S.w0 & 0xffffu, a1 = S.w1 & 0xffffu, a2 = S.w2 & 0xffffu;
+    G.v0 = lds_f(a0 + ADA_H);
+    G.v1 = lds_f(a1 + ADA_H);
+    G.v2 = lds_f(a2 + ADA_H);
+    G.y0 = lds_f(a0);
+    G.y1 = lds_f(a1);
+    G.y2 = lds_f(a2);
+}
+#else
+__device__ __forceinline__ void gatherA(const SlotA &S, GathA &G) {
     G.a0 = S.lo & 0xffffu;
     G.a1 = S.lo >> 16;
     G.a2 = S.hi & 0xffffu;
@@ -492,12 +524,20 @@ __device__ __forceinline__ void gatherA(const Slot &S, GathA &G) {
     G.y1 = lds_f(G.a1);
     G.y2 = lds_f(G.a2);
 }
+#endif
 
 __device__ __forceinline__ void frontA(const GathA &G, FrontA &F) {
+#if ONCHIP_ADA_P2_REC12 && ONCHIP_REC12
+    F.a0 = G.w0 & 0xffffu;
+    F.a1 = G.w1 & 0xffffu;
+    F.a2 = G.w2 & 0xffffu;
+    const uint32_t s0 = G.w0 & 0x80000000u, s1 = G.w1 & 0x80000000u, s2 = G.w2 & 0x80000000u;
+#else
     F.a0 = G.a0;
     F.a1 = G.a1;
     F.a2 = G.a2;
     const uint32_t s0 = G.hi & 0x80000000u, s1 = (G.hi << 1) & 0x80000000u, s2 = (G.hi << 2) & 0x80000000u;
+#endif
     const float val0 = 1.0f - __uint_as_float(__float_as_uint(G.v0) ^ s0);  // 1 - q v  (:47)
     const float val1 = 1.0f - __uint_as_float(__float_as_uint(G.v1) ^ s1);
     const float val2 = 1.0f - __uint_as_float(__float_as_uint(G.v2) ^ s2);
@@ -544,7 +584,7 @@ __device__ __forceinline__ void backA(const Args &a, const FrontA &F, float2 &me
     asm volatile("" : "+v"(mem.x), "+v"(mem.y), "+v"(e));
 }
 
-__device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &slot3, float2 &mem1, Pend &P,
+__device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, SlotA &slot3, float2 &mem1, Pend &P,
                                            FrontA &Fn, GathA &Gn, int t, float h, float hh, float hq, float &e,
                                            bool bar, bool first, uint32_t cnt, uint32_t &ep) {
     constexpr bool SPL = (ONCHIP_SPLITBAR & 2) != 0;
@@ -557,7 +597,7 @@ __device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &s
     if (SPL && bar) pair_signal(cnt, ++ep);
     GathA G3;
     gatherA(slot3, G3);
-    slot3 = load_rec(R, t + 7);
+    slot3 = load_recA(R, t + 7);
     __builtin_amdgcn_sched_barrier(0);
     backA(a, Fn, mem1, h, hh, hq, P, e);
     frontA(Gn, Fn);
@@ -569,7 +609,7 @@ __device__ __forceinline__ void tile_stepA(const Args &a, const Recs &R, Slot &s
 
 // Register tile T of pass 2; the pass's last tile ends no pair (pass2 closes with a barrier).
 template <int TR, int OFF, int T>
-__device__ __forceinline__ void reg_tileA(const Args &a, const Recs &R, float2 (&mr)[TR], Slot (&ring)[4], Pend &P,
+__device__ __forceinline__ void reg_tileA(const Args &a, const Recs &R, float2 (&mr)[TR], SlotA (&ring)[4], Pend &P,
                                           FrontA &Fn, GathA &Gn, float h, float hh, float hq, float &e, uint32_t cnt,
                                           uint32_t &ep) {
     constexpr bool bar = ((T + OFF) & 1) != 0 && T + 1 < TR;
@@ -584,7 +624,7 @@ __device__ __forceinline__ void reg_tileA(const Args &a, const Recs &R, float2 (
 
 template <int TR, int OFF, int... Ts>
 __device__ __forceinline__ void reg_tilesA(std::integer_sequence<int, Ts...>, const Args &a, const Recs &R,
-                                           float2 (&mr)[TR], Slot (&ring)[4], Pend &P, FrontA &Fn, GathA &Gn, float h,
+                                           float2 (&mr)[TR], SlotA (&ring)[4], Pend &P, FrontA &Fn, GathA &Gn, float h,
                                            float hh, float hq, float &e, uint32_t cnt, uint32_t &ep) {
     (reg_tileA<TR, OFF, Ts>(a, R, mr, ring, P, Fn, Gn, h, hh, hq, e, cnt, ep), ...);
 }
@@ -595,22 +635,26 @@ template <int TR, int OFF>
 __device__ __forceinline__ void pass2(const Args &a, float2 (&mr)[TR], float h, int lane, float &e, uint32_t cnt,
                                       uint32_t &ep) {
     Recs R;
+#if ONCHIP_ADA_P2_REC12 && ONCHIP_REC12
+    R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec12, 0, (int)a.rec12_bytes, 0x00020000);
+#else
     R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)a.rec, 0, (int)a.rec_bytes, 0x00020000);
-    R.voff = (uint32_t)lane * 8u;
+#endif
+    R.voff = (uint32_t)lane * RECA_BYTES;
     R.soff = 0u;
     asm volatile("" : "+s"(R.soff));
     const float hh = 0.5f * h, hq = 0.25f * h;
-    Slot ring[4];
+    SlotA ring[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) ring[s] = load_rec(R, s);
+    for (int s = 0; s < 4; ++s) ring[s] = load_recA(R, s);
     Pend P;
     GathA G0, G1, Gn;
     gatherA(ring[0], G0);
-    ring[0] = load_rec(R, 4);
+    ring[0] = load_recA(R, 4);
     gatherA(ring[1], G1);
-    ring[1] = load_rec(R, 5);
+    ring[1] = load_recA(R, 5);
     gatherA(ring[2], Gn);
-    ring[2] = load_rec(R, 6);
+    ring[2] = load_recA(R, 6);
     FrontA F0, Fn;
     frontA(G0, F0);
     frontA(G1, Fn);

@@ -105,9 +105,8 @@ inline uint64_t make_rec(uint32_t a0, uint32_t a1, uint32_t a2, bool n0, bool n1
 }
 // 12-byte records (the fixed-step kernel; ONCHIP_REC12=0 builds the 8-byte form, A/B: 12 bytes are
 // ~2 % faster, profiles/r03_rec12_ab.txt): one word per literal, its 16-bit LDS
-// address and its sign at bit 31, so no literal's sign needs a shift (the adaptive kernel's first
-// pass reads them too; its second pass keeps the 8-byte records: its registers have no room for three
-// sign words per clause in flight)
+// address and its sign at bit 31, so no literal's sign needs a shift (both passes of the adaptive
+// kernel read them too since round 5: ONCHIP_ADA_P2_REC12, onchip.hip)
 #ifndef ONCHIP_REC12
 #define ONCHIP_REC12 1
 #endif
