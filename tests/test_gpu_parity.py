@@ -726,27 +726,30 @@ def test_onchip_split_barrier_timeout_fails_the_call(xp):
 @pytest.mark.parametrize("stop", ["each", "any", "none"])
 def test_onchip_adaptive_matches_resident_and_oracle(stop, xp):
     """Adaptive steps on chip (k_onchip's adaptive variant: four voltage arrays in LDS, the clause
-    memories in VGPRs, one code instance for both passes) == k_resident's adaptive step
-    (knob ONCHIP_ADAPTIVE = 0) bit for bit on every stop policy, per-replica dt included, and
-    replica 0 == the oracle's f32 simulate with tol 1e-3 (system.rs:111-139, :204-234)."""
+    memories in VGPRs, each pass its own code instance since round 5), at either pair offset and the
+    tiler's own choice, == k_resident's adaptive step (knob ONCHIP_ADAPTIVE = 0) bit for bit on every
+    stop policy, per-replica dt included, and replica 0 == the oracle's f32 simulate with tol 1e-3
+    (system.rs:111-139, :204-234)."""
     from odesat_amd import _lib
     f, (cp, v_, n_) = _instance(3000, 12600, 5)
     pol = {"each": ODESAT_STOP_EACH, "any": ODESAT_STOP_ANY, "none": ODESAT_STOP_NONE}[stop]
     B, K = 6, 30
     out = []
-    for ada in ("1", "0"):
+    for ada, off in (("1", None), ("1", "0"), ("1", "1"), ("0", None)):
         xp.set("ONCHIP_ADAPTIVE", ada)
+        xp.set("PAIR_OFF", off)
         with Solver(f, B, "f32") as s:
             assert s.algorithm == _lib.ODESAT_ALG_ONCHIP
             assert s.step_kernel(True) == ("k_onchip" if ada == "1" else "k_resident")
             s.init_state(9)
             r = s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=K, stop=pol, poll_interval=10)
             out.append((r, s.get_state()))
-    (r1, s1), (r2, s2) = out
-    assert np.array_equal(r1["first_sat_step"], r2["first_sat_step"]) and np.array_equal(r1["steps_done"], r2["steps_done"])
-    assert same(r1["dt"], r2["dt"])
-    for x, y in zip(s1, s2):
-        assert same(x, y)
+    r1, s1 = out[0]
+    for r2, s2 in out[1:]:
+        assert np.array_equal(r1["first_sat_step"], r2["first_sat_step"]) and np.array_equal(r1["steps_done"], r2["steps_done"])
+        assert same(r1["dt"], r2["dt"])
+        for x, y in zip(s1, s2):
+            assert same(x, y)
     o = Oracle(cp, v_, n_, 3000, "f32")
     ov = init_voltages(9, 0, 1, 3000)[0].astype(np.float32)
     oxs, oxl = o.init_short_term_memory(), np.ones(12600, np.float32)
@@ -851,11 +854,12 @@ def test_resident_adaptive_clone_in_hbm_matches_fused_and_oracle(stop, narrow, x
             s.init_state(3)
             r = s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=K, stop=pol, poll_interval=10)
             out.append((r, s.get_state()))
-    (r1, s1), (r2, s2) = out
-    assert np.array_equal(r1["first_sat_step"], r2["first_sat_step"]) and np.array_equal(r1["steps_done"], r2["steps_done"])
-    assert same(r1["dt"], r2["dt"])
-    for x, y in zip(s1, s2):
-        assert same(x, y)
+    r1, s1 = out[0]
+    for r2, s2 in out[1:]:
+        assert np.array_equal(r1["first_sat_step"], r2["first_sat_step"]) and np.array_equal(r1["steps_done"], r2["steps_done"])
+        assert same(r1["dt"], r2["dt"])
+        for x, y in zip(s1, s2):
+            assert same(x, y)
     o = Oracle(cp, v_, n_, 7000, "f64")
     ov = init_voltages(3, 0, 1, 7000)[0]
     oxs, oxl = o.init_short_term_memory(), np.ones(29400)
