@@ -663,8 +663,8 @@ __device__ __forceinline__ void pass2(const Args &a, float2 (&mr)[TR], float h, 
     __syncthreads();
 }
 
-// Pass 1 takes plain barriers, as the fixed pass does (split barriers there: -2.7 %,
-// profiles/r05final2_ab_p1plain.txt; 1 = split barriers, A/B only); pass 2 keeps its split barriers.
+// Pass 1 takes plain barriers, as the fixed pass does: split barriers in pass 1 cost 2.7 %
+// (profiles/r05final2_ab_p1plain.txt; 1 = split barriers, A/B only).  Pass 2 keeps its split barriers.
 #ifndef ONCHIP_ADA_P1_SPL
 #define ONCHIP_ADA_P1_SPL 0
 #endif
