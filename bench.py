@@ -783,6 +783,46 @@ def config4_leg(args, world, rank, local, dist, solver_cls=None, config="config4
         "digest": digest}
 
 
+def c5_capture(ps, warmup, probe, gsteps, dt, zeta, dev_sync, dist, world, gpu):
+    """The timed steps of one config-5 partition as a HIP graph, or None (eager steps) with the error
+    text when capturing or replaying fails (RCCL collectives inside a graph have only
+    run at world 1).  probe = 1: the last warmup step is a captured one-step graph, replayed, so a
+    replay failure also shows before the timed region.  Every rank takes the same path (a MAX
+    all-reduce of the failure flag), and the warmup is completed eagerly to `warmup` steps whatever
+    the probe ran (steps_done is the device's own count)."""
+    g, err = None, None
+
+    def agree():  # every rank replays only if every rank can
+        nonlocal g, err
+        if dist is not None and world > 1:
+            import torch
+            import torch.distributed as tdist
+            flag = torch.tensor([0.0 if g is not None else 1.0], device="cuda" if gpu else "cpu")
+            dist.all_reduce(flag, op=tdist.ReduceOp.MAX)
+            if float(flag.item()) > 0 and g is not None:
+                g, err = None, "another rank's HIP-graph capture or replay failed"
+
+    if ps.capturable():
+        gp = None
+        try:  # both graphs captured (nothing runs) before any rank replays a collective
+            gp = ps.graph(1, dt, zeta, stop=False) if probe else None
+            g = ps.graph(gsteps, dt, zeta, stop=False)
+        except Exception as e:  # noqa: BLE001 -- recorded in the leg, the partition steps eagerly
+            g, err = None, f"{type(e).__name__}: {e}"
+        agree()
+        if g is not None and gp is not None:
+            try:
+                gp.replay()
+                dev_sync()
+            except Exception as e:  # noqa: BLE001
+                g, err = None, f"{type(e).__name__}: {e}"
+            agree()
+    done = ps.status(stop=False)["steps_done"]
+    for _ in range(warmup - done):
+        ps.step(dt, zeta, stop=False)
+    return g, err
+
+
 def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5"):
     """BASELINE configs[4]: one replica of n = 1M, m = 4.2M partitioned over the ranks (strong
     scaling), every partition.  A step = the rank's kernels + its collective(s) over
@@ -838,14 +878,13 @@ def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5")
         ps = part_cls(cp, v_, n_, n, mode, comm=comm, device=local)
         setup = time.perf_counter() - t0
         ps.set_state(v0, xs0, xl0)
-        for _ in range(args.warmup):
+        probe = 1 if ps.capturable() and args.warmup > 0 else 0
+        for _ in range(args.warmup - probe):
             ps.step(dt, zeta, stop=False)
-        g = None
-        if ps.capturable():
-            gsteps = args.config5_graph or args.steps
-            if args.steps % gsteps:
-                raise SystemExit("bench.py: --steps must be a multiple of --config5-graph")
-            g = ps.graph(gsteps, dt, zeta, stop=False)  # captured, not run
+        gsteps = args.config5_graph or args.steps
+        if ps.capturable() and args.steps % gsteps:
+            raise SystemExit("bench.py: --steps must be a multiple of --config5-graph")
+        g, gerr = c5_capture(ps, args.warmup, probe, gsteps, dt, zeta, dev_sync, dist, world, gpu)
         if gpu:  # HIP events on the stream the partition's kernels and collectives run on
             stream = torch.cuda.current_stream()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -886,6 +925,7 @@ def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5")
                            "variables": "all_gather"}[name],
             "exchange_bytes_per_rank": ps.exchange_bytes(), "local_clauses_rank0": mloc,
             "graph_steps": gsteps if g is not None else 0, "setup_s": setup,
+            **({"graph_error": gerr} if gerr else {}),
             "roofline": {"bound": "hbm", "kernel": "k_part_clause3 + k_part_var (+ collective), per step",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_step": alg_bytes, "gpu_ms_per_step": per_step_s * 1e3,
@@ -911,8 +951,14 @@ def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5")
         else:  # the same steps at world 1 on this GPU: the reference trajectory
             ps = part_cls(cp, v_, n_, n, VARIABLES, comm=LocalComm(), device=local)
             ps.set_state(v0, xs0, xl0)
+            gr = None
             if ps.capturable():
-                ps.graph(total, dt, zeta, stop=False).replay()
+                try:
+                    gr = ps.graph(total, dt, zeta, stop=False)
+                except Exception:  # noqa: BLE001 -- the reference trajectory then steps eagerly
+                    gr = None
+            if gr is not None:
+                gr.replay()
             else:
                 for _ in range(total):
                     ps.step(dt, zeta, stop=False)

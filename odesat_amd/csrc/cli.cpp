@@ -75,6 +75,10 @@ struct Opts {
     int64_t steps = 0, batch = 0;
     uint64_t seed = 42;
     int device = 0, dtype = ODESAT_F64, gpus = 1;
+    // hidden test hooks (not in USAGE): steps per bounded call of an unbounded run, and shards that
+    // share the visible GPUs round-robin (tests rehearse --gpus G on a one-GPU box)
+    int64_t run_chunk = (int64_t)1 << 20;
+    bool share_devices = false;
 };
 
 [[noreturn]] void usage_error(const std::string &msg) {
@@ -116,6 +120,10 @@ Opts parse_args(int argc, char **argv) {
             std::printf("%s", USAGE);
             std::exit(0);
         }
+        if (a == "--share-devices") {  // hidden test hook, takes no value
+            o.share_devices = true;
+            continue;
+        }
         if (i + 1 >= argc) usage_error("a value is required for '" + a + "'");
         const char *val = argv[++i];
         auto f64 = [&](double *dst, bool *has) {
@@ -147,6 +155,9 @@ Opts parse_args(int argc, char **argv) {
             i64(&g, nullptr);
             if (g < 1) usage_error("--gpus must be >= 1");
             o.gpus = (int)g;
+        } else if (a == "--run-chunk") {  // hidden test hook
+            i64(&o.run_chunk, nullptr);
+            if (o.run_chunk < 1) usage_error("--run-chunk must be >= 1");
         } else if (a == "--dtype") {
             if (std::string(val) == "f64") o.dtype = ODESAT_F64;
             else if (std::string(val) == "f32") o.dtype = ODESAT_F32;
@@ -233,8 +244,7 @@ void run_shard(const Opts &o, const odesat_cnf *norm, Shard &sh, int nshards, Ba
     p.tol = o.tol;
     p.dt = o.dt;
     p.zeta = o.has_zeta ? o.zeta : -1.0;
-    int64_t chunk = (int64_t)1 << 20;  // steps per bounded call of an unbounded run
-    if (const char *ev = std::getenv("ODESAT_RUN_CHUNK")) chunk = std::max<int64_t>(1, std::atoll(ev));
+    const int64_t chunk = o.run_chunk;  // steps per bounded call of an unbounded run
     const bool bounded = o.has_steps || o.cmd == "batch";
     if (nshards == 1 || o.cmd != "inter") {
         if (!sh.err.empty()) return;
@@ -357,9 +367,9 @@ int main(int argc, char **argv) {
     } else if (n > 0) {
         int ndev = 0;
         if (odesat_device_count(&ndev)) return die("devices");
-        // ODESAT_SHARE_DEVICES=1 lets shards share the visible GPUs round-robin (tests rehearse
-        // --gpus G on a one-GPU box); otherwise every shard needs a GPU of its own
-        const bool share = std::getenv("ODESAT_SHARE_DEVICES") != nullptr;
+        // --share-devices lets shards share the visible GPUs round-robin (tests rehearse --gpus G on
+        // a one-GPU box); otherwise every shard needs a GPU of its own
+        const bool share = o.share_devices;
         if (o.gpus > 1 && o.gpus > ndev && !share) {
             std::fprintf(stderr, "Error: --gpus %d but %d GPU(s) are visible\n", o.gpus, ndev);
             return 1;

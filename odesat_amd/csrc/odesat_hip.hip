@@ -72,16 +72,16 @@ struct odesat_solver {
     int wv_wpw = 1;             // k_wave: replicas per workgroup sharing the LDS topology
     bool solo = false;          // k_solo (wave.hpp) instead of k_wave: one replica per workgroup, lanes' slots in registers
     int solo_nl = 64, solo_cpl = 1, solo_vpl = 1;  // k_solo: lanes per replica, clause / variable slots per lane
-    bool solo_fast = true;      // k_solo's short arithmetic on in-range states (ODESAT_SOLO_FAST=0: the general form)
+    bool solo_fast = true;      // k_solo's short arithmetic on in-range states (knob SOLO_FAST = 0: the general form)
     bool solo_cv = true;        // k_solo_cv (clause-held voltages) for the short arithmetic when it fits
     bool solo_cv_z0 = false;    // the formula has variables of degree 0 (k_solo_cv's variable slots)
     int4 *cv_rec = nullptr;     // [solo_nl solo_cpl] k_solo_cv's per-slot records (cv_layout.cpp)
     int32_t *cv_blk = nullptr;  // [n + 1] k_solo_cv's term block per variable (n: the zero block)
     int32_t cv_nb = 0;          // blocks in use
     int64_t cv_cost_plain = 0, cv_cost = 0;  // the bank model's LDS cycles per pass, plain / chosen layout
-    bool wave_fast = true;      // k_wave's likewise (ODESAT_WAVE_FAST=0)
-    bool res_fast = true;       // k_resident's likewise, 3-SAT only (ODESAT_RES_FAST=0)
-    bool res_rc = true;         // f64 fixed steps: register-cached tiles (resident.hpp; ODESAT_RES_RC=0)
+    bool wave_fast = true;      // k_wave's likewise (knob WAVE_FAST = 0)
+    bool res_fast = true;       // k_resident's likewise, 3-SAT only (knob RES_FAST = 0)
+    bool res_rc = true;         // f64 fixed steps: register-cached tiles (resident.hpp; knob RES_RC = 0)
     int wv_tw = 1;              // k_wave: waves per replica, fixed steps
     int wv_tw_ada = 1;          // ... adaptive steps (four barriers per step instead of two: at most 4)
     bool res_ada = false; // adaptive steps run k_resident (else FUSED on the same layout)
@@ -1373,6 +1373,12 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         lorder.assign(m, 0);
     } else if (res_r > 0 && !build_tiles(f, n, cap, res_r, s->uniform_k == 3, pairs, perm, tiles, lorder, wst, s->oc_off)) {
         res_r = 0;
+    } else if (res_r > 0 && pairs && s->dtype == ODESAT_F64 &&
+               (odesat::xp_get("RES_RC", 1) == 0 || ((int)tiles.size() + 2) / 4 * 4 < RES_RC_ADA + 16)) {
+        // f64: only the register-tile launches run the paired barriers (launch_resident); without them
+        // the paired tiling can only cost tiles, so such solvers take the plain tiling
+        pairs = false;
+        if (!build_tiles(f, n, cap, res_r, s->uniform_k == 3, pairs, perm, tiles, lorder, wst, s->oc_off)) res_r = 0;
     }
     if (res_r != 1) s->res_narrow = false;
     if (res_r == 0 && !odesat::xp_isset("GROUP_WIDTH")) {

@@ -293,6 +293,7 @@ __device__ __forceinline__ void pair_signal(uint32_t cnt, uint32_t ep) {
 // which the kernel reports to the host at its end: the call then fails instead of returning results
 // that raced.
 __device__ __forceinline__ void pair_wait(uint32_t cnt, uint32_t target, uint32_t limit) {
+    static_assert(WAVES == 8, "the asm's fault slot (offset:32 = 8 counters) and tid & 7 assume 8 waves");
     __builtin_amdgcn_sched_barrier(0);
     const uint32_t addr = cnt + 4u * (threadIdx.x & 7);
     uint32_t tmp, it;
@@ -1071,7 +1072,8 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     // a split-barrier wait that gave up (EP_TIMEOUT): the dv updates may have raced, so the call must
     // fail -- the fault word beside the stop word, read by the host after the call (ODESAT_EDEVICE)
     // (the fault slots after the pair counts; every wave's store to them precedes the steps' last barrier)
-    if ((ONCHIP_SPLITBAR & (ADA ? 2 : 1)) && lane < WAVES && lds_f(CNT + 4u * (WAVES + lane)) != 0.0f)
+    // (compared as a word: pair_wait stores the integer 1, a denormal that a flushing build would read as 0)
+    if ((ONCHIP_SPLITBAR & (ADA ? 2 : 1)) && lane < WAVES && __float_as_uint(lds_f(CNT + 4u * (WAVES + lane))) != 0u)
         atomicOr(reinterpret_cast<unsigned *>(a.stop + 1), 1u);
     if (lane == 0) {
         if (a.oop) a.par[g] = (uint8_t)q;

@@ -214,3 +214,85 @@ def test_roofline_reads_the_committed_profiles():
     assert r64["bound"] == "hbm" and r64["traffic"] < 0.9 * r64["algorithmic_bytes_per_launch"]
     assert 0.0 < r64["fabric_traffic"]["achieved"] < r64["achieved"] and "register tiles" in r64["note"]
     assert "Infinity-Cache hits are included" in r64["traffic_counts"] and "fabric" in r["traffic_counts"]
+
+
+class _Graph:
+    """A captured graph of the host stand-in: replay runs the steps (or raises, as a failed replay)."""
+
+    def __init__(self, ps, steps, fail):
+        self.ps, self.steps, self.fail = ps, steps, fail
+
+    def replay(self):
+        if self.fail:
+            raise RuntimeError("hipGraphLaunch failed (test)")
+        for _ in range(self.steps):
+            self.ps.step(0.01, self.ps._zeta)
+
+
+def _capturing_part(fail_capture_ranks=(), fail_replay_ranks=()):
+    """HostPart that claims capturable collectives (as PartitionedSolver does over RCCL) and whose
+    graph() raises on the given ranks, or returns graphs whose replay raises."""
+    from tests.host_standins import HostPart
+
+    class CapPart(HostPart):
+        def capturable(self):
+            return True
+
+        def graph(self, steps, dt, zeta, stop=True):
+            self._zeta = zeta
+            if self.comm.rank in fail_capture_ranks:
+                raise RuntimeError("stream capture of an RCCL collective failed (test)")
+            return _Graph(self, steps, self.comm.rank in fail_replay_ranks)
+
+    return CapPart
+
+
+@pytest.mark.parametrize("fail", ["capture", "replay", "none"])
+def test_config5_leg_graph_failure_steps_eagerly(fail):
+    """a partition whose HIP-graph capture (or the probe's first replay) raises is still
+    timed, eagerly, with graph_steps 0 and the error text in the leg; the digest and the step count
+    hold.  fail = none: the graph path (replays) runs every step too."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    from odesat_amd import workloads as wl
+    wl.CONFIGS["tiny5"] = TINY5
+    part = _capturing_part(fail_capture_ranks=(0,) if fail == "capture" else (),
+                           fail_replay_ranks=(0,) if fail == "replay" else ())
+    r5 = bench.config5_leg(_args(12, 3), 1, 0, 0, None, part_cls=part, config="tiny5")
+    d = r5["digest"]
+    assert d["variables_bit_exact"] and d["clauses_within_tol"] and d["clauses_rs_within_tol"] and d["steps"] == 15
+    for name in ("clauses", "clauses_rs", "variables"):
+        leg = r5[name]
+        assert leg["value"] > 0
+        if fail == "none":
+            assert leg["graph_steps"] == 12 and "graph_error" not in leg
+        else:
+            assert leg["graph_steps"] == 0 and "(test)" in leg["graph_error"], leg
+
+
+def _cap_worker(rank, world, port, outdir):
+    import torch.distributed as td
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from odesat_amd import workloads as wl
+    wl.CONFIGS["tiny5"] = TINY5
+    r5 = bench.config5_leg(_args(12, 3), world, rank, 0, td, part_cls=_capturing_part(fail_capture_ranks=(1,)),
+                           config="tiny5")
+    with open(os.path.join(outdir, f"r{rank}.json"), "w") as fh:
+        json.dump(r5, fh)
+    td.destroy_process_group()
+
+
+def test_config5_leg_one_rank_capture_failure_all_ranks_eager(tmp_path):
+    """World 2 over gloo: rank 1's capture fails, rank 0's succeeds; both ranks step eagerly (a MAX
+    all-reduce of the failure flag), so the collectives stay matched, and the digest holds."""
+    import torch.multiprocessing as mp
+    mp.spawn(_cap_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = (json.load(open(tmp_path / f"r{r}.json")) for r in (0, 1))
+    assert r0["digest"]["variables_bit_exact"] and r0["digest"]["steps"] == 15
+    for name in ("clauses", "clauses_rs", "variables"):
+        assert r0[name]["graph_steps"] == 0 and r1[name]["graph_steps"] == 0
+        assert "another rank" in r0[name]["graph_error"] and "(test)" in r1[name]["graph_error"]

@@ -215,17 +215,16 @@ def test_config2_bench_leg_kernels_bitexact(leg, prec, adaptive, kernel):
 # ----------------------------------------------------------------------------------- config 1 ---
 def test_config1_cli_solve_easy_adaptive_matches_oracle(tmp_path):
     """`odesat solve -f easy.cnf` exactly as BASELINE states config 1 (adaptive step, tol 1e-3,
-    -r 7, the reference's f64), run unbounded in bounded calls of 64 steps (ODESAT_RUN_CHUNK) so the
+    -r 7, the reference's f64), run unbounded in bounded calls of 64 steps (the hidden --run-chunk flag) so the
     continue path carries dt and the step count across calls: the printed assignment equals the f64
     oracle's continuous run of the same preprocessed formula from the same initial state, mapped
     back through the same trace, and satisfies the input."""
     from odesat_amd import preprocess as pp
     path = os.path.join(ROOT, "tests", "golden", "easy.cnf")
     out = tmp_path / "easy.txt"
-    env = dict(os.environ, ODESAT_RUN_CHUNK="64")
     binp = os.path.join(ROOT, "odesat_amd", "bin", "odesat")
-    r = subprocess.run([binp, "solve", "-f", path, "-o", str(out)], capture_output=True, text=True, timeout=300,
-                       env=env)
+    r = subprocess.run([binp, "solve", "-f", path, "-o", str(out), "--run-chunk", "64"], capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "Checking if solution vector satisfies formula: true" in r.stdout
     got = {}

@@ -344,15 +344,14 @@ def _planted_file(tmp_path, n=60, m=240, seed=9):
 
 @pytest.mark.parametrize("cmd", [("batch", "-n", "20000"), ("inter",)])
 def test_cli_gpus_matches_one_gpu(tmp_path, cmd):
-    """`odesat batch|inter --gpus 3` (shards sharing the box's GPU, ODESAT_SHARE_DEVICES) prints the
+    """`odesat batch|inter --gpus 3` (shards sharing the box's GPU, the hidden --share-devices flag) prints the
     same result and assignment as --gpus 1 (replicas keep their global indices)."""
     p = _planted_file(tmp_path)
     binp = os.path.join(ROOT, "odesat_amd", "bin", "odesat")
     outs = []
     for g in ("1", "3"):
-        env = dict(os.environ, ODESAT_SHARE_DEVICES="1")
-        r = subprocess.run([binp, cmd[0], "-f", str(p), *cmd[1:], "-b", "11", "-s", "0.1", "--seed", "5", "--gpus", g],
-                           capture_output=True, text=True, timeout=300, env=env)
+        r = subprocess.run([binp, cmd[0], "-f", str(p), *cmd[1:], "-b", "11", "-s", "0.1", "--seed", "5", "--gpus", g,
+                            "--share-devices"], capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr
         outs.append(r.stdout)
     assert "satisfies formula: true" in outs[0]
