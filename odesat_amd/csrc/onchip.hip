@@ -664,6 +664,12 @@ __device__ __forceinline__ void pass2(const Args &a, float2 (&mr)[TR], float h, 
     __syncthreads();
 }
 
+// Diagnostic builds only (-DONCHIP_ADA_SKIP=1 | 2, scripts/build_variant.sh; results are wrong): the
+// adaptive step without its second / first pass, so that PMC counters of the full build minus those of
+// a skip build give one pass's share.
+#ifndef ONCHIP_ADA_SKIP
+#define ONCHIP_ADA_SKIP 0
+#endif
 // Pass 1 takes plain barriers, as the fixed pass does: split barriers in pass 1 cost 2.7 %
 // (profiles/r05final2_ab_p1plain.txt; 1 = split barriers, A/B only).  Pass 2 keeps its split barriers.
 #ifndef ONCHIP_ADA_P1_SPL
@@ -914,7 +920,12 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
             const float hk = dtr, hhk = 0.5f * dtr, hqk = 0.25f * dtr;
             const uint32_t flag = UNS + 4u * (k & 1);
             float e = 0.0f;
+#if ONCHIP_ADA_SKIP == 2  // diagnostic build (results wrong): no pass 1, every step takes pass 2
+            if (lane == 0) lds_st(flag, 1.0f);
+            __syncthreads();
+#else
             pass1<TR, OFF>(a, mr, lane, flag, CNT, ep);  // the RHS at y into D, the unsat flag
+#endif
             ADA_STAMP(ada_st[0]);
             const bool uns = lds_f(flag) != 0.0f;  // uniform
             if (!uns) {  // an allsat replica takes no step (:122): drop pass 1's terms
@@ -943,7 +954,9 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                 }
                 __syncthreads();
                 ADA_STAMP(ada_st[1]);
+#if ONCHIP_ADA_SKIP != 1  // (diagnostic build 1: no pass 2)
                 pass2<TR, OFF>(a, mr, hk, lane, e, CNT, ep);  // the RHS at the half step, the memories' step
+#endif
                 ADA_STAMP(ada_st[2]);
                 // second half step (:130), max_error (:101-108); the same lane ownership as the final
                 // store below

@@ -308,11 +308,13 @@ def test_f32_tracks_f64_on_short_horizon():
 
 
 # ---------------------------------------------------------------- full size (BASELINE config 2) ---
-@pytest.mark.parametrize("pair_off", [None, "0"])
-def test_config2_full_size_subset_bitexact_and_properties(xp, pair_off):
+@pytest.mark.parametrize("B,pair_off", [(1024, None), (1024, "0"), (256, None)])
+def test_config2_full_size_subset_bitexact_and_properties(xp, B, pair_off):
     """n=10k, m=42k, B=1024 f32 for 12 steps: replicas {0, 517, 1023} bit-exact vs the oracle's f32
     restatement; every replica: v in [-1,1], xs in [eps, 1-eps], xl in [1, 1e4 m], finite.  The
-    solver's wave-paired tiles (k_onchip<90, 1>) and the other pair offset (91 tiles: k_onchip<92, 0>)."""
+    solver's wave-paired tiles (k_onchip<90, 1>) and the other pair offset (91 tiles: k_onchip<92, 0>).
+    B = 256: BASELINE configs[1]'s own batch (one replica per CU, one round of workgroups), replicas
+    {0, 127, 255} (VERDICT r5 #6)."""
     if pair_off is not None:
         xp.set("PAIR_OFF", pair_off)
     c = wl.CONFIGS["config2"]
@@ -320,12 +322,13 @@ def test_config2_full_size_subset_bitexact_and_properties(xp, pair_off):
     cp, v_, n_ = wl.formula_arrays(var, neg)
     f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
     o = Oracle(cp, v_, n_, c["n"], "f32")
-    B, K = 1024, 12
+    K = 12
     with Solver(f, B, "f32") as s:
+        assert s.step_kernel(False) == "k_onchip"
         s.init_state(42)
         r = s.simulate(dt=0.01, max_steps=K, stop=ODESAT_STOP_NONE)
         assert r["steps_run"] == K and np.all(r["steps_done"] == K)
-        pick = [0, 517, 1023]
+        pick = [0, 517, 1023] if B == 1024 else [0, 127, 255]
         states = {b: s.get_state(b, 1) for b in pick}
         v, xs, xl = s.get_state()
     assert np.isfinite(v).all() and np.isfinite(xs).all() and np.isfinite(xl).all()
@@ -770,7 +773,8 @@ def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, adaptive, 
     tests/test_tiling.py's hook) for the register prefix (the host needs RC + 16); the adaptive one is
     large enough (n = 7 000) for the clone-in-HBM kernel.  Round 5: the default runs them on wave-paired
     tiles (resident.hpp PAIRS: a barrier after every second tile) at either pair offset; == plain tiles
-    (knob RES_PAIRS = 0)."""
+    (knob RES_PAIRS = 0).  Round 6: adaptive launches recompute the streamed tiles' first-pass mn from
+    y's voltages gathered from HBM (resident.hpp YG) == the stored mn (knob RES_YG = 0)."""
     from odesat_amd import _lib
     n, m = (7000, 29400) if adaptive else (3000, 12600)
     f, (cp, v_, n_) = _instance(n, m, 5)
@@ -778,10 +782,12 @@ def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, adaptive, 
     B = 4 if adaptive else 6
     kw = dict(adaptive=True, tol=1e-3) if adaptive else dict(dt=0.05)
     out = []
-    for rc, pairs, off in (("1", "1", None), ("1", "1", "0"), ("1", "1", "1"), ("1", "0", None), ("0", "0", None)):
+    for rc, pairs, off, yg in (("1", "1", None, None), ("1", "1", "0", None), ("1", "1", "1", None), ("1", "0", None, None),
+                               ("0", "0", None, None), ("1", "1", None, "0"), ("1", "0", None, "0")):
         xp.set("RES_RC", rc)
         xp.set("RES_PAIRS", pairs)
         xp.set("PAIR_OFF", off)  # both pair offsets (PAIRS = 1, 2), and the tiler's own choice
+        xp.set("RES_YG", yg)  # adaptive: the second pass's mn from y's gathered voltages (default) or stored
         with Solver(f, B, "f64") as s:
             assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.step_kernel(adaptive) == "k_resident"
             s.init_state(9)
