@@ -34,7 +34,6 @@ const char *const KNOBS[] = {
     "RES_NARROW",       // 1 / 0: k_resident with one wave (64-clause tiles) per replica / never
     "RES_FAST",         // 0: k_resident's general arithmetic on 3-SAT
     "RES_RC",           // 0: no register-cached tiles in the f64 k_resident
-    "RES_YG",           // 0: the f64 adaptive register-tile k_resident stores the first pass's mn (no y gathers)
     "RES_VFG",          // 0: f64 adaptive steps whose clone does not fit in LDS on FUSED, not k_resident
     "RES_PAIRS",        // 0: the f64 k_resident on plain tiles (a barrier after every tile) instead of wave-paired ones
     // partition (odesat_part_create)

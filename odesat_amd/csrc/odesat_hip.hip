@@ -82,7 +82,6 @@ struct odesat_solver {
     bool wave_fast = true;      // k_wave's likewise (knob WAVE_FAST = 0)
     bool res_fast = true;       // k_resident's likewise, 3-SAT only (knob RES_FAST = 0)
     bool res_rc = true;         // f64 fixed steps: register-cached tiles (resident.hpp; knob RES_RC = 0)
-    bool res_yg = false;        // f64 adaptive register-tile launches: pass 2 gathers y (resident.hpp YG; knob RES_YG = 1; measured slower)
     int wv_tw = 1;              // k_wave: waves per replica, fixed steps
     int wv_tw_ada = 1;          // ... adaptive steps (four barriers per step instead of two: at most 4)
     bool res_ada = false; // adaptive steps run k_resident (else FUSED on the same layout)
@@ -768,15 +767,15 @@ int onchip_setup(odesat_solver *s, const std::vector<int32_t> &tiles, const std:
 }
 
 template <typename T, int R, bool ADA, bool K3, int NTHR = ResShape<R>::NTH, bool VFG = false, bool FAST = false,
-          int RC = 0, int PAIRS = 0, bool YG = false>
+          int RC = 0, int PAIRS = 0>
 int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     const size_t lds = res_lds_bytes(s->n, R, sizeof(T), ADA && !VFG);
-    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR, VFG, FAST, RC, PAIRS, YG>),
+    HIP_TRY(odesat::ensure_max_lds(reinterpret_cast<const void *>(&k_resident<T, R, ADA, K3, NTHR, VFG, FAST, RC, PAIRS>),
                                    (int)RES_LDS_MAX));
     {
         Timed tm(s, 0);
-        hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR, VFG, FAST, RC, PAIRS, YG>), dim3(s->G), dim3(NTHR), lds,
-                           s->stream, a);
+        hipLaunchKernelGGL((k_resident<T, R, ADA, K3, NTHR, VFG, FAST, RC, PAIRS>), dim3(s->G), dim3(NTHR), lds, s->stream,
+                           a);
     }
     HIP_TRY(hipGetLastError());
     return ODESAT_OK;
@@ -930,7 +929,6 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
     a.cf = (T *)s->cf;
     a.ch = (T *)s->ch;
     a.vf = (T *)s->vf;
-    a.vy = (T *)s->vh;  // (the half-step scratch of FUSED; k_resident's YG keeps y there)
     a.dtr = (T *)s->dtr;
     a.act = s->act;
     a.sat_step = s->sat_step;
@@ -957,17 +955,11 @@ int launch_resident(odesat_solver *s, int step0, int nsteps, bool adaptive, doub
                         : launch_resident_k<T, 1, true, false, RES_NARROW, true>(s, a);
         if constexpr (std::is_same<T, double>::value) {
             // the first RES_RC_ADA tiles' memories and first-pass mn in VGPRs for the launch (resident.hpp)
-            // (YG: the second pass recomputes the streamed tiles' mn from y's voltages in HBM)
-            constexpr int NT1 = ResShape<1>::NTH;
-            if (f3 && s->res_rc && s->res_ntiles >= RES_RC_ADA + 16) {
-                if (s->res_yg)
-                    return !s->res_pairs ? launch_resident_k<T, 1, true, true, NT1, true, true, RES_RC_ADA, 0, true>(s, a)
-                           : s->oc_off   ? launch_resident_k<T, 1, true, true, NT1, true, true, RES_RC_ADA, 2, true>(s, a)
-                                         : launch_resident_k<T, 1, true, true, NT1, true, true, RES_RC_ADA, 1, true>(s, a);
-                return !s->res_pairs ? launch_resident_k<T, 1, true, true, NT1, true, true, RES_RC_ADA>(s, a)
-                       : s->oc_off   ? launch_resident_k<T, 1, true, true, NT1, true, true, RES_RC_ADA, 2>(s, a)
-                                     : launch_resident_k<T, 1, true, true, NT1, true, true, RES_RC_ADA, 1>(s, a);
-            }
+            if (f3 && s->res_rc && s->res_ntiles >= RES_RC_ADA + 16)
+                return !s->res_pairs ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA>(s, a)
+                       : s->oc_off
+                           ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA, 2>(s, a)
+                           : launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true, RES_RC_ADA, 1>(s, a);
         }
         return f3   ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true, true>(s, a)
                : k3 ? launch_resident_k<T, 1, true, true, ResShape<1>::NTH, true>(s, a)
@@ -1328,7 +1320,7 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         // fills 16 waves (4 per SIMD), fewer while the instance has under 32 clauses per wave.
         // Measured (config 3, B = 1024, adaptive / fixed): 59 / 120 M replica-steps/s at TW = 1,
         // 77 / 162 M at TW = 4; hard.cnf (m = 160) at B = 1: 36 / 17 ms per 10 000 steps at TW = 1,
-        // 26 / 14 ms at TW = 4.  ODESAT_WAVE_TEAM = 1/2/4/8/16 overrides (if the shape exists).
+        // 26 / 14 ms at TW = 4.  The WAVE_TEAM knob (1/2/4/8/16) overrides (if the shape exists).
         s->wv_tw = 16 / s->wv_wpw;
         while (s->wv_tw > 1 && 32 * (int64_t)s->wv_tw > m) s->wv_tw /= 2;
         // adaptive steps order their phases with four barriers, fixed ones with two: a wide team pays
@@ -1491,7 +1483,6 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
         s->res_ada = res_fits(n, res_r, s->tsize, true);
         s->res_fast = odesat::xp_get("RES_FAST", 1) != 0;
         s->res_rc = odesat::xp_get("RES_RC", 1) != 0;
-        s->res_yg = odesat::xp_get("RES_YG", 0) != 0;
         // adaptive steps whose clone of v does not fit beside v and dv (f64 at n > 6.7 k, the CLI's
         // default precision and mode on config 2): k_resident with the clone in HBM instead of FUSED
         // on the one-replica layout.  The RES_VFG knob = 0 keeps FUSED.

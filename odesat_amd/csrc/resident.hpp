@@ -57,7 +57,6 @@ template <typename T> struct RArgs {
     uint8_t *par;                      // flipped by an out-of-place launch
     T *cf, *ch;                        // adaptive scratch memories (full step, first half)
     T *vf;                             // adaptive full-step voltages in HBM (VFG: LDS holds only v and dv)
-    T *vy;                             // YG: y's voltages (the step's start) in HBM, gathered by pass 2
     T *dtr;
     uint8_t *act;
     int64_t *sat_step, *steps_done;
@@ -79,7 +78,6 @@ enum Pass : int { P_FIXED = 0, P_ADA1 = 1, P_ADA2 = 2 };
 template <typename T, int R> struct ResCtx {
     T *vL, *dvL, *vfL;  // LDS
     T *cf, *ch;         // this group's adaptive scratch: cf holds each clause's first-pass C
-    T *vyG;             // YG: this group's copy of y's voltages (HBM)
     int r, lc;          // this lane's replica and clause-lane index
     int w, wl;          // PAIRS: this lane's wave (uniform) and lane in it
 };
@@ -120,7 +118,6 @@ template <typename P> __device__ __forceinline__ P *at(P *base, uint32_t elem) {
 template <typename T> struct TileLoad {
     int4 lit;
     Vec<T, 2> mem, full;
-    T y[3];  // YG, pass 2: y's voltages of the clause's variables (res_gather_y)
     bool ok;
 };
 
@@ -155,7 +152,7 @@ template <typename T> __device__ __forceinline__ void res_stm(T *p, const Vec<T,
 
 // Loads of tile t (t >= ntiles: nothing to do, a valid address is read).  Unconditional, so the
 // ring's loads stay in flight across iterations (no control flow for the wait counters to merge).
-template <typename T, int R, int PK, int PAIRS = 0, bool YG = false>
+template <typename T, int R, int PK, int PAIRS = 0>
 __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CM, int t,
                                           TileLoad<T> &ld, bool mem = true) {
     const int cc = res_slot<T, R, PAIRS>(a, x, t, ld.ok);  // a valid clause
@@ -164,16 +161,7 @@ __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> 
     ld.lit = *at(a.cl4, (uint32_t)cc);
     const uint32_t ci = (uint32_t)(cc * R + x.r) * 2u;  // 32-bit offsets from the group's base
     if (mem) ld.mem = res_ldm<T>(at(CM, ci));  // (adaptive: y's memories, untouched until the second pass stores)
-    if (PK == P_ADA2 && mem && !YG) ld.full.e[0] = *at((const T *)x.cf, ci / 2u);  // the first pass's C
-}
-
-// YG (f64 adaptive register-tile kernels, pass 2 of a streamed tile): y's three voltages of the clause
-// in slot ld, from the group's HBM copy that the variable phase after pass 1 wrote (L2-resident: 80 KB
-// per replica at config 2).  Issued two tiles ahead of the clause, once its literals have arrived.
-template <typename T, int R> __device__ __forceinline__ void res_gather_y(const ResCtx<T, R> &x, TileLoad<T> &ld) {
-    ld.y[0] = *at((const T *)x.vyG, (uint32_t)((ld.lit.x >> 1) * R + x.r));
-    ld.y[1] = *at((const T *)x.vyG, (uint32_t)((ld.lit.y >> 1) * R + x.r));
-    ld.y[2] = *at((const T *)x.vyG, (uint32_t)((ld.lit.z >> 1) * R + x.r));
+    if (PK == P_ADA2 && mem) ld.full.e[0] = *at((const T *)x.cf, ci / 2u);  // the first pass's C
 }
 
 // The adaptive step's candidates for one clause's memories from y's memories and the first pass's
@@ -236,7 +224,7 @@ template <typename T> struct Pend {
 // One 3-SAT clause of tile t from its prefetched loads: C, the memories' update and the three dv
 // terms (system.rs:43-88).  Voltages are read-only during a pass, so this runs one tile ahead of
 // the dv updates.
-template <typename T, int R, int PK, bool FAST = false, int PAIRS = 0, bool YG = false>
+template <typename T, int R, int PK, bool FAST = false, int PAIRS = 0>
 __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R> &x, T *CM, int t,
                                             const TileLoad<T> &ld, Pend<T> &P, bool on, T h, bool &uns, T &e,
                                             bool copy) {
@@ -262,15 +250,9 @@ __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R
         const T hh = (T)0.5 * h, hq = (T)0.25 * h;
         T xs = ld.mem.e[0], xl = ld.mem.e[1], xs_f = xs, xl_f = xl;
         if (PK == P_ADA2) {  // y's memories -> the full-step clone and the first half step (:124-128)
-            // the first pass's mn: stored by it (C scratch), or (YG) recomputed from y's voltages with
-            // solo_terms' own expressions -- the same bits
-            T mn1 = ld.full.e[0];
-            if constexpr (YG) {
-                const T one = (T)1.0;
-                const T y0 = fma(nq_of<T>(sg[0]), ld.y[0], one), y1 = fma(nq_of<T>(sg[1]), ld.y[1], one),
-                        y2 = fma(nq_of<T>(sg[2]), ld.y[2], one);
-                mn1 = dmin(dmin(y0, y1), y2);
-            }
+            // (the first pass's mn from the C scratch: recomputing it from y's voltages gathered from HBM
+            // measured 22 % slower)
+            const T mn1 = ld.full.e[0];
             solo_mem<T>(xs, xl, mn1, hh, h, a.xl_max, xs_f, xl_f);
             solo_mem<T>(ld.mem.e[0], ld.mem.e[1], mn1, hq, hh, a.xl_max, xs, xl);
         }
@@ -285,7 +267,7 @@ __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R
             solo_mem<T>(xs, xl, mn, hh, h, a.xl_max, o.e[0], o.e[1]);
             res_stm<T>(at(CM, ci), o);
         } else if (PK == P_ADA1) {
-            if (!YG) *at(x.cf, ci / 2u) = mn;  // (YG: pass 2 recomputes it)
+            *at(x.cf, ci / 2u) = mn;
         } else {
             Vec<T, 2> o;
             solo_mem<T>(xs, xl, mn, hq, hh, a.xl_max, o.e[0], o.e[1]);  // second half step (:130)
@@ -430,44 +412,39 @@ __device__ __forceinline__ void res_clause3_reg(const RArgs<T> &a, const ResCtx<
 // Iteration TT of the pipeline below with a static tile index: tile TT+1's clause from the registers
 // (TT+1 < RC) or from its slot, tile TT's terms applied, the slot refilled with tile TT+1+D (its
 // memories only if that tile streams).
-template <typename T, int R, int PK, bool FAST, int RC, int D, int PAIRS, bool YG, int TT>
+template <typename T, int R, int PK, bool FAST, int RC, int D, int PAIRS, int TT>
 __device__ __forceinline__ void res_iter3_rc(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM,
                                              TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h, bool &uns, T &e,
                                              Vec<T, 2> (&rm)[RC], T (&rmn)[RC]) {
     Pend<T> Q;
     TileLoad<T> &S = b[(TT + 1) % D];
     if constexpr (TT + 1 < RC) res_clause3_reg<T, R, PK>(a, x, S, Q, on, h, uns, e, rm[TT + 1], rmn[TT + 1]);
-    else res_clause3<T, R, PK, FAST, PAIRS, YG>(a, x, CM, TT + 1, S, Q, on, h, uns, e, CMr != CM);
+    else res_clause3<T, R, PK, FAST, PAIRS>(a, x, CM, TT + 1, S, Q, on, h, uns, e, CMr != CM);
     res_apply3<T, R>(x, P);
-    // YG: tile TT+3's y gathers (its literals arrived; issued before the refill so that waiting on
-    // them two tiles later does not wait on the refill's loads)
-    if constexpr (YG && PK == P_ADA2 && TT + 3 >= RC) res_gather_y<T, R>(x, b[(TT + 3) % D]);
-    res_load3<T, R, PK, PAIRS, YG>(a, x, CMr, TT + 1 + D, S, TT + 1 + D >= RC);
+    res_load3<T, R, PK, PAIRS>(a, x, CMr, TT + 1 + D, S, TT + 1 + D >= RC);
 #ifdef RES_TIMING_PAIRS  // timing-only diagnostic build (results race): a barrier after odd tiles only
     if (TT & 1)
 #endif
     if constexpr (res_bar_after<PAIRS>(TT)) __syncthreads();  // PAIRS: after the pair's second tile only
     P = Q;
 }
-template <typename T, int R, int PK, bool FAST, int RC, int D, int PAIRS, bool YG, int... Ts>
+template <typename T, int R, int PK, bool FAST, int RC, int D, int PAIRS, int... Ts>
 __device__ __forceinline__ void res_prefix(std::integer_sequence<int, Ts...>, const RArgs<T> &a, const ResCtx<T, R> &x,
                                            const T *CMr, T *CM, TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h,
                                            bool &uns, T &e, Vec<T, 2> (&rm)[RC], T (&rmn)[RC]) {
-    (res_iter3_rc<T, R, PK, FAST, RC, D, PAIRS, YG, Ts>(a, x, CMr, CM, b, P, on, h, uns, e, rm, rmn), ...);
+    (res_iter3_rc<T, R, PK, FAST, RC, D, PAIRS, Ts>(a, x, CMr, CM, b, P, on, h, uns, e, rm, rmn), ...);
 }
 
 // One step of the 3-SAT tile pipeline: the terms of tile t+1 are computed from slot S (which is
 // then refilled with tile t+1+RES_DEPTH), tile t's terms P are applied to dv, barrier (tile t+1
 // may touch the same dv entries).
-template <typename T, int R, int PK, bool FAST = false, int D = res_depth<T>(), int PAIRS = 0, bool BAR = true,
-          bool YG = false>
+template <typename T, int R, int PK, bool FAST = false, int D = res_depth<T>(), int PAIRS = 0, bool BAR = true>
 __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, int t,
-                                          TileLoad<T> &S, TileLoad<T> &Gs, Pend<T> &P, bool on, T h, bool &uns, T &e) {
+                                          TileLoad<T> &S, Pend<T> &P, bool on, T h, bool &uns, T &e) {
     Pend<T> Q;
-    res_clause3<T, R, PK, FAST, PAIRS, YG>(a, x, CM, t + 1, S, Q, on, h, uns, e, CMr != CM);  // Q.ok = false past the last tile
+    res_clause3<T, R, PK, FAST, PAIRS>(a, x, CM, t + 1, S, Q, on, h, uns, e, CMr != CM);  // Q.ok = false past the last tile
     res_apply3<T, R>(x, P);
-    if constexpr (YG && PK == P_ADA2) res_gather_y<T, R>(x, Gs);  // tile t+3 (res_iter3_rc)
-    res_load3<T, R, PK, PAIRS, YG>(a, x, CMr, t + 1 + D, S);
+    res_load3<T, R, PK, PAIRS>(a, x, CMr, t + 1 + D, S);
 #ifdef RES_TIMING_PAIRS  // timing-only diagnostic build (results race): a barrier after odd tiles only
     if (t & 1)
 #endif
@@ -475,18 +452,18 @@ __device__ __forceinline__ void res_iter3(const RArgs<T> &a, const ResCtx<T, R> 
     P = Q;
 }
 // Iterations t0 + Is of the pipeline (t0 even), slot (slot0 + Is) % D each, with their static barriers.
-template <typename T, int R, int PK, bool FAST, int D, int PAIRS, bool YG, int... Is>
+template <typename T, int R, int PK, bool FAST, int D, int PAIRS, int... Is>
 __device__ __forceinline__ void res_block(std::integer_sequence<int, Is...>, const RArgs<T> &a, const ResCtx<T, R> &x,
                                           const T *CMr, T *CM, int t0, TileLoad<T> (&b)[D], Pend<T> &P, bool on, T h,
                                           bool &uns, T &e) {
-    (res_iter3<T, R, PK, FAST, D, PAIRS, res_bar_after<PAIRS>(Is), YG>(a, x, CMr, CM, t0 + Is, b[(Is + 1) % D],
-                                                                       b[(Is + 3) % D], P, on, h, uns, e),
+    (res_iter3<T, R, PK, FAST, D, PAIRS, res_bar_after<PAIRS>(Is)>(a, x, CMr, CM, t0 + Is, b[(Is + 1) % D], P, on, h, uns,
+                                                                   e),
      ...);
 }
 
 // One RHS pass over all tiles: dv (LDS) accumulates; memories are read from CMr (or the adaptive
 // scratch) and written by kind (P_FIXED: to CM).  Ends with a barrier (dv complete).
-template <typename T, int R, int PK, bool K3, bool FAST = false, int RC = 0, int PAIRS = 0, bool YG = false>
+template <typename T, int R, int PK, bool K3, bool FAST = false, int RC = 0, int PAIRS = 0>
 __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &x, const T *CMr, T *CM, bool on, T h,
                                          bool &uns, T &e, Vec<T, 2> (&rm)[RC > 0 ? RC : 1], T (&rmn)[RC > 0 ? RC : 1]) {
     const int NT_ = a.ntiles;
@@ -496,7 +473,6 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
         static_assert(D == 4 || D == 8 || (D == 6 && RC > 0), "the pipeline below is unrolled for 4, 6 or 8 slots");
         static_assert(RC == 0 || (FAST && RC % D == 0 && RC >= D),
                       "register tiles: short-form steps, whole ring blocks (the host needs ntiles > RC + D)");
-        static_assert(!YG || (RC >= 4 && D == 4), "YG: the y gathers run two tiles ahead in a ring of 4 after >= 4 register tiles");
         // the host pads 3-SAT tilings to a multiple of 4 tiles (empty tiles), so the unrolled loop
         // below runs whole (D = 8: blocks of 8, then at most one static block of 4; D = 6, register
         // tiles only (a sweep point of RES_RC_DEPTH): blocks of 6, then a static block of 4 or 2)
@@ -507,13 +483,13 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
         TileLoad<T> b[D];
         Pend<T> P;
 #pragma unroll
-        for (int i = 0; i < D; ++i) res_load3<T, R, PK, PAIRS, YG>(a, x, CMr, i, b[i], i >= RC);
+        for (int i = 0; i < D; ++i) res_load3<T, R, PK, PAIRS>(a, x, CMr, i, b[i], i >= RC);
         int t0 = 0;
         if constexpr (RC > 0) {
             res_clause3_reg<T, R, PK>(a, x, b[0], P, on, h, uns, e, rm[0], rmn[0]);
-            res_load3<T, R, PK, PAIRS, YG>(a, x, CMr, D, b[0], D >= RC);
-            res_prefix<T, R, PK, FAST, RC, D, PAIRS, YG>(std::make_integer_sequence<int, RC>{}, a, x, CMr, CM, b, P, on,
-                                                         h, uns, e, rm, rmn);
+            res_load3<T, R, PK, PAIRS>(a, x, CMr, D, b[0], D >= RC);
+            res_prefix<T, R, PK, FAST, RC, D, PAIRS>(std::make_integer_sequence<int, RC>{}, a, x, CMr, CM, b, P, on, h,
+                                                     uns, e, rm, rmn);
             t0 = RC;
         } else {
             res_clause3<T, R, PK, FAST, PAIRS>(a, x, CM, 0, b[0], P, on, h, uns, e, CMr != CM);
@@ -521,20 +497,19 @@ __device__ __forceinline__ void res_pass(const RArgs<T> &a, const ResCtx<T, R> &
         }
         // iteration t computes tile t+1 from slot (t+1) % D (t0 stays even: RC and D are multiples of 4)
         for (; t0 + D <= NT_; t0 += D)
-            res_block<T, R, PK, FAST, D, PAIRS, YG>(std::make_integer_sequence<int, D>{}, a, x, CMr, CM, t0, b, P, on, h,
-                                                    uns, e);
+            res_block<T, R, PK, FAST, D, PAIRS>(std::make_integer_sequence<int, D>{}, a, x, CMr, CM, t0, b, P, on, h, uns, e);
         if constexpr (D == 8) {
             if (t0 < NT_)  // four tiles left: slots 1 .. 4
-                res_block<T, R, PK, FAST, D, PAIRS, false>(std::make_integer_sequence<int, 4>{}, a, x, CMr, CM, t0, b, P, on,
-                                                           h, uns, e);
+                res_block<T, R, PK, FAST, D, PAIRS>(std::make_integer_sequence<int, 4>{}, a, x, CMr, CM, t0, b, P, on,
+                                                    h, uns, e);
         }
         if constexpr (D == 6) {  // (t0 - RC is a multiple of 6 and NT_ - RC is even)
             if (NT_ - t0 == 4)
-                res_block<T, R, PK, FAST, D, PAIRS, false>(std::make_integer_sequence<int, 4>{}, a, x, CMr, CM, t0, b, P, on,
-                                                           h, uns, e);
+                res_block<T, R, PK, FAST, D, PAIRS>(std::make_integer_sequence<int, 4>{}, a, x, CMr, CM, t0, b, P, on,
+                                                    h, uns, e);
             else if (NT_ - t0 == 2)
-                res_block<T, R, PK, FAST, D, PAIRS, false>(std::make_integer_sequence<int, 2>{}, a, x, CMr, CM, t0, b, P, on,
-                                                           h, uns, e);
+                res_block<T, R, PK, FAST, D, PAIRS>(std::make_integer_sequence<int, 2>{}, a, x, CMr, CM, t0, b, P, on,
+                                                    h, uns, e);
         }
         if constexpr (PAIRS != 0) __syncthreads();  // dv complete whatever the last tile's parity
     } else {
@@ -573,14 +548,9 @@ __device__ unsigned long long g_res_clk[4096 * 64];
 #else
 #define RES_STAMP(i) do {} while (0)
 #endif
-// YG (f64 adaptive register-tile launches): the first pass stores no mn for streamed tiles; the variable
-// phase after it writes y's voltages to HBM (a.vy, the replica's n words) and the second pass gathers
-// them to recompute each streamed clause's first-pass mn: 16 bytes per streamed clause and step less
-// HBM traffic (the mn write and read-back) for n words written and 3 L2 gathers per clause.
 template <typename T, int R, bool ADAPTIVE, bool K3, int NTHR, bool VFG = false, bool FAST = false, int RC = 0,
-          int PAIRS = 0, bool YG = false>
+          int PAIRS = 0>
 __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
-    static_assert(!YG || (ADAPTIVE && VFG && RC > 0), "YG: the VFG adaptive register-tile kernels");
     static_assert(!FAST || K3, "the short forms are 3-SAT only (res_clause_any has none)");
     static_assert(RC == 0 || (FAST && R == 1), "register tiles: short-form steps, R = 1");
     static_assert(!PAIRS || (FAST && R == 1 && NTHR == 512), "wave-paired tiles: 8 waves, one replica, short forms");
@@ -604,7 +574,6 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
     x.vL = reinterpret_cast<T *>(res_smem);
     x.dvL = x.vL + nR;
     x.vfL = VFG ? a.vf + (size_t)blockIdx.x * nR : x.dvL + nR;
-    x.vyG = YG ? a.vy + (size_t)blockIdx.x * nR : nullptr;
     const bool p = __builtin_amdgcn_readfirstlane((int)a.par[g]) != 0;  // uniform: SGPR bases
     const bool oop = !ADAPTIVE && a.oop;
     T *V = (p ? a.v1 : a.v0) + (size_t)g * nR;
@@ -678,7 +647,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
                 }
             }
         } else {  // euler_step (system.rs:111-139), per-replica dt
-            res_pass<T, R, P_ADA1, K3, FAST, RC, PAIRS, YG>(a, x, CM, CM, on, h, uns, e, rm, rmn);
+            res_pass<T, R, P_ADA1, K3, FAST, RC, PAIRS>(a, x, CM, CM, on, h, uns, e, rm, rmn);
             if (uns) unsL[x.r] = 1u;
             __syncthreads();
             const bool st = on && unsL[x.r] != 0u;  // allsat replicas take no step (:122)
@@ -689,7 +658,6 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
                 x.dvL[idx] = (T)0.0;
                 if (st) {
                     const T v = x.vL[idx];
-                    if (YG) x.vyG[idx] = v;  // y, gathered by the second pass (visible after the barrier below)
                     x.vfL[idx] = dmin(dmax(v + hf * d, (T)-1.0), (T)1.0);   // full-step clone
                     x.vL[idx] = dmin(dmax(v + half * d, (T)-1.0), (T)1.0);  // first half step
                 }
@@ -700,7 +668,7 @@ __global__ __launch_bounds__(NTHR) void k_resident(RArgs<T> a) {
             for (int j = 0; j < R; ++j) any_st = any_st || (actL[j] != 0 && unsL[j] != 0u);
             if (any_st) {  // uniform
                 bool u2 = false;
-                res_pass<T, R, P_ADA2, K3, FAST, RC, PAIRS, YG>(a, x, CM, CM, st, h, u2, e, rm, rmn);
+                res_pass<T, R, P_ADA2, K3, FAST, RC, PAIRS>(a, x, CM, CM, st, h, u2, e, rm, rmn);
                 for (int i = x.lc; i < a.n; i += NL) {
                     const int idx = i * R + x.r;
                     const T d = x.dvL[idx];

@@ -773,8 +773,7 @@ def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, adaptive, 
     tests/test_tiling.py's hook) for the register prefix (the host needs RC + 16); the adaptive one is
     large enough (n = 7 000) for the clone-in-HBM kernel.  Round 5: the default runs them on wave-paired
     tiles (resident.hpp PAIRS: a barrier after every second tile) at either pair offset; == plain tiles
-    (knob RES_PAIRS = 0).  Round 6: adaptive launches recompute the streamed tiles' first-pass mn from
-    y's voltages gathered from HBM (resident.hpp YG) == the stored mn (knob RES_YG = 0)."""
+    (knob RES_PAIRS = 0)."""
     from odesat_amd import _lib
     n, m = (7000, 29400) if adaptive else (3000, 12600)
     f, (cp, v_, n_) = _instance(n, m, 5)
@@ -782,12 +781,10 @@ def test_resident_f64_register_tiles_match_streaming_and_oracle(stop, adaptive, 
     B = 4 if adaptive else 6
     kw = dict(adaptive=True, tol=1e-3) if adaptive else dict(dt=0.05)
     out = []
-    for rc, pairs, off, yg in (("1", "1", None, None), ("1", "1", "0", None), ("1", "1", "1", None), ("1", "0", None, None),
-                               ("0", "0", None, None), ("1", "1", None, "0"), ("1", "0", None, "0")):
+    for rc, pairs, off in (("1", "1", None), ("1", "1", "0"), ("1", "1", "1"), ("1", "0", None), ("0", "0", None)):
         xp.set("RES_RC", rc)
         xp.set("RES_PAIRS", pairs)
         xp.set("PAIR_OFF", off)  # both pair offsets (PAIRS = 1, 2), and the tiler's own choice
-        xp.set("RES_YG", yg)  # adaptive: the second pass's mn from y's gathered voltages (default) or stored
         with Solver(f, B, "f64") as s:
             assert s.algorithm == _lib.ODESAT_ALG_RESIDENT and s.step_kernel(adaptive) == "k_resident"
             s.init_state(9)
