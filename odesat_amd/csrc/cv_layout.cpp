@@ -27,6 +27,7 @@
 
 #include "../../include/odesat.h"
 #include "cnf.hpp"
+#include "solo_blocks.hpp"
 
 namespace odesat {
 
@@ -107,14 +108,14 @@ struct Rng {
 bool cv_layout(int64_t n, int64_t m, const int32_t *lits, const int32_t *vst, int nl, int cpl, int tsize, int blk_cap,
                int iters, std::vector<int32_t> &slot_clause, std::vector<int32_t> &slot_order,
                std::vector<int32_t> &blk, int64_t *cost_plain, int64_t *cost_opt) {
-    const int bs = 8 + 16 / tsize;        // SOLO_CV_BS
+    const int bs = solo_cv_bs((size_t)tsize);  // the kernel's own block stride (solo_blocks.hpp)
     const int stride = bs * tsize / 16;   // bank sets per block step (odd: every colour reachable)
     Search S;
     S.n = (int)n;
     S.m = (int)m;
     S.nslots = nl * cpl;
     S.per16 = 16 / tsize;
-    S.nb_reads = 8 / S.per16;
+    S.nb_reads = solo_dpad_reads((size_t)tsize);
     S.lits.assign(lits, lits + 3 * m);
     S.deg.resize(n);
     S.var_clauses.assign(n, {});

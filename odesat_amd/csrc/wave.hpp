@@ -21,6 +21,7 @@
 #pragma once
 
 #include "kernels.hpp"
+#include "solo_blocks.hpp"
 
 #include <type_traits>
 
@@ -650,7 +651,7 @@ __global__ __launch_bounds__(SOLO_MAX_NL) void k_solo(WArgs<T> a) {
 //     right after pass 1, the second half step after pass 2).
 // Bit-identical to k_solo, k_wave and the oracle (tests/test_gpu_parity.py, tests/test_gpu_fuzz.py).
 // ------------------------------------------------------------------------------------------------
-constexpr int SOLO_DPAD = 8;
+// (SOLO_DPAD: solo_blocks.hpp, shared with cv_layout.cpp's bank model)
 #ifndef SOLO_FOLD_EARLY
 #define SOLO_FOLD_EARLY 1
 #endif
@@ -996,7 +997,7 @@ constexpr uint32_t SOLO_CV_AREA = 32768;  // bytes per term area: the second at 
 
 // A k_solo_cv term area: blocks of SOLO_CV_BS slots (the variables' and the zero block, placed by
 // cv_layout.cpp), then a sink word per lane; the blocks that fit SOLO_CV_AREA bytes
-__host__ __device__ constexpr int solo_cv_bs(size_t tsize) { return SOLO_DPAD + 16 / (int)tsize; }
+// (solo_cv_bs: solo_blocks.hpp)
 __host__ __device__ constexpr int solo_cv_blk_cap(size_t tsize) {
     return ((int)(SOLO_CV_AREA / tsize) - SOLO_CV_MAX_NL) / solo_cv_bs(tsize);
 }
