@@ -131,7 +131,6 @@ struct Gath {  // a clause's gathered inputs: LDS byte addresses of its voltages
     uint32_t hi;
 #endif
     float v0, v1, v2;
-    float h0, h1, h2;  // gather_il only: the other half of each (y, h) pair, unused
 };
 
 // The records are read with buffer loads: the resource (SGPRs) holds the base, the per-lane offset
@@ -189,30 +188,6 @@ __device__ __forceinline__ void gather(const SlotF &S, Gath &G) {
     G.v2 = lds_f(G.a2);
 }
 
-#if ONCHIP_ADA_IL
-static_assert(ONCHIP_REC12, "the interleaved adaptive layout reads the 12-byte records");
-// The adaptive step's first pass on the interleaved layout (onchip.hpp ONCHIP_ADA_IL): each literal's
-// (y, h) pair with one ds_read_b64 at 2 x its record address.  A b32 read at the pairs' 8-byte stride
-// would bank over 16 banks; a b64 read banks over 64, so it conflicts as a b32 read of a plain array
-// does.  The pair's h (stale in pass 1) is not used, but front<true> keeps it live so that the read is
-// not narrowed to 4 bytes.
-__device__ __forceinline__ void gather_il(const SlotF &S, Gath &G) {
-    G.a0 = S.w0 & 0xffffu;
-    G.a1 = S.w1 & 0xffffu;
-    G.a2 = S.w2 & 0xffffu;
-    G.s0 = S.w0;
-    G.s1 = S.w1;
-    G.s2 = S.w2;
-    const float2 p0 = *lds_f2(2u * G.a0 + ADA_AH), p1 = *lds_f2(2u * G.a1 + ADA_AH), p2 = *lds_f2(2u * G.a2 + ADA_AH);
-    G.v0 = p0.x;
-    G.v1 = p1.x;
-    G.v2 = p2.x;
-    G.h0 = p0.y;
-    G.h1 = p1.y;
-    G.h2 = p2.y;
-}
-#endif
-
 // One clause (system.rs:43-88), in two halves that run one tile step apart (so a step interleaves
 // two independent halves of two tiles).  Exact rewritten forms (C = mn / 2 exactly):
 //   C < gamma  <=>  mn < 0.5, so cmax folds the bits of mn (mn >= +0 orders as its bits);
@@ -234,8 +209,7 @@ struct Front {  // first half: the min (:49-55) and each literal's signed select
     float sel0, sel1, sel2, mn;
 };
 
-template <bool IL = false> __device__ __forceinline__ void front(const Gath &G, Front &F) {
-    if constexpr (IL) asm volatile("" ::"v"(G.h0), "v"(G.h1), "v"(G.h2));  // (gather_il: the reads stay 8 bytes)
+__device__ __forceinline__ void front(const Gath &G, Front &F) {
     F.a0 = G.a0;
     F.a1 = G.a1;
     F.a2 = G.a2;
@@ -361,7 +335,7 @@ __device__ __forceinline__ void pair_wait(uint32_t cnt, uint32_t target, uint32_
 // t+2's first half -- independent, so they interleave -- while the writes and the gathers drain.
 // After the second tile of a pair (bar), the barrier orders the pair's dv updates against the next
 // pair's; inside a pair the same-wave order suffices (see the header).
-template <bool SPL = false, uint32_t DVO = DVC, bool UPD = true, bool IL = false>
+template <bool SPL = false, uint32_t DVO = DVC, bool UPD = true>
 __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, SlotF &slot3, float2 &mem1, Pend &P, Front &Fn,
                                           Gath &Gn, int t, float h, float hh, uint32_t &cmax, Stamps &S, bool bar,
                                           bool first = false, uint32_t cnt = 0, uint32_t *ep = nullptr) {
@@ -377,15 +351,11 @@ __device__ __forceinline__ void tile_step(const Args &a, const Recs &R, SlotF &s
     S.rmw += t_rmw - S.last;
 #endif
     Gath G3;
-#if ONCHIP_ADA_IL
-    if constexpr (IL) gather_il(slot3, G3);
-    else
-#endif
-        gather(slot3, G3);
+    gather(slot3, G3);
     slot3 = load_recf(R, t + 7);
     __builtin_amdgcn_sched_barrier(0);
     back<UPD>(a, Fn, mem1, h, hh, P, cmax);  // P <- tile t+1's terms (tile t's were written above)
-    front<IL>(Gn, Fn);                  // Fn <- tile t+2's first half
+    front(Gn, Fn);                      // Fn <- tile t+2's first half
     __builtin_amdgcn_sched_barrier(0);  // a tile's work stays between its barriers
 #ifdef ONCHIP_STAMPS
     const uint64_t t_pre = memtime();
@@ -529,23 +499,7 @@ struct FrontA {  // the min at H and each literal's signed selected value (see F
     float sel0, sel1, sel2, mn, mn1;
 };
 
-#if ONCHIP_ADA_IL
-static_assert(ONCHIP_ADA_P2_REC12, "the interleaved adaptive layout reads the 12-byte records");
-// the interleaved layout: one ds_read_b64 per literal brings its (y, h) pair
-__device__ __forceinline__ void gatherA(const SlotA &S, GathA &G) {
-    G.w0 = S.w0;
-    G.w1 = S.w1;
-    G.w2 = S.w2;
-    const uint32_t a0 = S.w0 & 0xffffu, a1 = S.w1 & 0xffffu, a2 = S.w2 & 0xffffu;
-    const float2 p0 = *lds_f2(2u * a0 + ADA_AH), p1 = *lds_f2(2u * a1 + ADA_AH), p2 = *lds_f2(2u * a2 + ADA_AH);
-    G.y0 = p0.x;
-    G.y1 = p1.x;
-    G.y2 = p2.x;
-    G.v0 = p0.y;
-    G.v1 = p1.y;
-    G.v2 = p2.y;
-}
-#elif ONCHIP_ADA_P2_REC12 && ONCHIP_REC12
+#if ONCHIP_ADA_P2_REC12 && ONCHIP_REC12
 __device__ __forceinline__ void gatherA(const SlotA &S, GathA &G) {
     G.w0 = S.w0;
     G.w1 = S.w1;
@@ -730,12 +684,11 @@ __device__ __forceinline__ void reg_tile1(const Args &a, const Recs &R, float2 (
     constexpr bool first = T > 0 && ((T - 1 + OFF) & 1) != 0;
     constexpr bool SPL = (ONCHIP_SPLITBAR & 2) != 0 && ONCHIP_ADA_P1_SPL;
     if constexpr (T + 1 < TR) {
-        tile_step<SPL, ADA_D, false, ONCHIP_ADA_IL>(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, 0.0f, 0.0f, cmax, S,
-                                                    bar, first, cnt, ep);
+        tile_step<SPL, ADA_D, false>(a, R, ring[(T + 3) % 4], mr[T + 1], P, Fn, Gn, T, 0.0f, 0.0f, cmax, S, bar, first,
+                                     cnt, ep);
     } else {  // the (empty) tile after the last: its terms are never applied
         float2 m = make_float2(0.001f, 1.0f);
-        tile_step<SPL, ADA_D, false, ONCHIP_ADA_IL>(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, 0.0f, 0.0f, cmax, S, bar,
-                                                    first, cnt, ep);
+        tile_step<SPL, ADA_D, false>(a, R, ring[(T + 3) % 4], m, P, Fn, Gn, T, 0.0f, 0.0f, cmax, S, bar, first, cnt, ep);
     }
 }
 
@@ -767,24 +720,15 @@ __device__ __forceinline__ void pass1(const Args &a, float2 (&mr)[TR], int lane,
     for (int s = 0; s < 4; ++s) ring[s] = load_recf(R, s);
     Pend P;
     Gath G0, G1, Gn;
-#if ONCHIP_ADA_IL
-    gather_il(ring[0], G0);
-    ring[0] = load_recf(R, 4);
-    gather_il(ring[1], G1);
-    ring[1] = load_recf(R, 5);
-    gather_il(ring[2], Gn);
-    ring[2] = load_recf(R, 6);
-#else
     gather(ring[0], G0);
     ring[0] = load_recf(R, 4);
     gather(ring[1], G1);
     ring[1] = load_recf(R, 5);
     gather(ring[2], Gn);
     ring[2] = load_recf(R, 6);
-#endif
     Front F0, Fn;
-    front<ONCHIP_ADA_IL>(G0, F0);
-    front<ONCHIP_ADA_IL>(G1, Fn);
+    front(G0, F0);
+    front(G1, Fn);
     back<false>(a, F0, mr[0], 0.0f, 0.0f, P, cmax);
     reg_tiles1<TR, OFF>(std::make_integer_sequence<int, TR>{}, a, R, mr, ring, P, Fn, Gn, cmax, S, cnt, &ep);
     if (!(__uint_as_float(cmax) < 0.5f)) lds_st(flag, 1.0f);
@@ -915,9 +859,6 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     mem_load<TR>(std::make_integer_sequence<int, TR>{}, tcw, mem_rsrc((p ? a.c1 : a.c0) + (size_t)g * a.m * 2, a.m),
                  8u * (uint32_t)wl, mr);
     {   // v (sinks = 1.0) into LDS, dv = 0 (:33): the loads of a pass issued together, then the stores
-        // (the interleaved adaptive layout: v into the pairs' y halves, 1.0 into their h halves -- the
-        // sinks' h is gathered by pass 2, the others' is written before it)
-        [[maybe_unused]] constexpr bool IL = ADA && ONCHIP_ADA_IL != 0;
         if ((a.n & 3) == 0) {  // 16 bytes per access (V, v, dv and H are 16-byte aligned; n + SINKS % 4 == 0)
             constexpr int U = 4;
             const int n4 = n2 >> 2, nv4 = a.n >> 2;
@@ -930,18 +871,9 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                     const int q = q0 + u * NTH;
                     if (q < n4) {
                         const f4v one4 = {1.0f, 1.0f, 1.0f, 1.0f};
-                        lds_st4(16u * q + DV, f4v{0.0f, 0.0f, 0.0f, 0.0f});
-#if ONCHIP_ADA_IL
-                        if constexpr (IL) {
-                            const f4v xv = q < nv4 ? x[u] : one4;
-                            lds_st4(ADA_AH + 32u * q, f4v{xv.x, 1.0f, xv.y, 1.0f});
-                            lds_st4(ADA_AH + 32u * q + 16u, f4v{xv.z, 1.0f, xv.w, 1.0f});
-                            continue;
-                        }
-#else
-                        if (ADA && q >= nv4) lds_st4(16u * q + ADA_H, one4);  // H's sinks (pass 2 gathers them)
-#endif
                         lds_st4(16u * q, q < nv4 ? x[u] : one4);
+                        lds_st4(16u * q + DV, f4v{0.0f, 0.0f, 0.0f, 0.0f});
+                        if (ADA && q >= nv4) lds_st4(16u * q + ADA_H, one4);  // H's sinks (pass 2 gathers them)
                     }
                 }
             }
@@ -955,16 +887,9 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                 for (int u = 0; u < U; ++u) {
                     const int i = i0 + u * NTH;
                     if (i < n2) {
-                        lds_st(4u * i + DV, 0.0f);
-#if ONCHIP_ADA_IL
-                        if constexpr (IL) {
-                            *lds_f2(ADA_AH + 8u * i) = make_float2(i < a.n ? x[u] : 1.0f, 1.0f);
-                            continue;
-                        }
-#else
-                        if (ADA && i >= a.n) lds_st(4u * i + ADA_H, 1.0f);  // H's sinks (pass 2 gathers them)
-#endif
                         lds_st(4u * i, i < a.n ? x[u] : 1.0f);
+                        lds_st(4u * i + DV, 0.0f);
+                        if (ADA && i >= a.n) lds_st(4u * i + ADA_H, 1.0f);  // H's sinks (pass 2 gathers them)
                     }
                 }
             }
@@ -1008,31 +933,6 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
             } else {
                 // full-step clone and first half step (:124-128), four variables per LDS access (A, D,
                 // H and F are 16-byte aligned), then the n % 4 last ones
-#if ONCHIP_ADA_IL
-                for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {  // (y, h) pairs: the h halves of 4 variables
-                    const uint32_t o = 16u * (uint32_t)i4, oa = ADA_AH + 32u * (uint32_t)i4;
-                    const f4v d2 = lds_f4(o + ADA_D), p01 = lds_f4(oa), p23 = lds_f4(oa + 16u);
-                    lds_st4(o + ADA_D, f4v{0.0f, 0.0f, 0.0f, 0.0f});
-                    const float y[4] = {p01.x, p01.z, p23.x, p23.z};
-                    f4v vf;
-                    float vh[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        vf[u] = __builtin_amdgcn_fmed3f(y[u] + hhk * d2[u], -1.0f, 1.0f);
-                        vh[u] = __builtin_amdgcn_fmed3f(y[u] + hqk * d2[u], -1.0f, 1.0f);
-                    }
-                    lds_st4(o + ADA_F, vf);
-                    lds_st4(oa, f4v{y[0], vh[0], y[1], vh[1]});
-                    lds_st4(oa + 16u, f4v{y[2], vh[2], y[3], vh[3]});
-                }
-                for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) {
-                    const float d2 = lds_f(4u * i + ADA_D);
-                    const float y = lds_f2(ADA_AH + 8u * i)->x;
-                    lds_st(4u * i + ADA_D, 0.0f);
-                    lds_st(4u * i + ADA_F, __builtin_amdgcn_fmed3f(y + hhk * d2, -1.0f, 1.0f));
-                    *lds_f2(ADA_AH + 8u * i) = make_float2(y, __builtin_amdgcn_fmed3f(y + hqk * d2, -1.0f, 1.0f));
-                }
-#else
                 for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
                     const uint32_t o = 16u * (uint32_t)i4;
                     const f4v d2 = lds_f4(o + ADA_D), y = lds_f4(o);
@@ -1052,7 +952,6 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                     lds_st(4u * i + ADA_F, __builtin_amdgcn_fmed3f(y + hhk * d2, -1.0f, 1.0f));
                     lds_st(4u * i + ADA_H, __builtin_amdgcn_fmed3f(y + hqk * d2, -1.0f, 1.0f));
                 }
-#endif
                 __syncthreads();
                 ADA_STAMP(ada_st[1]);
 #if ONCHIP_ADA_SKIP != 1  // (diagnostic build 1: no pass 2)
@@ -1061,30 +960,6 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                 ADA_STAMP(ada_st[2]);
                 // second half step (:130), max_error (:101-108); the same lane ownership as the final
                 // store below
-#if ONCHIP_ADA_IL
-                for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {  // (y, h) pairs: the y halves of 4 variables
-                    const uint32_t o = 16u * (uint32_t)i4, oa = ADA_AH + 32u * (uint32_t)i4;
-                    const f4v d2 = lds_f4(o + ADA_D), p01 = lds_f4(oa), p23 = lds_f4(oa + 16u), vf = lds_f4(o + ADA_F);
-                    lds_st4(o + ADA_D, f4v{0.0f, 0.0f, 0.0f, 0.0f});
-                    const float vh[4] = {p01.y, p01.w, p23.y, p23.w};
-                    float vn[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        vn[u] = __builtin_amdgcn_fmed3f(vh[u] + hqk * d2[u], -1.0f, 1.0f);
-                        e = fmaxf(e, fabsf(vf[u] - vn[u]));
-                    }
-                    lds_st4(oa, f4v{vn[0], vh[0], vn[1], vh[1]});
-                    lds_st4(oa + 16u, f4v{vn[2], vh[2], vn[3], vh[3]});
-                }
-                for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) {
-                    const float d2 = lds_f(4u * i + ADA_D);
-                    lds_st(4u * i + ADA_D, 0.0f);
-                    const float2 yh = *lds_f2(ADA_AH + 8u * i);
-                    const float vn = __builtin_amdgcn_fmed3f(yh.y + hqk * d2, -1.0f, 1.0f);
-                    e = fmaxf(e, fabsf(lds_f(4u * i + ADA_F) - vn));
-                    *lds_f2(ADA_AH + 8u * i) = make_float2(vn, yh.y);
-                }
-#else
                 for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
                     const uint32_t o = 16u * (uint32_t)i4;
                     const f4v d2 = lds_f4(o + ADA_D), vh = lds_f4(o + ADA_H), vf = lds_f4(o + ADA_F);
@@ -1104,7 +979,6 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
                     e = fmaxf(e, fabsf(lds_f(4u * i + ADA_F) - vn));
                     lds_st(4u * i, vn);
                 }
-#endif
                 uint32_t eb = __float_as_uint(e);  // non-negative: the bits order as the values
 #pragma unroll
                 for (int off = 32; off >= 1; off >>= 1) eb = max(eb, (uint32_t)__shfl_xor((int)eb, off, 64));
@@ -1178,28 +1052,14 @@ __global__ __launch_bounds__(NTH) void k_onchip(Args a) {
     ONCHIP_PHASE(2);
     float *Vo = (q ? a.v1 : a.v0) + (size_t)g * a.n;
     // written by this lane in the last update (four variables per lane, then the tail)
-#if ONCHIP_ADA_IL
-    if constexpr (ADA) {  // the y halves of the (y, h) pairs
-        for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
-            const f4v p01 = lds_f4(ADA_AH + 32u * (uint32_t)i4), p23 = lds_f4(ADA_AH + 32u * (uint32_t)i4 + 16u);
-            st_state(&Vo[4 * i4], p01.x);
-            st_state(&Vo[4 * i4 + 1], p01.z);
-            st_state(&Vo[4 * i4 + 2], p23.x);
-            st_state(&Vo[4 * i4 + 3], p23.z);
-        }
-        for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) st_state(&Vo[i], lds_f2(ADA_AH + 8u * i)->x);
-    } else
-#endif
-    {
-        for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
-            const f4v v = lds_f4(16u * (uint32_t)i4);
-            st_state(&Vo[4 * i4], v.x);
-            st_state(&Vo[4 * i4 + 1], v.y);
-            st_state(&Vo[4 * i4 + 2], v.z);
-            st_state(&Vo[4 * i4 + 3], v.w);
-        }
-        for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) st_state(&Vo[i], lds_f(4u * i));
+    for (int i4 = lane; i4 < (a.n >> 2); i4 += NTH) {
+        const f4v v = lds_f4(16u * (uint32_t)i4);
+        st_state(&Vo[4 * i4], v.x);
+        st_state(&Vo[4 * i4 + 1], v.y);
+        st_state(&Vo[4 * i4 + 2], v.z);
+        st_state(&Vo[4 * i4 + 3], v.w);
     }
+    for (int i = (a.n & ~3) + lane; i < a.n; i += NTH) st_state(&Vo[i], lds_f(4u * i));
     {   // opaque copies: the store addresses are recomputed here instead of being kept live (two
         // VGPRs per tile) across the step loop from the loads above
         float2 *CMs = reinterpret_cast<float2 *>((q ? a.c1 : a.c0) + (size_t)g * a.m * 2);

@@ -52,25 +52,12 @@ inline int tl_max(int64_t n) {
 }
 
 // Adaptive steps (system.rs:111-139) keep four voltage arrays in LDS and every tile's memories in
-// VGPRs (no LDS tiles): A = the step's starting voltages y (and then its result), D = 2 dv, H = the
-// half step, F = the full-step clone, n + SINKS floats each.
-// ONCHIP_ADA_IL (round 6, the default): A and H interleaved as (y, h) pairs (AH, 8-byte stride), so the
-// second pass gathers both of a literal's voltages with one ds_read_b64 instead of two ds_read_b32;
-// D at 0, whose addresses are the records' own (4 var), AH at 40960 (2 x the record address + the
-// ds instructions' 16-bit immediate), F at 122880.  D's region also holds the unsat flags and the
-// waves' error words.  ONCHIP_ADA_IL=0 (A/B): A at 0 (the flags after it), D at 40960 (within the
-// immediate of A's addresses), H at 81920, F at 122880.
-#ifndef ONCHIP_ADA_IL
-#define ONCHIP_ADA_IL 0
-#endif
-constexpr uint32_t ADA_REGION = 40960;  // bytes of one array of n + SINKS floats and the flags
-#if ONCHIP_ADA_IL
-constexpr uint32_t ADA_D = 0, ADA_AH = 40960, ADA_F = 122880;
-#else
+// VGPRs (no LDS tiles): A = the step's starting voltages y (and then its result), D = 2 dv (within
+// the ds instructions' 16-bit immediate of A, as DVC), H = the half step, F = the full-step clone,
+// n + SINKS floats each; A's region also holds the unsat flags and the waves' error words.
 constexpr uint32_t ADA_D = 40960, ADA_H = 81920, ADA_F = 122880;
-#endif
 constexpr int ADA_FLAGS = 2 + 3 * WAVES;  // two unsat flags, the waves' error words, their pair counts, the fault slots
-constexpr int ADA_MAX_N = (int)(ADA_REGION / 4) - SINKS - ADA_FLAGS;
+constexpr int ADA_MAX_N = (int)(ADA_D / 4) - SINKS - ADA_FLAGS;
 
 struct Args {
     const uint64_t *rec; // [tiles][NTH] slot-major clause records (make_rec), padded with empty tiles
