@@ -138,6 +138,15 @@ template <typename T> __device__ __forceinline__ Vec<T, 2> res_ldm(const T *p) {
         return ldv<T, 2>(p);
     }
 }
+// one word of the adaptive C scratch, with the memories' policy
+template <typename T> __device__ __forceinline__ T res_ld1(const T *p) {
+    if constexpr (RES_NT != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <typename T> __device__ __forceinline__ void res_st1(T *p, T x) {
+    if constexpr (RES_NT != 0) __builtin_nontemporal_store(x, p);
+    else *p = x;
+}
 template <typename T> __device__ __forceinline__ void res_stm(T *p, const Vec<T, 2> &v) {
     if constexpr (RES_NT != 0) {
         typedef T t2 __attribute__((ext_vector_type(2)));
@@ -161,7 +170,7 @@ __device__ __forceinline__ void res_load3(const RArgs<T> &a, const ResCtx<T, R> 
     ld.lit = *at(a.cl4, (uint32_t)cc);
     const uint32_t ci = (uint32_t)(cc * R + x.r) * 2u;  // 32-bit offsets from the group's base
     if (mem) ld.mem = res_ldm<T>(at(CM, ci));  // (adaptive: y's memories, untouched until the second pass stores)
-    if (PK == P_ADA2 && mem) ld.full.e[0] = *at((const T *)x.cf, ci / 2u);  // the first pass's C
+    if (PK == P_ADA2 && mem) ld.full.e[0] = res_ld1<T>(at((const T *)x.cf, ci / 2u));  // the first pass's C
 }
 
 // The adaptive step's candidates for one clause's memories from y's memories and the first pass's
@@ -267,12 +276,12 @@ __device__ __forceinline__ void res_clause3(const RArgs<T> &a, const ResCtx<T, R
             solo_mem<T>(xs, xl, mn, hh, h, a.xl_max, o.e[0], o.e[1]);
             res_stm<T>(at(CM, ci), o);
         } else if (PK == P_ADA1) {
-            *at(x.cf, ci / 2u) = mn;
+            res_st1<T>(at(x.cf, ci / 2u), mn);
         } else {
             Vec<T, 2> o;
             solo_mem<T>(xs, xl, mn, hq, hh, a.xl_max, o.e[0], o.e[1]);  // second half step (:130)
             e = dmax(e, dmax(dabs(xs_f - o.e[0]), dabs(xl_f - o.e[1])));  // :132
-            stv<T, 2>(at(CM, ci), o);
+            res_stm<T>(at(CM, ci), o);
         }
         return;
     }
