@@ -70,6 +70,9 @@ def test_help():
     (("stoch", "-f", "x.cnf", "-s", "0.1"), "stoch takes only"),
     (("solve", "-f"), "value is required"),
     (("inter", "-f", "x.cnf", "-b", "0"), "batch-size"),
+    (("solve", "-f", "x.cnf", "--run-chunk", "0"), "--run-chunk"),   # hidden test hooks
+    (("solve", "-f", "x.cnf", "--run-chunk", "x"), "invalid value"),
+    (("solve", "--share-devices"), "--input"),  # a flag without a value: parsing goes on to the required ones
 ])
 def test_usage_errors(argv, needle):
     r = run(*argv)
