@@ -783,7 +783,7 @@ def config4_leg(args, world, rank, local, dist, solver_cls=None, config="config4
         "digest": digest}
 
 
-def c5_capture(ps, warmup, probe, gsteps, dt, zeta, dev_sync, dist, world, gpu):
+def c5_capture(ps, warmup, probe, gsteps, dt, zeta, dev_sync, dist, world):
     """The timed steps of one config-5 partition as a HIP graph, or None (eager steps) with the error
     text when capturing or replaying fails (RCCL collectives inside a graph have only
     run at world 1).  probe = 1: the last warmup step is a captured one-step graph, replayed, so a
@@ -795,11 +795,8 @@ def c5_capture(ps, warmup, probe, gsteps, dt, zeta, dev_sync, dist, world, gpu):
     def agree():  # every rank replays only if every rank can
         nonlocal g, err
         if dist is not None and world > 1:
-            import torch
-            import torch.distributed as tdist
-            flag = torch.tensor([0.0 if g is not None else 1.0], device="cuda" if gpu else "cpu")
-            dist.all_reduce(flag, op=tdist.ReduceOp.MAX)
-            if float(flag.item()) > 0 and g is not None:
+            from odesat_amd.sharding import max_over_ranks
+            if max_over_ranks(dist, 0.0 if g is not None else 1.0) > 0 and g is not None:
                 g, err = None, "another rank's HIP-graph capture or replay failed"
 
     if ps.capturable():
@@ -884,7 +881,7 @@ def config5_leg(args, world, rank, local, dist, part_cls=None, config="config5")
         gsteps = args.config5_graph or args.steps
         if ps.capturable() and args.steps % gsteps:
             raise SystemExit("bench.py: --steps must be a multiple of --config5-graph")
-        g, gerr = c5_capture(ps, args.warmup, probe, gsteps, dt, zeta, dev_sync, dist, world, gpu)
+        g, gerr = c5_capture(ps, args.warmup, probe, gsteps, dt, zeta, dev_sync, dist, world)
         if gpu:  # HIP events on the stream the partition's kernels and collectives run on
             stream = torch.cuda.current_stream()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
