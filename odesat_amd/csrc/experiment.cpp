@@ -26,6 +26,7 @@ const char *const KNOBS[] = {
     "WAVE",             // 1: k_wave where its LDS fits; 0: the tile kernels
     "WAVE_TEAM",        // k_wave waves per replica: 1, 2, 4, 8 or 16
     "WAVE_FAST",        // 0: k_wave's general arithmetic on in-range states
+    "WAVE_TAIL",        // 0: a partial last round of k_wave workgroups stays in the main launch
     "SOLO",             // 1 / 0: k_solo instead of / never instead of k_wave
     "SOLO_LANES",       // k_solo lanes per replica (a multiple of 64)
     "SOLO_FAST",        // 0: k_solo's general arithmetic on in-range states

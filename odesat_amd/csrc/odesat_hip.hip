@@ -84,6 +84,8 @@ struct odesat_solver {
     bool res_rc = true;         // f64 fixed steps: register-cached tiles (resident.hpp; knob RES_RC = 0)
     int wv_tw = 1;              // k_wave: waves per replica, fixed steps
     int wv_tw_ada = 1;          // ... adaptive steps (four barriers per step instead of two: at most 4)
+    int cus = 256;              // the device's CUs (k_wave's device rounds)
+    bool wave_tail = true;      // k_wave: a partial last round runs as its own launch, fewer replicas per workgroup
     bool res_ada = false; // adaptive steps run k_resident (else FUSED on the same layout)
     bool res_vfg = false; // ... with the full-step voltage clone in HBM (v and dv fill the LDS)
     int res_ntiles = 0;
@@ -781,11 +783,12 @@ int launch_resident_k(odesat_solver *s, const RArgs<T> &a) {
     return ODESAT_OK;
 }
 
-template <typename T, bool ADA, int WPW, int TW, bool FAST> int launch_wave_k(odesat_solver *s, WArgs<T> a) {
+// replicas [a.g0, g1) of the solver's G
+template <typename T, bool ADA, int WPW, int TW, bool FAST> int launch_wave_k(odesat_solver *s, WArgs<T> a, int64_t g1) {
     a.topo_bytes = (uint32_t)wave_topo_bytes(s->n, s->m);
     a.rep_bytes = (uint32_t)wave_lds_bytes(s->n, s->m, s->L, sizeof(T), ADA);
     const size_t lds = a.topo_bytes + (size_t)WPW * a.rep_bytes;
-    const unsigned grid = (unsigned)((s->G + WPW - 1) / WPW), block = WAVE_NTH * WPW * TW;
+    const unsigned grid = (unsigned)((g1 - a.g0 + WPW - 1) / WPW), block = WAVE_NTH * WPW * TW;
     HIP_TRY((wave_launch<T, ADA, WPW, TW, FAST>(true, a, grid, block, lds, (int)RES_LDS_MAX, s->stream)));
     hipError_t e;
     {
@@ -879,28 +882,52 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
             default: return fail(ODESAT_EINVAL, "k_solo shape not available");
         }
     }
+    int64_t g1 = s->G;
     auto go = [&](auto ww, auto tw) -> int {
         constexpr int WPW = decltype(ww)::value, TW = decltype(tw)::value;
         if (fast && s->wave_fast)  // in-range states: the short arithmetic (wave.hpp lane_clauses)
-            return adaptive ? launch_wave_k<T, true, WPW, TW, true>(s, a) : launch_wave_k<T, false, WPW, TW, true>(s, a);
-        return adaptive ? launch_wave_k<T, true, WPW, TW, false>(s, a) : launch_wave_k<T, false, WPW, TW, false>(s, a);
+            return adaptive ? launch_wave_k<T, true, WPW, TW, true>(s, a, g1) : launch_wave_k<T, false, WPW, TW, true>(s, a, g1);
+        return adaptive ? launch_wave_k<T, true, WPW, TW, false>(s, a, g1) : launch_wave_k<T, false, WPW, TW, false>(s, a, g1);
     };
     // (replicas per workgroup, waves per replica): at most 16 waves per workgroup
-    switch (s->wv_wpw * 100 + (adaptive ? s->wv_tw_ada : s->wv_tw)) {
-        case 401: return go(IC<4>{}, IC<1>{});
-        case 402: return go(IC<4>{}, IC<2>{});
-        case 404: return go(IC<4>{}, IC<4>{});
-        case 201: return go(IC<2>{}, IC<1>{});
-        case 202: return go(IC<2>{}, IC<2>{});
-        case 204: return go(IC<2>{}, IC<4>{});
-        case 208: return go(IC<2>{}, IC<8>{});
-        case 101: return go(IC<1>{}, IC<1>{});
-        case 102: return go(IC<1>{}, IC<2>{});
-        case 104: return go(IC<1>{}, IC<4>{});
-        case 108: return go(IC<1>{}, IC<8>{});
-        case 116: return go(IC<1>{}, IC<16>{});
-        default: return fail(ODESAT_EINVAL, "k_wave shape not available");
-    }
+    auto shape = [&](int wpw, int tw) -> int {
+        switch (wpw * 100 + tw) {
+            case 401: return go(IC<4>{}, IC<1>{});
+            case 402: return go(IC<4>{}, IC<2>{});
+            case 404: return go(IC<4>{}, IC<4>{});
+            case 201: return go(IC<2>{}, IC<1>{});
+            case 202: return go(IC<2>{}, IC<2>{});
+            case 204: return go(IC<2>{}, IC<4>{});
+            case 208: return go(IC<2>{}, IC<8>{});
+            case 101: return go(IC<1>{}, IC<1>{});
+            case 102: return go(IC<1>{}, IC<2>{});
+            case 104: return go(IC<1>{}, IC<4>{});
+            case 108: return go(IC<1>{}, IC<8>{});
+            case 116: return go(IC<1>{}, IC<16>{});
+            default: return fail(ODESAT_EINVAL, "k_wave shape not available");
+        }
+    };
+    const int wpw = s->wv_wpw, tw = adaptive ? s->wv_tw_ada : s->wv_tw;
+    // One workgroup of wpw replicas per CU: the device works in rounds of wpw * cus replicas.  A partial
+    // last round at the solver's shape costs a whole one (config 3, B = 1280: 320 workgroups of 4, the
+    // last 64 alone in a second round -- DESIGN.md §6.3), so it runs as a launch of its own after the
+    // whole rounds, at fewer replicas per workgroup (the solver's rule: halve while a CU would idle) and
+    // the wider teams that leaves room for.  Replicas are independent; a STOP_ANY stop is read by the
+    // later launch as by a later round of one launch, and the call's replay logic is unchanged.
+    const int64_t round = (int64_t)wpw * s->cus, g_main = s->G / round * round;
+    if (!s->wave_tail || wpw == 1 || g_main == 0 || g_main == s->G) return shape(wpw, tw);
+    g1 = g_main;
+    int rc = shape(wpw, tw);
+    if (rc) return rc;
+    const int64_t rem = s->G - g_main;
+    int wpw_t = wpw;
+    while (wpw_t > 1 && (rem + wpw_t - 1) / wpw_t < s->cus) wpw_t /= 2;
+    int tw_t = 16 / wpw_t;
+    while (tw_t > 1 && 32 * (int64_t)tw_t > s->m) tw_t /= 2;
+    if (adaptive) tw_t = std::min(tw_t, 4);
+    a.g0 = (int32_t)g_main;
+    g1 = s->G;
+    return shape(wpw_t, tw_t);
 }
 
 #ifndef RES_RC
@@ -1311,7 +1338,9 @@ extern "C" int odesat_solver_create(int device, const odesat_cnf *f, int64_t bat
             int cus = 256;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0)
                 cus = 256;
+            s->cus = cus;
             while (s->wv_wpw > 1 && (batch + s->wv_wpw - 1) / s->wv_wpw < cus) s->wv_wpw /= 2;
+            s->wave_tail = odesat::xp_get("WAVE_TAIL", 1) != 0;
         }
         s->res_wave = ev >= 0 ? (ev != 0 && topo + rep <= RES_LDS_MAX) : topo + 2 * rep <= RES_LDS_MAX;
         // waves per replica: LDS holds one workgroup (wv_wpw replicas) per CU, so a replica of one

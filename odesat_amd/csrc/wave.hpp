@@ -40,6 +40,7 @@ template <typename T> struct WArgs {
     int64_t *sat_step, *steps_done;
     int32_t *stop;
     int32_t n, m, L, G;                 // G: replicas (groups of width 1)
+    int32_t g0;                         // k_wave: this launch's first replica (a partial round's tail launch)
     uint32_t topo_bytes, rep_bytes;     // LDS: the shared topology, then WPW replicas of rep_bytes
     int32_t step0, nsteps, stop_mode;
     int32_t oop;  // 1: the final state goes to the other buffer and par flips (STOP_ANY replay)
@@ -279,7 +280,7 @@ __global__ __launch_bounds__(WAVE_NTH * WPW * TW) void k_wave(WArgs<T> a) {
     __shared__ U errL[WPW];
     __shared__ int unsL[WPW * TW];  // TW > 1: each wave's "some clause unsat"
     const int w = threadIdx.x / NL, l = threadIdx.x % NL;
-    const int g = blockIdx.x * WPW + w;  // this team's replica (group width 1)
+    const int g = a.g0 + (int)blockIdx.x * WPW + w;  // this team's replica (group width 1)
     int4 *rec4 = reinterpret_cast<int4 *>(wave_smem);
     int32_t *vst = reinterpret_cast<int32_t *>(rec4 + a.m);
     copy_to_lds<8>(rec4, a.rec4, (int)threadIdx.x, a.m, NL * WPW);

@@ -26,8 +26,13 @@ def main():
     p.add_argument("--steady", type=int, default=6)
     p.add_argument("--batches", default=",".join(map(str, BATCHES)))
     p.add_argument("--families", default="", help="comma-separated config:dtype:mode, default all")
+    p.add_argument("--knob", action="append", default=[], metavar="KEY=VALUE", help="experiment knob (A/B)")
     a = p.parse_args()
     import bench
+    from odesat_amd import _lib
+    for kv in a.knob:
+        k, v = kv.split("=", 1)
+        _lib.set_experiment(k.strip(), int(v))
     from odesat_amd.system import ODESAT_STOP_NONE, Solver
     fams = FAMILIES
     if a.families:
@@ -50,6 +55,7 @@ def main():
                            "value": B * ran / wall, "ms_per_step": wall * 1e3 / ran,
                            "kernel_us_per_step": ms[0] * 1e3 / ran,
                            "steady_value": st["value"], "steady_kernel_us_per_step": st["kernel_us_per_call"] / ran,
+                           "knobs": a.knob,
                            "date": time.strftime("%Y-%m-%d %H:%M:%S")}
                 fh.write(json.dumps(rec) + "\n")
                 fh.flush()

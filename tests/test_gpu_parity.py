@@ -942,3 +942,64 @@ def test_wave_teams_equal_fused(xp, stop, adaptive):
         assert np.array_equal(out[0][0]["steps_done"], r["steps_done"]) and same(out[0][0]["dt"], r["dt"])
         for x, y in zip(out[0][1], st):
             assert same(x, y)
+
+
+@pytest.mark.parametrize("stop", [ODESAT_STOP_EACH, ODESAT_STOP_ANY, ODESAT_STOP_NONE])
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_wave_partial_round_tail_launch(xp, stop, adaptive):
+    """k_wave's partial last round as a launch of its own (round 6, knob WAVE_TAIL): B = 1100 on easy.cnf
+    is one device round of 256 workgroups x 4 replicas plus 76 replicas, which now run after it at one
+    replica per workgroup.  Replicas satisfy and freeze at their own steps inside 300-step launches, and
+    STOP_ANY's stop word set in the first launch is read by the second: every state, sat step, step
+    count and dt equals the single launch's (WAVE_TAIL = 0) and FUSED's."""
+    from odesat_amd import _lib
+    f = product_formula("easy")
+    out = []
+    for alg, tail in ((_lib.ODESAT_ALG_RESIDENT, None), (_lib.ODESAT_ALG_RESIDENT, "0"), (_lib.ODESAT_ALG_FUSED, None)):
+        xp.set("WAVE", "1")
+        xp.set("SOLO", "0")
+        xp.set("WAVE_TAIL", tail)
+        with Solver(f, 1100, "f32") as s:
+            s.set_algorithm(alg)
+            if alg == _lib.ODESAT_ALG_RESIDENT:
+                assert s.step_kernel(adaptive) == "k_wave"
+            s.init_state(6)
+            r = s.simulate(adaptive=adaptive, dt=0.1, tol=1e-3, max_steps=1500, stop=stop, poll_interval=300)
+            out.append((r, s.get_state()))
+    assert (out[0][0]["first_sat_step"] >= 0).any()
+    for r, st in out[1:]:
+        assert np.array_equal(out[0][0]["first_sat_step"], r["first_sat_step"])
+        assert np.array_equal(out[0][0]["steps_done"], r["steps_done"]) and same(out[0][0]["dt"], r["dt"])
+        for x, y in zip(out[0][1], st):
+            assert same(x, y)
+
+
+def test_wave_partial_round_config3_vs_oracle(xp):
+    """Config 3 (n = 250, m = 1065) at B = 1280: 1024 replicas in the main launch and 256 in the tail's
+    (one replica per workgroup, 16-wave teams for fixed steps, 4 for adaptive).  20 adaptive steps equal
+    the single launch's bit for bit, and replicas 0, 1023 (main) and 1024, 1279 (tail) equal the
+    oracle's f32 simulate."""
+    c = wl.CONFIGS["config3"]
+    var, neg = wl.random_ksat(c["n"], c["m"], 3, c["seed"])
+    cp, v_, n_ = wl.formula_arrays(var, neg)
+    f = cnf.CNFFormula.from_arrays(cp, v_, n_, c["n"])
+    B, K = 1280, 20
+    out = []
+    for tail in (None, "0"):
+        xp.set("WAVE_TAIL", tail)
+        with Solver(f, B, "f32") as s:
+            assert s.step_kernel(True) == "k_wave"
+            s.init_state(42)
+            r = s.simulate(adaptive=True, dt=0.01, tol=1e-3, max_steps=K, stop=ODESAT_STOP_NONE)
+            out.append((r, s.get_state()))
+    (r1, s1), (r2, s2) = out
+    assert np.all(r1["steps_done"] == K) and same(r1["dt"], r2["dt"])
+    for x, y in zip(s1, s2):
+        assert same(x, y)
+    o = Oracle(cp, v_, n_, c["n"], "f32")
+    for b in (0, 1023, 1024, 1279):
+        ov = init_voltages(42, b, 1, c["n"])[0].astype(np.float32)
+        oxs, oxl = o.init_short_term_memory(), np.ones(c["m"], np.float32)
+        t, _, _, h, _ = o.simulate(ov, oxs, oxl, tol=np.float32(1e-3), dt=None, steps=K)
+        assert t == K and same(np.float32(h), np.float32(r1["dt"][b]))
+        assert same(s1[0][b], ov) and same(s1[1][b], oxs) and same(s1[2][b], oxl), f"replica {b}"
