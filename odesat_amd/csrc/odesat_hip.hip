@@ -911,17 +911,18 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     // One workgroup of wpw replicas per CU: the device works in rounds of wpw * cus replicas.  A partial
     // last round at the solver's shape costs a whole one (config 3, B = 1280: 320 workgroups of 4, the
     // last 64 alone in a second round -- DESIGN.md §6.3), so it runs as a launch of its own after the
-    // whole rounds, at fewer replicas per workgroup (the solver's rule: halve while a CU would idle) and
-    // the wider teams that leaves room for.  Replicas are independent; a STOP_ANY stop is read by the
+    // whole rounds, at fewer replicas per workgroup and the wider teams that leaves room for.  Replicas are independent; a STOP_ANY stop is read by the
     // later launch as by a later round of one launch, and the call's replay logic is unchanged.
-    const int64_t round = (int64_t)wpw * s->cus, g_main = s->G / round * round;
-    if (!s->wave_tail || wpw == 1 || g_main == 0 || g_main == s->G) return shape(wpw, tw);
+    // The tail takes the fewest replicas per workgroup that still fit it in one round: when that is
+    // wpw itself (more than (wpw / 2) cus replicas left), one launch does as well (measured: config 3,
+    // B = 1792, a tail at 2 per workgroup in two rounds was 14 % slower).
+    const int64_t round = (int64_t)wpw * s->cus, g_main = s->G / round * round, rem = s->G - g_main;
+    int wpw_t = 1;
+    while (wpw_t < wpw && (rem + wpw_t - 1) / wpw_t > s->cus) wpw_t *= 2;
+    if (!s->wave_tail || wpw_t == wpw || g_main == 0 || rem == 0) return shape(wpw, tw);
     g1 = g_main;
     int rc = shape(wpw, tw);
     if (rc) return rc;
-    const int64_t rem = s->G - g_main;
-    int wpw_t = wpw;
-    while (wpw_t > 1 && (rem + wpw_t - 1) / wpw_t < s->cus) wpw_t /= 2;
     int tw_t = 16 / wpw_t;
     while (tw_t > 1 && 32 * (int64_t)tw_t > s->m) tw_t /= 2;
     if (adaptive) tw_t = std::min(tw_t, 4);

@@ -11,6 +11,6 @@ tail -2 "$OUT/wave_tests.log"
 for r in 1 2; do
     for k in "" "--knob WAVE_TAIL=0"; do
         timeout -k 10 300 python -u scripts/batch_scaling.py --out "$OUT/tail_scaling.jsonl" --families config3:f32:adaptive,config3:f32:fixed \
-            --batches 1024,1100,1280,1536,1792,2048 $k || exit 1
+            --batches ${BATCHES:-1024,1100,1280,1536,1792,2048} $k || exit 1
     done
 done
