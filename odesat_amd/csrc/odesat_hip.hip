@@ -915,11 +915,13 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     // later launch as by a later round of one launch, and the call's replay logic is unchanged.
     // The tail takes the fewest replicas per workgroup that still fit it in one round: when that is
     // wpw itself (more than (wpw / 2) cus replicas left), one launch does as well (measured: config 3,
-    // B = 1792, a tail at 2 per workgroup in two rounds was 14 % slower).
+    // B = 1792, a tail at 2 per workgroup in two rounds was 14 % slower).  Only workgroups of 16 waves
+    // are known to run one per CU; smaller ones may share a CU, and a split measured slower there
+    // (config 3 adaptive, B = 768: 2 replicas x 4 waves, 11.3 against 9.0 µs per step).
     const int64_t round = (int64_t)wpw * s->cus, g_main = s->G / round * round, rem = s->G - g_main;
     int wpw_t = 1;
     while (wpw_t < wpw && (rem + wpw_t - 1) / wpw_t > s->cus) wpw_t *= 2;
-    if (!s->wave_tail || wpw_t == wpw || g_main == 0 || rem == 0) return shape(wpw, tw);
+    if (!s->wave_tail || wpw * tw != 16 || wpw_t == wpw || g_main == 0 || rem == 0) return shape(wpw, tw);
     g1 = g_main;
     int rc = shape(wpw, tw);
     if (rc) return rc;
