@@ -911,8 +911,9 @@ int launch_wave(odesat_solver *s, int step0, int nsteps, bool adaptive, double d
     // One workgroup of wpw replicas per CU: the device works in rounds of wpw * cus replicas.  A partial
     // last round at the solver's shape costs a whole one (config 3, B = 1280: 320 workgroups of 4, the
     // last 64 alone in a second round -- DESIGN.md §6.3), so it runs as a launch of its own after the
-    // whole rounds, at fewer replicas per workgroup and the wider teams that leaves room for.  Replicas are independent; a STOP_ANY stop is read by the
-    // later launch as by a later round of one launch, and the call's replay logic is unchanged.
+    // whole rounds, at fewer replicas per workgroup and the wider teams that leaves room for.  Replicas
+    // are independent; a STOP_ANY stop is read by the later launch as by a later round of one launch,
+    // and the call's replay logic is unchanged.
     // The tail takes the fewest replicas per workgroup that still fit it in one round: when that is
     // wpw itself (more than (wpw / 2) cus replicas left), one launch does as well (measured: config 3,
     // B = 1792, a tail at 2 per workgroup in two rounds was 14 % slower).  Only workgroups of 16 waves
