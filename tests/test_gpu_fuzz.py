@@ -419,3 +419,28 @@ def test_fuzz_caller_states_match_oracle(seed, prec):
                 ctx = f"{name} {prec} {'adaptive' if adaptive else 'fixed'} {label} (alg {galg}) replica {b}"
                 assert r["steps_done"][b] == t and (r["first_sat_step"][b] >= 0) == sat, ctx
                 assert same(gv[b], ov) and same(gxs[b], oxs) and same(gxl[b], oxl), ctx
+
+
+# ---------------------------------------------------------- k_wave's partial-round tail launch ---
+TAIL_SEEDS = [s for s in range(SEED0, SEED0 + NSEED) if s % 6 < 3][::4]  # 3-SAT shapes (gen's k3 kind)
+
+
+@pytest.mark.parametrize("seed", TAIL_SEEDS)
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_fuzz_wave_tail_matches_single_launch(seed, adaptive):
+    """k_wave at B = 1100 (one device round plus 76 replicas where the workgroups hold 4 replicas):
+    the partial round as its own launch (the default) == the single launch (knob WAVE_TAIL = 0) bit
+    for bit -- sat steps, steps, dt and every state -- on the fuzzed 3-SAT shapes, f32, STOP_EACH."""
+    name, n, cp, var, neg = gen(seed)
+    f = cnf.CNFFormula.from_arrays(cp, var, neg, n)
+    env = {"WAVE": "1", "SOLO": "0"}
+    a = run_variant(f, 1100, "f32", env, _lib.ODESAT_ALG_RESIDENT, adaptive, 60, 20)
+    b = run_variant(f, 1100, "f32", {**env, "WAVE_TAIL": "0"}, _lib.ODESAT_ALG_RESIDENT, adaptive, 60, 20)
+    if a is None or b is None:
+        pytest.skip(f"{name}: k_wave not available")
+    (_, ra, sa), (_, rb, sb) = a, b
+    ctx = f"seed {seed} {name} adaptive={adaptive}"
+    assert np.array_equal(ra["first_sat_step"], rb["first_sat_step"]), ctx
+    assert np.array_equal(ra["steps_done"], rb["steps_done"]) and same(ra["dt"], rb["dt"]), ctx
+    for x, y in zip(sa, sb):
+        assert same(x, y), ctx
